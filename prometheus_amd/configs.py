@@ -1,0 +1,146 @@
+"""Named problem configurations in the reference's setup-file schema.
+
+The reference reads a JSON "setup file" with five sections (written by
+``pythonScripts/setup.py:554-581``, read by ``prometheus.py:56-134``); every
+value is already in cgs.  The presets below are the BASELINE.json configs
+C1..C5 plus reduced variants used for golden fixtures and
+parity tests.  They are plain dicts so the same object feeds this package's
+loader, the CPU oracle and the reference itself (fixture generator).
+"""
+from __future__ import annotations
+
+import copy
+import csv
+import os
+
+_RES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "resources")
+
+# cgs constants needed to express grids relative to the system (constants.py:19-26)
+_R_J = 7.1492e9
+_AU = 1.496e13
+_R_SUN = 6.96e10
+_KMS = 1e5
+_AMU = 1.661 * 10 ** (-24)
+_ANG = 1e-8
+
+
+def _system(name="WASP-49b"):
+    """(a, R_p, R_star) in cm from the bundled catalogue (celestialBodies.py:597-638)."""
+    stars = {}
+    with open(os.path.join(_RES, "stars.csv"), newline="") as fh:
+        for row in csv.DictReader(fh):
+            stars[row["name"]] = float(row["R_sun"]) * _R_SUN
+    with open(os.path.join(_RES, "planets.csv"), newline="") as fh:
+        for row in csv.DictReader(fh):
+            if row["name"] == name:
+                return (float(row["a_AU"]) * _AU, float(row["R_J"]) * _R_J, stars[row["hostStar"]])
+    raise KeyError(name)
+
+
+def _grids(lower_w, upper_w, res_low, res_high, width=2 * _ANG, x_steps=30, rho_steps=40,
+           phi_steps=60, orbphase_border=0.1, orbphase_steps=8, planet="WASP-49b"):
+    a, Rp, Rs = _system(planet)
+    return {"lower_w": lower_w, "upper_w": upper_w, "widthHighRes": width,
+            "resolutionLow": res_low, "resolutionHigh": res_high,
+            "x_midpoint": a, "x_border": 5. * Rp, "x_steps": x_steps,
+            "phi_steps": phi_steps, "rho_steps": rho_steps, "upper_rho": Rs,
+            "orbphase_border": orbphase_border, "orbphase_steps": orbphase_steps}
+
+
+def _fund(doppler):
+    return {"ExomoonSource": False, "DopplerPlanetRotation": False, "CLV_variations": False,
+            "RM_effect": False, "DopplerOrbitalMotion": bool(doppler)}
+
+
+def c1():
+    """barometric Na, low-res grid (mainRetrieval.py:28,33), 1 phase: CPU plumbing."""
+    return {"Fundamentals": _fund(False),
+            "Scenarios": {"barometric": {"T": 3000., "P_0": 1e4, "mu": 2.3 * _AMU}},
+            "Architecture": {"planetName": "WASP-49b"},
+            "Species": {"barometric": {"NaI": {"chi": 1e-6}}},
+            "Grids": _grids(5888e-8, 5900e-8, 5e-9, 2e-10, orbphase_border=0., orbphase_steps=1)}
+
+
+def c2():
+    """barometric Na + K, high-res grid, 8 phases (the bench workload at N=1)."""
+    return {"Fundamentals": _fund(False),
+            "Scenarios": {"barometric": {"T": 3000., "P_0": 1e4, "mu": 2.3 * _AMU}},
+            "Architecture": {"planetName": "WASP-49b"},
+            "Species": {"barometric": {"NaI": {"chi": 1e-6}, "KI": {"chi": 1e-6}}},
+            "Grids": _grids(5880e-8, 7710e-8, 1e-10, 1e-11)}
+
+
+def c3():
+    """pressure-normalised powerLaw (PowerLawAtmosphere), Na I + Ca II + Mg I, Doppler, 16 phases."""
+    return {"Fundamentals": _fund(True),
+            "Scenarios": {"powerLaw": {"q_esc": 6., "P_0": 1e-3, "T": 3000.}},
+            "Architecture": {"planetName": "WASP-49b"},
+            "Species": {"powerLaw": {"NaI": {"chi": 1e-6}, "CaII": {"chi": 1e-6},
+                                     "MgI": {"chi": 1e-6}}},
+            "Grids": _grids(2800e-8, 6000e-8, 1e-10, 1e-11, orbphase_steps=16)}
+
+
+def c4():
+    """Na torus (N=1e33, a=2 R_p, v_ej=5 km/s, sigma_v=10 km/s), Doppler, 8 phases."""
+    _, Rp, _ = _system()
+    return {"Fundamentals": _fund(True),
+            "Scenarios": {"torus": {"a_torus": 2. * Rp, "v_ej": 5. * _KMS}},
+            "Architecture": {"planetName": "WASP-49b"},
+            "Species": {"torus": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 1e33}}},
+            "Grids": _grids(5880e-8, 7710e-8, 1e-10, 1e-11)}
+
+
+def c5():
+    """hydrostatic + synthetic H2O table, 1-2 micron at 1e-10 cm (1e6 points), 32 phases."""
+    return {"Fundamentals": _fund(False),
+            "Scenarios": {"hydrostatic": {"T": 1500., "P_0": 1e5, "mu": 2.3 * _AMU}},
+            "Architecture": {"planetName": "WASP-49b"},
+            "Species": {"hydrostatic": {"H2O": {"chi": 1e-3}}},
+            "Grids": _grids(1.0e-4, 2.0e-4, 1e-10, 1e-11, orbphase_steps=32)}
+
+
+def exomoon():
+    """moon exosphere (exomoon scenario, prometheus.py:89-93), Doppler on."""
+    _, Rp, _ = _system()
+    cfg = {"Fundamentals": _fund(True),
+           "Scenarios": {"exomoon": {"q_moon": 3.34}},
+           "Architecture": {"planetName": "WASP-49b", "R_moon": 1.822e8,
+                            "a_moon": 1.44 * Rp, "starting_orbphase_moon": 0.65 * 2. * 3.141592653589793},
+           "Species": {"exomoon": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 1e32}}},
+           "Grids": _grids(5880e-8, 5910e-8, 5e-10, 1e-11, orbphase_steps=6)}
+    cfg["Fundamentals"]["ExomoonSource"] = True
+    return cfg
+
+
+PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C5": c5, "exomoon": exomoon}
+
+
+def get(name: str) -> dict:
+    return copy.deepcopy(PRESETS[name]())
+
+
+def reduced(cfg: dict, *, phi_steps=12, rho_steps=20, orbphase_steps=None,
+            res_low=None, res_high=None, lower_w=None, upper_w=None) -> dict:
+    """A spatially/spectrally reduced copy (golden fixtures and CPU-sized parity tests)."""
+    out = copy.deepcopy(cfg)
+    g = out["Grids"]
+    g["phi_steps"], g["rho_steps"] = phi_steps, rho_steps
+    if orbphase_steps is not None:
+        g["orbphase_steps"] = orbphase_steps
+    for k, v in (("resolutionLow", res_low), ("resolutionHigh", res_high),
+                 ("lower_w", lower_w), ("upper_w", upper_w)):
+        if v is not None:
+            g[k] = v
+    return out
+
+
+def fixture_configs():
+    """The reduced problems pinned by golden R vectors (tests/golden/transit_*.npz)."""
+    return {
+        "C1": c1(),
+        "C2r": reduced(c2(), orbphase_steps=4, res_low=5e-9, res_high=1e-10),
+        "C3r": reduced(c3(), orbphase_steps=4, res_low=1e-8, res_high=5e-10),
+        "C4r": reduced(c4(), orbphase_steps=4, res_low=5e-9, res_high=1e-10),
+        "C5r": reduced(c5(), orbphase_steps=3, res_low=2.5e-8),
+        "exomoon": reduced(exomoon(), orbphase_steps=4),
+    }
