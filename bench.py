@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Benchmark: spectrum points per second of the fused transit integrator on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu-baseline]
+
+N=1: the BASELINE.json configs[1] workload (C2: barometric Na + K, 190,205 wavelengths x 8
+orbital phases x 2,400 chords x 30 samples, WASP-49b).  One step = one pass of the hot path over
+the whole spectrum with all inputs resident in HBM: density + column densities + culling,
+sigma resample of every species at every phase, and the fused tau -> exp(-tau) -> disk-sum ->
+ratio kernel (prom_transit_run).
+
+N>1 (launched by torch.distributed.run, one process per GPU): weak scaling by wavelength
+sharding.  The global spectrum is the C2 grid at N-times finer resolution (resolutionLow/N,
+resolutionHigh/N: ~N x 190k wavelengths); rank r integrates the contiguous shard r of it.  No
+collective touches the data path; torch.distributed is used only for the timing barrier and the
+max-over-ranks time.
+
+Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402  (first: one HIP runtime per process, torch's; used for sync + gloo timing only)
+
+FP64_VALU_PEAK_TFLOPS = 78.6     # MI355X FP64 vector peak (AMD spec; the FP64 matrix peak is the same)
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-wavelengths", type=int, default=12288)
+    return ap.parse_args()
+
+
+def dist_env():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def global_config(name: str, world: int) -> dict:
+    from prometheus_amd import configs
+    cfg = configs.get(name)
+    if world > 1:
+        g = cfg["Grids"]
+        g["resolutionLow"] = g["resolutionLow"] / world
+        g["resolutionHigh"] = g["resolutionHigh"] / world
+    return cfg
+
+
+def kernel_flops_per_cle(n_atoms: int) -> int:
+    """Algorithmic FP64 operations per chord-wavelength evaluation of k_tau:
+    tau = sum_s N_s sigma_s (n_atoms mul + n_atoms-1 add), F_out * exp(-tau) (1 mul), += (1 add),
+    and exp counted as EXP_FLOPS (a table-driven 1-ulp FP64 exp = 11 FP64 ops)."""
+    return 2 * n_atoms + 1 + EXP_FLOPS
+
+
+EXP_FLOPS = 11
+
+
+def latest_profile_traffic():
+    """HBM bytes per k_tau launch from the committed rocprofv3 PMC summary, if present."""
+    hits = sorted(glob.glob(os.path.join(REPO, "profiles", "*k_tau_traffic*.json")))
+    if not hits:
+        return None
+    try:
+        with open(hits[-1]) as fh:
+            return json.load(fh).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg: dict, n_sample: int):
+    """The oracle (numpy restatement of the reference dataflow, single process) on a bounded sample:
+    every phase and chord of the config, the first n_sample wavelengths of the grid."""
+    from oracle import prom_oracle as O
+    scen, dop, grids = O.from_setup(cfg)
+    tabs = O.build_tables(scen, grids)
+    wav = O.simulation_wavelengths(grids, O.atomic_species(scen))
+    sel = wav[:n_sample]
+    t0 = time.perf_counter()
+    O.transit_depth(scen, dop, grids, sel, tabs)
+    dt = time.perf_counter() - t0
+    pts = len(sel) * int(grids["orbphase_steps"])
+    return {"value": pts / dt, "unit": "spectrum points/s", "cores": 1, "kind": "port",
+            "sample": "%s: all %d phases x %d chords, first %d of %d wavelengths (%d points) in %.2f s, "
+                      "single-process numpy" % (cfg.get("_name", "config"), int(grids["orbphase_steps"]),
+                                                int(grids["phi_steps"]) * int(grids["rho_steps"]), len(sel),
+                                                len(wav), pts, dt)}
+
+
+def main():
+    args = parse()
+    rank, local_rank, world = dist_env()
+    if args.gpus != world and world > 1:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811  (gloo: barrier + max-reduce of times only)
+        dist.init_process_group("gloo")
+    from prometheus_amd import _native, setupfile, gasProperties  # noqa: F401
+    _native.set_default_device(local_rank)
+
+    cfg = global_config(args.config, world)
+    cfg_name = args.config
+    t_setup = time.perf_counter()
+    tr = setupfile.build_transit(cfg)   # lambda grid + device Voigt tables on this rank's GPU
+    dev = _native.get_device(local_rank)
+    n_wav_global = len(tr.wavelength)
+    edges = np.linspace(0, n_wav_global, world + 1).round().astype(np.int64)
+    w0, w1 = int(edges[rank]), int(edges[rank + 1])
+    host = tr._host_inputs()
+    prob = tr._problem(dev, host, w0, w1, 0.0)
+    dev.transit_set(prob)
+    st = dev.transit_run(stats=True)
+    setup_s = time.perf_counter() - t_setup
+    n_orb = len(host["orb"])
+    n_pts_rank = (w1 - w0) * n_orb
+
+    have_torch_gpu = torch.cuda.is_available()
+
+    def sync():
+        dev.synchronize()
+        if have_torch_gpu:
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        dev.transit_run()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    dev.timing_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dev.transit_run()
+    sync()
+    t1 = time.perf_counter()
+    ms_runs = dev.timing_end(max_runs=args.steps)
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        pts = torch.tensor([float(n_pts_rank)], dtype=torch.float64)
+        dist.all_reduce(pts, op=dist.ReduceOp.SUM)
+        total_pts = float(pts.item())
+    else:
+        total_pts = float(n_pts_rank)
+    ms_step = elapsed / args.steps * 1e3
+    value = total_pts * args.steps / elapsed
+
+    # dominant kernel: k_tau (fused tau/exp/disk-sum), average launch duration from live hipEvents
+    tau_ms = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
+    n_atoms = prob.n_atoms
+    cle = st["chord_lambda_evals"]
+    flops = cle * kernel_flops_per_cle(n_atoms)
+    achieved_tflops = flops / (tau_ms * 1e-3) / 1e12
+    traffic = latest_profile_traffic()
+    # end-to-end (host prep + H2D + run + D2H) for reference, one call
+    t_e2e = time.perf_counter()
+    R = tr.sumOverChords(devices=[local_rank]) if world == 1 else None
+    e2e_s = time.perf_counter() - t_e2e
+    result = {
+        "metric": "spectrum points/sec (phase x wavelength)",
+        "value": value,
+        "unit": "spectrum points/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (WASP-49b catalogue system, NIST line list bundled from the reference)",
+        "config": {"workload": "%s: barometric Na I + K I, %d wavelengths x %d phases x %d chords x %d samples"
+                               % (cfg_name, n_wav_global, n_orb, len(host["y"]), len(host["x"])),
+                   "global_wavelengths": n_wav_global, "orbital_phases": n_orb,
+                   "chords_per_phase": len(host["y"]), "los_samples": len(host["x"]),
+                   "parallelism": "wavelength shards x%d (no collective)" % world},
+        "roofline": {"bound": "valu", "kernel": "k_tau", "achieved": achieved_tflops,
+                     "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tflops / FP64_VALU_PEAK_TFLOPS, "traffic": traffic,
+                     "tau_ms": tau_ms, "chord_lambda_evals": cle,
+                     "flops_per_cle": kernel_flops_per_cle(n_atoms),
+                     "exp_per_s": cle / (tau_ms * 1e-3)},
+        "stage_ms": {"density": float(np.mean(ms_runs[:, 0])) if len(ms_runs) else None,
+                     "sigma": float(np.mean(ms_runs[:, 1])) if len(ms_runs) else None,
+                     "tau": tau_ms,
+                     "total": float(np.mean(ms_runs[:, 3])) if len(ms_runs) else None},
+        "chords": {"active": st["active_chords"], "transparent": st["transparent_chords"],
+                   "blocked": st["blocked_chords"]},
+        "setup_s": setup_s,
+        "end_to_end_s": e2e_s if R is not None else None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cfgc = dict(cfg)
+        cfgc["_name"] = cfg_name
+        result["cpu_baseline"] = cpu_baseline(cfgc, args.cpu_sample_wavelengths)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result))
+
+
+if __name__ == "__main__":
+    main()

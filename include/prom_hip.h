@@ -1,0 +1,189 @@
+/*
+ * prom_hip.h -- C-ABI of libprom_hip.so, the MI355X (gfx950) transit radiative-transfer core.
+ *
+ * The reference (CrazeXD/Prometheus) is pure Python with a duck-typed plugin protocol and no
+ * FFI.  Each entry point below replaces one function (or one fused group of functions) on its
+ * per-(orbital phase, wavelength) optical-depth path; the file:line it replaces is cited next to
+ * it (paths relative to the reference tree).  A Python binding over ctypes lives in
+ * prometheus_amd/_native.py; the stub a maintainer would add to the reference is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Plain C types only: int32_t/int64_t sizes, double arrays (IEEE binary64, C order).
+ *   - Every function returns PROM_OK (0) or a negative prom_status; the message of the last failure
+ *     on a context is prom_last_error(ctx).  No exception crosses the ABI.
+ *   - Host pointers passed in are read during the call only (inputs are copied to device memory
+ *     owned by the context); output pointers are host buffers the caller owns.
+ *   - One context per device.  Calls on different contexts may run concurrently from different host
+ *     threads; a context is not re-entrant.  The library keeps no global mutable state.
+ */
+#ifndef PROM_HIP_H
+#define PROM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PROM_ABI_VERSION 1
+
+typedef struct prom_ctx prom_ctx;
+
+enum prom_status {
+  PROM_OK = 0,
+  PROM_E_ARG = -1,      /* invalid argument (shape, null pointer, unknown id/kind) */
+  PROM_E_HIP = -2,      /* HIP runtime error (device missing, launch failure, ...) */
+  PROM_E_NOMEM = -3,    /* device allocation failed */
+  PROM_E_STATE = -4     /* call out of order (e.g. prom_transit_run before prom_transit_set) */
+};
+
+/* ---- context ------------------------------------------------------------------------------- */
+int32_t prom_abi_version(void);
+int32_t prom_device_count(int32_t* count);
+int32_t prom_create(int32_t device, prom_ctx** out);
+void prom_destroy(prom_ctx* ctx);
+const char* prom_last_error(const prom_ctx* ctx);
+int32_t prom_synchronize(prom_ctx* ctx);
+
+/* ---- log-sigma lookup tables ----------------------------------------------------------------
+ * A table is the (x, log10(sigma + offset)) pair that the reference stores in an interp1d object
+ * (AtmosphericConstituent.constructLookupFunction, gasProperties.py:694-715).  Tables live in
+ * device memory, identified by an id local to the context. */
+
+/* Upload a precomputed table (x strictly as given, must be non-decreasing). */
+int32_t prom_table_upload(prom_ctx* ctx, int64_t n, const double* x, const double* log_sigma,
+                          double offset, int32_t* table_id);
+
+/* Build the table on the device: sigma(x) = sum over lines, in the given order, of
+ *   (pi e^2 / (m_e c)) f_l * voigt_profile(c/x - c/lambda_l, sigma_v/lambda_l, gamma_l)
+ * then log10(sigma + offset).  Replaces calculateVoigtProfile + constructLookupFunction
+ * (gasProperties.py:672-715); line_coef[l] = (pi e^2/(m_e c)) * f_l computed by the caller in
+ * the reference's evaluation order.  log_sigma_out (host, n) may be NULL. */
+int32_t prom_table_build_voigt(prom_ctx* ctx, int64_t n, const double* x, int32_t n_lines,
+                               const double* line_wavelength, const double* line_gamma,
+                               const double* line_coef, double sigma_v, double c_light,
+                               double offset, int32_t* table_id, double* log_sigma_out);
+
+/* sigma(x) itself (no log, no table): calculateVoigtProfile (gasProperties.py:672-692). */
+int32_t prom_voigt_sigma(prom_ctx* ctx, int64_t n, const double* x, int32_t n_lines,
+                         const double* line_wavelength, const double* line_gamma,
+                         const double* line_coef, double sigma_v, double c_light,
+                         double* sigma_out);
+
+/* out[i] = 10^(interp(targets[i], table)) - offset with numpy.interp semantics (clamping, exact
+ * node hits): n_interp_log (gasProperties.py:34-51) / AtmosphericConstituent.getSigmaAbs (:727-735). */
+int32_t prom_table_lookup(prom_ctx* ctx, int32_t table_id, int64_t n_targets, const double* targets,
+                          double* out);
+
+/* ---- molecular tables (MolecularConstituent, gasProperties.py:765-818) ----------------------
+ * Axes in the reference's units after its conversions: P [dyn cm^-2] (= p[Pa] * 10), T [K],
+ * wavelength [cm] (= 1/bin_edges reversed, increasing); log_sigma[n_p][n_t][n_w] = log10(xsec + offset)
+ * on those axes.  Lookup is trilinear in (P, T, wavelength) with RegularGridInterpolator(
+ * bounds_error=False, fill_value=log10(offset)) semantics; P is clipped below at 1e-4. */
+int32_t prom_molecular_upload(prom_ctx* ctx, int32_t n_p, const double* P, int32_t n_t, const double* T,
+                              int64_t n_w, const double* wavelength, const double* log_sigma,
+                              double offset, int32_t* table_id);
+/* getSigmaAbs: sigma[c][x][w] for P[c][x], fixed T, wavelength[c][w] (gasProperties.py:789-818). */
+int32_t prom_molecular_sigma(prom_ctx* ctx, int32_t table_id, int64_t n_chords, int32_t n_x,
+                             const double* P, double T, int64_t n_wav, const double* wavelength,
+                             double* sigma_out);
+
+/* ---- density scenarios (calculateNumberDensity, gasProperties.py:143-516) ------------------- */
+enum prom_density_kind {
+  PROM_DENSITY_BAROMETRIC = 1,  /* :143-161  p = {n_0, R, H}                                     */
+  PROM_DENSITY_HYDROSTATIC = 2, /* :185-204  p = {n_0, R, G*mu*M, k_B*T, Jeans_0}                */
+  PROM_DENSITY_POWERLAW = 3,    /* :228-244, :311-330, :356-374  p = {n_0, R, q} (planet or moon) */
+  PROM_DENSITY_TORUS = 4,       /* :491-516  p = {n_0, a_torus, 4*H_torus, H_torus}              */
+  PROM_DENSITY_TABULATED = 5    /* any other plugin: n(c, x) evaluated by the caller              */
+};
+
+typedef struct prom_density_model {
+  int32_t kind;
+  int32_t reserved;
+  double p[8];   /* scalars precomputed on the host in the reference's evaluation order */
+} prom_density_model;
+
+/* n[c][x] at chords with sky-plane coordinates (y[c], z[c]) = rho*(sin phi, cos phi) and density
+ * centre (body_x[c], body_y[c]) (the planet's or moon's getPosition at that chord's phase). */
+int32_t prom_number_density(prom_ctx* ctx, const prom_density_model* model, int32_t n_x,
+                            const double* x, int64_t n_chords, const double* y, const double* z,
+                            const double* body_x, const double* body_y, double* n_out);
+
+/* ---- the fused transit integrator (Transit.sumOverChords, gasProperties.py:1160-1258, with
+ *      Atmosphere.getLOSopticalDepth_Batch :885-956 and the density / sigma lookups inside) ----- */
+typedef struct prom_constituent {
+  int32_t table_id;      /* atomic: lookup-table id; molecular: molecular-table id */
+  int32_t is_molecule;
+  double chi;            /* mixing ratio (1.0 for exospheres) */
+} prom_constituent;
+
+typedef struct prom_scenario {
+  prom_density_model density;
+  const double* body_x;        /* [n_orb] density centre per phase (planet or moon)          */
+  const double* body_y;        /* [n_orb]                                                     */
+  const double* shift;         /* [n_orb] Doppler factor per phase (constants.py:31-45)       */
+  const double* n_tabulated;   /* TABULATED only: n[c][x] in the reference's chord order
+                                  (c = ip * n_orb + o, geometryHandler.py:202-207)            */
+  double T;                    /* molecular constituents: lookup temperature                  */
+  int32_t n_constituents;
+  int32_t reserved;
+  const prom_constituent* constituents;
+} prom_scenario;
+
+typedef struct prom_transit_problem {
+  int64_t n_wav;               /* wavelengths of this shard                                   */
+  const double* wavelength;    /* [n_wav] cm                                                  */
+  int32_t n_pr;                /* chord positions per phase = phi_steps * rho_steps           */
+  int32_t n_orb;               /* orbital phases                                              */
+  const double* chord_y;       /* [n_pr] rho sin(phi), phi-major order                        */
+  const double* chord_z;       /* [n_pr] rho cos(phi)                                         */
+  const double* chord_fout;    /* [n_pr] F_out = rho * F_star * clv (flat star)               */
+  int32_t n_x;                 /* line-of-sight samples                                       */
+  int32_t n_scenarios;
+  const double* x;             /* [n_x] cm                                                    */
+  double delta_x;
+  const double* planet_y;      /* [n_orb] planet y per phase: blocked if sqrt(dy^2+z^2) < R   */
+  double planet_R;
+  int32_t n_moons;
+  int32_t reserved;
+  const double* moon_y;        /* [n_moons][n_orb]: blocked if dy^2 + z^2 < R_m^2             */
+  const double* moon_R;        /* [n_moons]                                                   */
+  const prom_scenario* scenarios;
+  double cull_tau;             /* chords whose tau upper bound is below this are transparent
+                                  (exp(-tau) == 1 to the last ulp); <= 0 selects 2^-60       */
+} prom_transit_problem;
+
+typedef struct prom_transit_stats {
+  double ms_total;             /* device time of the last prom_transit_run (hipEvents)        */
+  double ms_density;           /* density + column-density + culling kernels                  */
+  double ms_sigma;             /* sigma resample kernel                                       */
+  double ms_tau;               /* fused tau -> exp -> disk-sum kernel                         */
+  int64_t active_chords;       /* chord-phase pairs integrated (all phases)                   */
+  int64_t transparent_chords;  /* chord-phase pairs folded in as exp(-tau) = 1                */
+  int64_t blocked_chords;
+  int64_t chord_lambda_evals;  /* active_chords * n_wav: exp evaluations of the fused kernel  */
+  int32_t tau_kernel_variant;
+  int32_t reserved;
+} prom_transit_stats;
+
+/* Copy a problem to the device (all host arrays are read during the call). */
+int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* problem);
+/* Run the integrator on the device; R stays in device memory.  stats may be NULL. */
+int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats);
+/* Copy R[n_orb][n_wav] (row-major) of the last run to a host buffer. */
+int32_t prom_transit_result(prom_ctx* ctx, double* R_out);
+/* Column densities N[s][o][ip] of the last run (atomic constituents in scenario order); testing aid. */
+int32_t prom_transit_columns(prom_ctx* ctx, double* N_out);
+
+/* Live per-run stage timing without per-run synchronisation: between prom_timing_begin and
+ * prom_timing_end every prom_transit_run records its own hipEvents on the context's stream;
+ * prom_timing_end waits for them and returns ms[run][4] = {density, sigma, tau, total} for up to
+ * max_runs runs (n_runs receives the count). */
+int32_t prom_timing_begin(prom_ctx* ctx);
+int32_t prom_timing_end(prom_ctx* ctx, int32_t max_runs, double* ms, int32_t* n_runs);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PROM_HIP_H */

@@ -1,0 +1,361 @@
+"""ctypes binding of libprom_hip.so (C-ABI declared in include/prom_hip.h).
+
+The library is built in-tree for gfx950 (``python -m prometheus_amd.build`` or
+``__graft_entry__.build()``).  There is no CPU fallback: if the library or a GPU is
+missing, every compute call raises ``NativeUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+LIB_NAME = "libprom_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+PROM_OK = 0
+STATUS = {-1: "PROM_E_ARG", -2: "PROM_E_HIP", -3: "PROM_E_NOMEM", -4: "PROM_E_STATE"}
+
+DENSITY_BAROMETRIC = 1
+DENSITY_HYDROSTATIC = 2
+DENSITY_POWERLAW = 3
+DENSITY_TORUS = 4
+DENSITY_TABULATED = 5
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP library is not built/loadable or no GPU is visible."""
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class DensityModel(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("p", C.c_double * 8)]
+
+
+class Constituent(C.Structure):
+    _fields_ = [("table_id", C.c_int32), ("is_molecule", C.c_int32), ("chi", C.c_double)]
+
+
+class Scenario(C.Structure):
+    _fields_ = [("density", DensityModel), ("body_x", _dp), ("body_y", _dp), ("shift", _dp),
+                ("n_tabulated", _dp), ("T", C.c_double), ("n_constituents", C.c_int32),
+                ("reserved", C.c_int32), ("constituents", C.POINTER(Constituent))]
+
+
+class TransitProblem(C.Structure):
+    _fields_ = [("n_wav", C.c_int64), ("wavelength", _dp), ("n_pr", C.c_int32), ("n_orb", C.c_int32),
+                ("chord_y", _dp), ("chord_z", _dp), ("chord_fout", _dp), ("n_x", C.c_int32),
+                ("n_scenarios", C.c_int32), ("x", _dp), ("delta_x", C.c_double), ("planet_y", _dp),
+                ("planet_R", C.c_double), ("n_moons", C.c_int32), ("reserved", C.c_int32),
+                ("moon_y", _dp), ("moon_R", _dp), ("scenarios", C.POINTER(Scenario)),
+                ("cull_tau", C.c_double)]
+
+
+class TransitStats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_density", C.c_double), ("ms_sigma", C.c_double),
+                ("ms_tau", C.c_double), ("active_chords", C.c_int64), ("transparent_chords", C.c_int64),
+                ("blocked_chords", C.c_int64), ("chord_lambda_evals", C.c_int64),
+                ("tau_kernel_variant", C.c_int32), ("reserved", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+# every exported symbol: name -> (restype, argtypes)
+SIGNATURES = {
+    "prom_abi_version": (C.c_int32, []),
+    "prom_device_count": (C.c_int32, [_ip]),
+    "prom_create": (C.c_int32, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "prom_destroy": (None, [C.c_void_p]),
+    "prom_last_error": (C.c_char_p, [C.c_void_p]),
+    "prom_synchronize": (C.c_int32, [C.c_void_p]),
+    "prom_table_upload": (C.c_int32, [C.c_void_p, C.c_int64, _dp, _dp, C.c_double, _ip]),
+    "prom_table_build_voigt": (C.c_int32, [C.c_void_p, C.c_int64, _dp, C.c_int32, _dp, _dp, _dp,
+                                           C.c_double, C.c_double, C.c_double, _ip, _dp]),
+    "prom_voigt_sigma": (C.c_int32, [C.c_void_p, C.c_int64, _dp, C.c_int32, _dp, _dp, _dp, C.c_double,
+                                     C.c_double, _dp]),
+    "prom_table_lookup": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int64, _dp, _dp]),
+    "prom_molecular_upload": (C.c_int32, [C.c_void_p, C.c_int32, _dp, C.c_int32, _dp, C.c_int64, _dp, _dp,
+                                          C.c_double, _ip]),
+    "prom_molecular_sigma": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, _dp, C.c_double,
+                                         C.c_int64, _dp, _dp]),
+    "prom_number_density": (C.c_int32, [C.c_void_p, C.POINTER(DensityModel), C.c_int32, _dp, C.c_int64,
+                                        _dp, _dp, _dp, _dp, _dp]),
+    "prom_transit_set": (C.c_int32, [C.c_void_p, C.POINTER(TransitProblem)]),
+    "prom_transit_run": (C.c_int32, [C.c_void_p, C.POINTER(TransitStats)]),
+    "prom_transit_result": (C.c_int32, [C.c_void_p, _dp]),
+    "prom_transit_columns": (C.c_int32, [C.c_void_p, _dp]),
+    "prom_timing_begin": (C.c_int32, [C.c_void_p]),
+    "prom_timing_end": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _ip]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: Optional[str] = None):
+    """Load (once) and type the C-ABI library.  Raises NativeUnavailable if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or os.environ.get("PROMETHEUS_AMD_LIB", LIB_PATH)
+        if not os.path.exists(p):
+            raise NativeUnavailable("%s not found: build it with `python -m prometheus_amd.build` "
+                                    "(hipcc --offload-arch=gfx950); there is no CPU fallback" % p)
+        try:
+            lib = C.CDLL(p)
+        except OSError as e:  # pragma: no cover - depends on the image
+            raise NativeUnavailable("cannot load %s: %s" % (p, e))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.prom_abi_version() != 1:
+            raise NativeUnavailable("ABI version mismatch")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = C.c_int32(0)
+    lib.prom_device_count(C.byref(n))
+    return int(n.value)
+
+
+def _d(a: np.ndarray):
+    return a.ctypes.data_as(_dp)
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Device:
+    """One prom_ctx (one GPU).  Not thread-safe; use one Device per host thread."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        n = device_count()
+        if n == 0:
+            raise NativeUnavailable("no HIP device visible (libprom_hip needs an MI355X / gfx950 GPU)")
+        h = C.c_void_p()
+        st = self.lib.prom_create(int(device), C.byref(h))
+        if st != PROM_OK:
+            raise NativeUnavailable("prom_create(%d) failed with %s" % (device, STATUS.get(st, st)))
+        self.h = h
+        self.device = int(device)
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.prom_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int, what: str):
+        if st != PROM_OK:
+            msg = self.lib.prom_last_error(self.h)
+            raise NativeError("%s: %s (%s)" % (what, STATUS.get(st, st), msg.decode() if msg else ""))
+
+    def synchronize(self):
+        self._check(self.lib.prom_synchronize(self.h), "prom_synchronize")
+
+    # ---- tables -----------------------------------------------------------------------
+    def table_upload(self, x, y, offset: float) -> int:
+        x, y = _f64(x), _f64(y)
+        tid = C.c_int32(-1)
+        self._check(self.lib.prom_table_upload(self.h, len(x), _d(x), _d(y), float(offset), C.byref(tid)),
+                    "prom_table_upload")
+        return int(tid.value)
+
+    def table_build_voigt(self, x, line_w, line_g, line_coef, sigma_v, c_light, offset, want_host=True):
+        x, lw, lg, lc = _f64(x), _f64(line_w), _f64(line_g), _f64(line_coef)
+        out = np.empty_like(x) if want_host else None
+        tid = C.c_int32(-1)
+        self._check(self.lib.prom_table_build_voigt(self.h, len(x), _d(x), len(lw), _d(lw), _d(lg), _d(lc),
+                                                    float(sigma_v), float(c_light), float(offset), C.byref(tid),
+                                                    _d(out) if out is not None else None),
+                    "prom_table_build_voigt")
+        return int(tid.value), out
+
+    def voigt_sigma(self, x, line_w, line_g, line_coef, sigma_v, c_light) -> np.ndarray:
+        x, lw, lg, lc = _f64(x), _f64(line_w), _f64(line_g), _f64(line_coef)
+        out = np.empty_like(x)
+        self._check(self.lib.prom_voigt_sigma(self.h, x.size, _d(x), len(lw), _d(lw), _d(lg), _d(lc),
+                                              float(sigma_v), float(c_light), _d(out)), "prom_voigt_sigma")
+        return out
+
+    def table_lookup(self, table_id: int, targets) -> np.ndarray:
+        t = _f64(targets)
+        out = np.empty_like(t)
+        self._check(self.lib.prom_table_lookup(self.h, int(table_id), t.size, _d(t), _d(out)),
+                    "prom_table_lookup")
+        return out
+
+    # ---- molecular ----------------------------------------------------------------------
+    def molecular_upload(self, P, T, W, V, offset) -> int:
+        P, T, W, V = _f64(P), _f64(T), _f64(W), _f64(V)
+        assert V.shape == (len(P), len(T), len(W))
+        tid = C.c_int32(-1)
+        self._check(self.lib.prom_molecular_upload(self.h, len(P), _d(P), len(T), _d(T), len(W), _d(W), _d(V),
+                                                   float(offset), C.byref(tid)), "prom_molecular_upload")
+        return int(tid.value)
+
+    def molecular_sigma(self, table_id, P, T, wav) -> np.ndarray:
+        P, wav = _f64(P), _f64(wav)
+        nc, nx = P.shape
+        assert wav.shape[0] == nc
+        nw = wav.shape[1]
+        out = np.empty((nc, nx, nw))
+        self._check(self.lib.prom_molecular_sigma(self.h, int(table_id), nc, nx, _d(P), float(T), nw, _d(wav),
+                                                  _d(out)), "prom_molecular_sigma")
+        return out
+
+    # ---- density ------------------------------------------------------------------------
+    def number_density(self, kind: int, params: Sequence[float], x, y, z, bx, by) -> np.ndarray:
+        m = DensityModel()
+        m.kind = int(kind)
+        for i, v in enumerate(params):
+            m.p[i] = float(v)
+        x, y, z, bx, by = _f64(x), _f64(y), _f64(z), _f64(bx), _f64(by)
+        out = np.empty((len(y), len(x)))
+        self._check(self.lib.prom_number_density(self.h, C.byref(m), len(x), _d(x), len(y), _d(y), _d(z), _d(bx),
+                                                 _d(by), _d(out)), "prom_number_density")
+        return out
+
+    # ---- transit ------------------------------------------------------------------------
+    def transit_set(self, prob: "TransitInputs"):
+        self._keep = prob.keepalive
+        self._check(self.lib.prom_transit_set(self.h, C.byref(prob.struct)), "prom_transit_set")
+        self._shape = (prob.struct.n_orb, prob.struct.n_wav)
+        self._n_atoms = prob.n_atoms
+        self._n_pr = prob.struct.n_pr
+
+    def transit_run(self, stats: bool = False):
+        st = TransitStats() if stats else None
+        self._check(self.lib.prom_transit_run(self.h, C.byref(st) if st is not None else None), "prom_transit_run")
+        return st.as_dict() if st is not None else None
+
+    def transit_result(self) -> np.ndarray:
+        out = np.empty(self._shape)
+        self._check(self.lib.prom_transit_result(self.h, _d(out)), "prom_transit_result")
+        return out
+
+    def timing_begin(self):
+        self._check(self.lib.prom_timing_begin(self.h), "prom_timing_begin")
+
+    def timing_end(self, max_runs: int = 4096) -> np.ndarray:
+        """ms[run] = (density, sigma, tau, total) of every run since timing_begin (live hipEvents)."""
+        ms = np.zeros((max_runs, 4))
+        n = C.c_int32(0)
+        self._check(self.lib.prom_timing_end(self.h, max_runs, _d(ms), C.byref(n)), "prom_timing_end")
+        return ms[:min(int(n.value), max_runs)]
+
+    def transit_columns(self) -> np.ndarray:
+        out = np.empty((self._n_atoms, self._shape[0], self._n_pr))
+        self._check(self.lib.prom_transit_columns(self.h, _d(out)), "prom_transit_columns")
+        return out
+
+
+class TransitInputs:
+    """Owns the numpy arrays behind one prom_transit_problem (kept alive while in use)."""
+
+    def __init__(self, *, wavelength, chord_y, chord_z, chord_fout, n_orb, x, delta_x, planet_y, planet_R,
+                 moon_y, moon_R, scenarios, cull_tau=0.0):
+        keep = []
+
+        def arr(a):
+            a = _f64(a)
+            keep.append(a)
+            return a
+
+        s = TransitProblem()
+        w = arr(wavelength)
+        s.n_wav, s.wavelength = len(w), _d(w)
+        cy, cz, cf = arr(chord_y), arr(chord_z), arr(chord_fout)
+        s.n_pr, s.chord_y, s.chord_z, s.chord_fout = len(cy), _d(cy), _d(cz), _d(cf)
+        s.n_orb = int(n_orb)
+        xx = arr(x)
+        s.n_x, s.x, s.delta_x = len(xx), _d(xx), float(delta_x)
+        py = arr(planet_y)
+        s.planet_y, s.planet_R = _d(py), float(planet_R)
+        s.n_moons = len(moon_R)
+        my, mr = arr(np.reshape(moon_y, (-1,)) if len(moon_R) else np.zeros(1)), arr(moon_R if len(moon_R) else np.zeros(1))
+        s.moon_y, s.moon_R = _d(my), _d(mr)
+        scs = (Scenario * len(scenarios))()
+        n_atoms = 0
+        for i, sc in enumerate(scenarios):
+            d = scs[i]
+            d.density.kind = int(sc["kind"])
+            for j, v in enumerate(sc.get("params", ())):
+                d.density.p[j] = float(v)
+            if sc.get("body_x") is not None:
+                d.body_x, d.body_y = _d(arr(sc["body_x"])), _d(arr(sc["body_y"]))
+            d.shift = _d(arr(sc["shift"]))
+            if sc.get("n_tabulated") is not None:
+                d.n_tabulated = _d(arr(sc["n_tabulated"]))
+            d.T = float(sc.get("T", 0.0))
+            cons = sc["constituents"]
+            ca = (Constituent * max(1, len(cons)))()
+            for k, c in enumerate(cons):
+                ca[k].table_id = int(c["table_id"])
+                ca[k].is_molecule = int(bool(c.get("is_molecule", False)))
+                ca[k].chi = float(c["chi"])
+                n_atoms += 0 if c.get("is_molecule", False) else 1
+            keep.append(ca)
+            d.n_constituents = len(cons)
+            d.constituents = ca
+        keep.append(scs)
+        s.n_scenarios = len(scenarios)
+        s.scenarios = scs
+        s.cull_tau = float(cull_tau)
+        self.struct = s
+        self.keepalive = keep
+        self.n_atoms = n_atoms
+
+
+_default_device = int(os.environ.get("PROMETHEUS_DEVICE", "0"))
+
+
+def set_default_device(device: int) -> None:
+    """GPU used by calls that do not name one (table builds, plugin methods)."""
+    global _default_device
+    _default_device = int(device)
+
+
+def default_device() -> int:
+    return _default_device
+
+
+_ctx_lock = threading.Lock()
+_contexts: Dict[int, Device] = {}
+
+
+def get_device(device: int = 0) -> Device:
+    """Process-wide context of one GPU.  Serialise use with ``dev.lock`` (one host thread per
+    device at a time; different devices run concurrently, ctypes drops the GIL)."""
+    key = int(device)
+    with _ctx_lock:
+        d = _contexts.get(key)
+        if d is None:
+            d = Device(device)
+            d.lock = threading.RLock()
+            _contexts[key] = d
+        return d

@@ -1,0 +1,44 @@
+"""Build libprom_hip.so in-tree for gfx950:  python -m prometheus_amd.build [-v]"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SOURCES = ["csrc/prom_api.hip", "csrc/prom_kernels.hip"]
+HEADERS = ["csrc/prom_internal.h", "csrc/faddeeva.h", "../include/prom_hip.h"]
+OUT = os.path.join(HERE, "libprom_hip.so")
+ARCH = os.environ.get("PROM_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=" + ARCH, "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
+         "-Wno-unused-function"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(os.path.join(HERE, f)) <= t for f in SOURCES + HEADERS + ["build.py"])
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return OUT
+    cmd = [hipcc()] + FLAGS + ["-o", OUT + ".tmp"] + [os.path.join(HERE, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=HERE)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="-f" in sys.argv, verbose="-v" in sys.argv))

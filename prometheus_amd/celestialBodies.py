@@ -1,0 +1,153 @@
+"""Star, planet, moon and the bundled system catalogue (mirrors ``pythonScripts/celestialBodies.py``).
+
+Orbital geometry is evaluated on the host with numpy: it is O(n_orbphase) scalar work (positions
+and line-of-sight velocities per phase) that feeds the device kernels, and keeping numpy here makes
+those per-phase scalars bit-identical to the reference.  The O(chords x samples) distance fields
+(``getDistanceFromPlanet`` etc.) are kept for user-written density plugins; the built-in scenarios
+evaluate them on the GPU instead (``prom_number_density`` / the fused transit kernel).
+"""
+from __future__ import annotations
+
+import csv
+import os
+from typing import Any, Optional, Tuple
+
+import numpy as np
+
+from . import constants as const
+from . import geometryHandler as geom
+
+_RES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "resources")
+
+
+class Star:
+    """Host star: radius/mass [cgs], CLV coefficients, rotation (celestialBodies.py:26-95)."""
+
+    def __init__(self, R: float, dR: float, M: float, dM: float, T_eff: float, dT_eff: float, log_g: float,
+                 dlog_g: float, Z: float, dZ: float, alpha: float) -> None:
+        self.R, self.dR, self.M, self.dM = R, dR, M, dM
+        self.T_eff, self.dT_eff, self.log_g, self.dlog_g = T_eff, dT_eff, log_g, dlog_g
+        self.Z, self.dZ, self.alpha = Z, dZ, alpha
+        self.CLV_u1 = 0.
+        self.CLV_u2 = 0.
+        self.vsiniStarrot = 0.
+        self.phiStarrot = 0.
+        self.Fstar_function = None
+
+    def addCLVparameters(self, CLV_u1: float, CLV_u2: float) -> None:
+        self.CLV_u1, self.CLV_u2 = CLV_u1, CLV_u2
+
+    def addRMparameters(self, vsiniStarrot: float, phiStarrot: float) -> None:
+        self.vsiniStarrot, self.phiStarrot = vsiniStarrot, phiStarrot
+
+    def getSurfaceVelocity(self, phi, rho):
+        return self.vsiniStarrot * rho / self.R * np.cos(phi - self.phiStarrot)
+
+    def calculateCLV(self, rho):
+        arg = 1. - np.sqrt(1. - rho ** 2 / self.R ** 2)
+        return 1. - self.CLV_u1 * arg - self.CLV_u2 * arg ** 2
+
+    def getSpectrum(self):
+        raise NotImplementedError("PHOENIX spectra are fetched over FTP by the reference "
+                                  "(celestialBodies.py:128-209); this build has no network and does not "
+                                  "ship them (out of scope, SURVEY.md §8f rank 2)")
+
+    def addFstarFunction(self, wavelength) -> None:
+        self.getSpectrum()
+
+
+class Planet:
+    """Planet on a circular, edge-on orbit (celestialBodies.py:335-470)."""
+
+    def __init__(self, name: str, R: float, M: float, a: float, hostStar: Star, transitDuration: float,
+                 orbitalPeriod: float, b: float) -> None:
+        self.name, self.R, self.M, self.a, self.hostStar = name, R, M, a, hostStar
+        self.transitDuration, self.orbitalPeriod, self.b = transitDuration, orbitalPeriod, b
+
+    def getPosition(self, orbphase) -> Tuple[Any, Any]:
+        return self.a * np.cos(orbphase), self.a * np.sin(orbphase)
+
+    def getLOSvelocity(self, orbphase):
+        return -np.sin(orbphase) * np.sqrt(const.G * self.hostStar.M / self.a)
+
+    def getDistanceFromPlanet(self, x, phi, rho, orbphase):
+        y, z = geom.Grid.getCartesianFromCylinder(phi, rho)
+        xp, yp = self.getPosition(orbphase)
+        x_, xp_, yp_, y_, z_ = _batch(x, xp, yp, y, z)
+        return np.sqrt((x_ - xp_) ** 2 + (y_ - yp_) ** 2 + z_ ** 2)
+
+    def getTorusCoords(self, x, phi, rho, orbphase):
+        y, z = geom.Grid.getCartesianFromCylinder(phi, rho)
+        xp, yp = self.getPosition(orbphase)
+        x_, xp_, yp_, y_, z_ = _batch(x, xp, yp, y, z)
+        return np.sqrt((x_ - xp_) ** 2 + (y_ - yp_) ** 2), z_
+
+
+class Moon:
+    """Moon on a circular orbit around its planet (celestialBodies.py:473-583)."""
+
+    def __init__(self, midTransitOrbphase: float, R: float, a: float, hostPlanet: Planet) -> None:
+        self.midTransitOrbphase, self.R, self.a, self.hostPlanet = midTransitOrbphase, R, a, hostPlanet
+
+    def getOrbphase(self, orbphase):
+        p = self.hostPlanet
+        ratio = np.sqrt((np.float64(p.a) ** 3 * np.float64(p.M)) /
+                        (np.float64(self.a) ** 3 * np.float64(p.hostStar.M)))
+        return self.midTransitOrbphase + np.float64(orbphase) * ratio
+
+    def getPosition(self, orbphase):
+        om = self.getOrbphase(orbphase)
+        xp, yp = self.hostPlanet.getPosition(orbphase)
+        return xp + self.a * np.cos(om), yp + self.a * np.sin(om)
+
+    def getLOSvelocity(self, orbphase):
+        vp = self.hostPlanet.getLOSvelocity(orbphase)
+        return vp - np.sin(self.getOrbphase(orbphase)) * np.sqrt(const.G * self.hostPlanet.M / self.a)
+
+    def getDistanceFromMoon(self, x, phi, rho, orbphase):
+        y, z = geom.Grid.getCartesianFromCylinder(phi, rho)
+        xm, ym = self.getPosition(orbphase)
+        x_, xm_, ym_, y_, z_ = _batch(x, xm, ym, y, z)
+        return np.sqrt((x_ - xm_) ** 2 + (y_ - ym_) ** 2 + z_ ** 2)
+
+
+def _batch(x, bx, by, y, z):
+    """Scalar chord -> (n_x,); arrays of chords -> (n_chords, n_x) (celestialBodies.py:421-435)."""
+    x, bx, by, y, z = (np.asarray(v) for v in (x, bx, by, y, z))
+    if bx.ndim > 0:
+        return x[np.newaxis, :], bx[:, np.newaxis], by[:, np.newaxis], y[:, np.newaxis], z[:, np.newaxis]
+    return x, bx, by, y, z
+
+
+class AvailablePlanets:
+    """Systems from the bundled ``resources/stars.csv`` and ``planets.csv`` (celestialBodies.py:586-664)."""
+
+    def __init__(self) -> None:
+        self.stars = {}
+        with open(os.path.join(_RES, "stars.csv"), newline="") as fh:
+            for row in csv.DictReader(fh):
+                f = {k: float(v) for k, v in row.items() if k != "name"}
+                self.stars[row["name"]] = Star(f["R_sun"] * const.R_sun, f["dR_sun"] * const.R_sun,
+                                               f["M_sun"] * const.M_sun, f["dM_sun"] * const.M_sun, f["T_eff"],
+                                               f["dT_eff"], f["log_g"], f["dlog_g"], f["Fe_H"], f["dFe_H"], 0)
+        self.planetList = []
+        with open(os.path.join(_RES, "planets.csv"), newline="") as fh:
+            for row in csv.DictReader(fh):
+                star = self.stars.get(row["hostStar"])
+                if star is None:
+                    print(f"Warning: Host star {row['hostStar']} not found for planet {row['name']}")
+                    continue
+                self.planetList.append(Planet(row["name"], float(row["R_J"]) * const.R_J,
+                                              float(row["M_J"]) * const.M_J, float(row["a_AU"]) * const.AU, star,
+                                              float(row["transitDuration"]), float(row["P"]),
+                                              float(row["b"]) * star.R))
+
+    def listPlanetNames(self):
+        return [p.name for p in self.planetList]
+
+    def findPlanet(self, namePlanet: str) -> Optional[Planet]:
+        for p in self.planetList:
+            if p.name == namePlanet:
+                return p
+        print('System', namePlanet, 'was not found.')
+        return None

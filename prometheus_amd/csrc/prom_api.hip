@@ -1,0 +1,459 @@
+// C-ABI layer of libprom_hip.so (declared in include/prom_hip.h).  Host code only: argument checks,
+// device memory owned by the context, H2D/D2H copies and kernel launches on the context's stream.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <exception>
+
+#include "prom_internal.h"
+
+using prom::DevBuf;
+using prom::Error;
+
+namespace {
+
+template <class F>
+int32_t guarded(prom_ctx* ctx, F&& f) {
+  if (!ctx) return PROM_E_ARG;
+  try {
+    PROM_HIP(hipSetDevice(ctx->device));
+    f();
+    ctx->err.clear();
+    return PROM_OK;
+  } catch (const Error& e) {
+    ctx->err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    ctx->err = e.what();
+    return PROM_E_HIP;
+  }
+}
+
+template <class T>
+void upload(DevBuf& b, const T* h, int64_t n, hipStream_t s) {
+  b.ensure(sizeof(T) * (size_t)std::max<int64_t>(n, 1));
+  if (n > 0) PROM_HIP(hipMemcpyAsync(b.p, h, sizeof(T) * (size_t)n, hipMemcpyHostToDevice, s));
+}
+
+template <class T>
+void download(T* h, const DevBuf& b, int64_t n, hipStream_t s) {
+  if (n > 0) PROM_HIP(hipMemcpyAsync(h, b.p, sizeof(T) * (size_t)n, hipMemcpyDeviceToHost, s));
+}
+
+prom::DensityDev to_dev(const prom_density_model& m) {
+  prom::DensityDev d{};
+  d.kind = m.kind;
+  for (int i = 0; i < 8; ++i) d.p[i] = m.p[i];
+  return d;
+}
+
+bool valid_kind(int32_t k) { return k >= PROM_DENSITY_BAROMETRIC && k <= PROM_DENSITY_TABULATED; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t prom_abi_version(void) { return PROM_ABI_VERSION; }
+
+int32_t prom_device_count(int32_t* count) {
+  if (!count) return PROM_E_ARG;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return PROM_OK;
+}
+
+int32_t prom_create(int32_t device, prom_ctx** out) {
+  if (!out) return PROM_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return PROM_E_HIP;
+  prom_ctx* ctx = new (std::nothrow) prom_ctx();
+  if (!ctx) return PROM_E_NOMEM;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return PROM_E_HIP;
+  }
+  for (auto& e : ctx->ev) {
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete ctx;
+      return PROM_E_HIP;
+    }
+  }
+  *out = ctx;
+  return PROM_OK;
+}
+
+void prom_destroy(prom_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->tev) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;  // DevBuf destructors free device memory
+}
+
+const char* prom_last_error(const prom_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int32_t prom_synchronize(prom_ctx* ctx) {
+  return guarded(ctx, [&] { PROM_HIP(hipStreamSynchronize(ctx->stream)); });
+}
+
+// ------------------------------------------------------------------------------ tables
+int32_t prom_table_upload(prom_ctx* ctx, int64_t n, const double* x, const double* log_sigma,
+                          double offset, int32_t* table_id) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(n >= 1 && x && log_sigma && table_id, "prom_table_upload: bad arguments");
+    for (int64_t i = 1; i < n; ++i) PROM_REQUIRE(!(x[i] < x[i - 1]), "prom_table_upload: x must be non-decreasing");
+    prom::AtomTable t;
+    upload(t.x, x, n, ctx->stream);
+    upload(t.y, log_sigma, n, ctx->stream);
+    t.n = n;
+    t.offset = offset;
+    double m = -INFINITY;
+    for (int64_t i = 0; i < n; ++i) m = std::max(m, log_sigma[i]);
+    t.ymax = m;
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->tables.push_back(std::move(t));
+    *table_id = (int32_t)ctx->tables.size() - 1;
+  });
+}
+
+static void voigt_common(prom_ctx* ctx, int64_t n, const double* x, int32_t n_lines, const double* lw,
+                         const double* lg, const double* lc, DevBuf& dx) {
+  PROM_REQUIRE(n >= 0 && (n == 0 || x) && n_lines >= 0 && (n_lines == 0 || (lw && lg && lc)),
+               "voigt: bad arguments");
+  upload(dx, x, n, ctx->stream);
+  upload(ctx->scratch[1], lw, n_lines, ctx->stream);
+  upload(ctx->scratch[2], lg, n_lines, ctx->stream);
+  upload(ctx->scratch[3], lc, n_lines, ctx->stream);
+}
+
+int32_t prom_table_build_voigt(prom_ctx* ctx, int64_t n, const double* x, int32_t n_lines,
+                               const double* line_wavelength, const double* line_gamma,
+                               const double* line_coef, double sigma_v, double c_light,
+                               double offset, int32_t* table_id, double* log_sigma_out) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(n >= 1 && table_id, "prom_table_build_voigt: bad arguments");
+    for (int64_t i = 1; i < n; ++i) PROM_REQUIRE(!(x[i] < x[i - 1]), "prom_table_build_voigt: x must be non-decreasing");
+    prom::AtomTable t;
+    voigt_common(ctx, n, x, n_lines, line_wavelength, line_gamma, line_coef, t.x);
+    t.y.ensure(sizeof(double) * n);
+    prom::launch_voigt(ctx->stream, t.x.as<double>(), n, ctx->scratch[1].as<double>(),
+                       ctx->scratch[2].as<double>(), ctx->scratch[3].as<double>(), n_lines, sigma_v, c_light,
+                       offset, 1, t.y.as<double>());
+    ctx->scratch[4].ensure(sizeof(double));
+    t.ymax = prom::reduce_max(ctx->stream, t.y.as<double>(), n, ctx->scratch[4].as<double>());
+    t.n = n;
+    t.offset = offset;
+    if (log_sigma_out) {
+      download(log_sigma_out, t.y, n, ctx->stream);
+      PROM_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    ctx->tables.push_back(std::move(t));
+    *table_id = (int32_t)ctx->tables.size() - 1;
+  });
+}
+
+int32_t prom_voigt_sigma(prom_ctx* ctx, int64_t n, const double* x, int32_t n_lines,
+                         const double* line_wavelength, const double* line_gamma,
+                         const double* line_coef, double sigma_v, double c_light, double* sigma_out) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(sigma_out || n == 0, "prom_voigt_sigma: bad arguments");
+    voigt_common(ctx, n, x, n_lines, line_wavelength, line_gamma, line_coef, ctx->scratch[0]);
+    ctx->scratch[4].ensure(sizeof(double) * std::max<int64_t>(n, 1));
+    prom::launch_voigt(ctx->stream, ctx->scratch[0].as<double>(), n, ctx->scratch[1].as<double>(),
+                       ctx->scratch[2].as<double>(), ctx->scratch[3].as<double>(), n_lines, sigma_v, c_light,
+                       0.0, 0, ctx->scratch[4].as<double>());
+    download(sigma_out, ctx->scratch[4], n, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int32_t prom_table_lookup(prom_ctx* ctx, int32_t table_id, int64_t n_targets, const double* targets,
+                          double* out) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(table_id >= 0 && table_id < (int32_t)ctx->tables.size(), "prom_table_lookup: unknown table");
+    PROM_REQUIRE(n_targets >= 0 && (n_targets == 0 || (targets && out)), "prom_table_lookup: bad arguments");
+    const prom::AtomTable& t = ctx->tables[table_id];
+    upload(ctx->scratch[0], targets, n_targets, ctx->stream);
+    ctx->scratch[1].ensure(sizeof(double) * std::max<int64_t>(n_targets, 1));
+    prom::launch_table_lookup(ctx->stream, t.x.as<double>(), t.y.as<double>(), t.n, t.offset,
+                              ctx->scratch[0].as<double>(), n_targets, ctx->scratch[1].as<double>());
+    download(out, ctx->scratch[1], n_targets, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+// ------------------------------------------------------------------------------ molecular
+int32_t prom_molecular_upload(prom_ctx* ctx, int32_t n_p, const double* P, int32_t n_t, const double* T,
+                              int64_t n_w, const double* wavelength, const double* log_sigma,
+                              double offset, int32_t* table_id) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(n_p >= 2 && n_t >= 2 && n_w >= 2 && P && T && wavelength && log_sigma && table_id,
+                 "prom_molecular_upload: bad arguments (each axis needs >= 2 nodes)");
+    prom::MolTable t;
+    upload(t.P, P, n_p, ctx->stream);
+    upload(t.T, T, n_t, ctx->stream);
+    upload(t.W, wavelength, n_w, ctx->stream);
+    const int64_t nv = (int64_t)n_p * n_t * n_w;
+    upload(t.V, log_sigma, nv, ctx->stream);
+    t.n_p = n_p;
+    t.n_t = n_t;
+    t.n_w = n_w;
+    t.offset = offset;
+    double m = -INFINITY;
+    for (int64_t i = 0; i < nv; ++i) m = std::max(m, log_sigma[i]);
+    t.vmax = m;
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->mtables.push_back(std::move(t));
+    *table_id = (int32_t)ctx->mtables.size() - 1;
+  });
+}
+
+int32_t prom_molecular_sigma(prom_ctx* ctx, int32_t table_id, int64_t n_chords, int32_t n_x,
+                             const double* P, double T, int64_t n_wav, const double* wavelength,
+                             double* sigma_out) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(table_id >= 0 && table_id < (int32_t)ctx->mtables.size(), "prom_molecular_sigma: unknown table");
+    PROM_REQUIRE(n_chords >= 0 && n_x >= 0 && n_wav >= 0, "prom_molecular_sigma: bad sizes");
+    const int64_t tot = n_chords * n_x * n_wav;
+    upload(ctx->scratch[0], P, n_chords * n_x, ctx->stream);
+    upload(ctx->scratch[1], wavelength, n_chords * n_wav, ctx->stream);
+    ctx->scratch[2].ensure(sizeof(double) * std::max<int64_t>(tot, 1));
+    prom::launch_molecular_sigma(ctx->stream, ctx->mtables[table_id], n_chords, n_x, ctx->scratch[0].as<double>(),
+                                 T, n_wav, ctx->scratch[1].as<double>(), ctx->scratch[2].as<double>());
+    download(sigma_out, ctx->scratch[2], tot, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+// ------------------------------------------------------------------------------ density
+int32_t prom_number_density(prom_ctx* ctx, const prom_density_model* model, int32_t n_x, const double* x,
+                            int64_t n_chords, const double* y, const double* z, const double* body_x,
+                            const double* body_y, double* n_out) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(model && valid_kind(model->kind) && model->kind != PROM_DENSITY_TABULATED,
+                 "prom_number_density: unknown or tabulated density kind");
+    PROM_REQUIRE(n_x >= 0 && n_chords >= 0, "prom_number_density: bad sizes");
+    upload(ctx->scratch[0], x, n_x, ctx->stream);
+    upload(ctx->scratch[1], y, n_chords, ctx->stream);
+    upload(ctx->scratch[2], z, n_chords, ctx->stream);
+    upload(ctx->scratch[3], body_x, n_chords, ctx->stream);
+    upload(ctx->scratch[4], body_y, n_chords, ctx->stream);
+    ctx->scratch[5].ensure(sizeof(double) * std::max<int64_t>(n_chords * n_x, 1));
+    prom::launch_density(ctx->stream, to_dev(*model), ctx->scratch[0].as<double>(), n_x,
+                         ctx->scratch[1].as<double>(), ctx->scratch[2].as<double>(), ctx->scratch[3].as<double>(),
+                         ctx->scratch[4].as<double>(), n_chords, ctx->scratch[5].as<double>());
+    download(n_out, ctx->scratch[5], n_chords * n_x, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+// ------------------------------------------------------------------------------ transit
+int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(pb, "prom_transit_set: null problem");
+    prom::TransitDev& tr = ctx->tr;
+    tr.ready = false;
+    tr.ran = false;
+    PROM_REQUIRE(pb->n_wav >= 1 && pb->wavelength, "transit: need >= 1 wavelength");
+    PROM_REQUIRE(pb->n_pr >= 1 && pb->n_orb >= 1 && pb->chord_y && pb->chord_z && pb->chord_fout,
+                 "transit: need chords and phases");
+    PROM_REQUIRE(pb->n_x >= 1 && pb->x, "transit: need line-of-sight samples");
+    PROM_REQUIRE(pb->planet_y, "transit: planet_y missing");
+    PROM_REQUIRE(pb->n_moons >= 0 && (pb->n_moons == 0 || (pb->moon_y && pb->moon_R)), "transit: moons");
+    PROM_REQUIRE(pb->n_scenarios >= 1 && pb->scenarios, "transit: need >= 1 density scenario");
+    PROM_REQUIRE(pb->n_wav <= ((int64_t)65535 << 8), "transit: n_wav too large for one shard");
+    tr.n_wav = pb->n_wav;
+    tr.n_pr = pb->n_pr;
+    tr.n_orb = pb->n_orb;
+    tr.n_x = pb->n_x;
+    tr.n_sc = pb->n_scenarios;
+    tr.n_moons = pb->n_moons;
+    tr.delta_x = pb->delta_x;
+    tr.planet_R = pb->planet_R;
+    tr.cull_tau = pb->cull_tau > 0.0 ? pb->cull_tau : std::ldexp(1.0, -60);
+    tr.terms.clear();
+    tr.dens.clear();
+    tr.atom_sigma_max.clear();
+    tr.tab_off.assign(tr.n_sc, -1);
+    const hipStream_t s = ctx->stream;
+    const int64_t n_orb = tr.n_orb;
+    std::vector<double> bx(tr.n_sc * n_orb), by(tr.n_sc * n_orb), sh(tr.n_sc * n_orb);
+    int64_t tab_total = 0;
+    int32_t n_atoms = 0, n_mol = 0;
+    for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
+      const prom_scenario& S = pb->scenarios[sc];
+      PROM_REQUIRE(valid_kind(S.density.kind), "transit: unknown density kind");
+      tr.dens.push_back(to_dev(S.density));
+      PROM_REQUIRE(S.shift, "transit: scenario shift[] missing");
+      if (S.density.kind == PROM_DENSITY_TABULATED) {
+        PROM_REQUIRE(S.n_tabulated, "transit: tabulated scenario without n_tabulated");
+        tr.tab_off[sc] = tab_total;
+        tab_total += n_orb * tr.n_pr * tr.n_x;
+      } else {
+        PROM_REQUIRE(S.body_x && S.body_y, "transit: scenario body position missing");
+      }
+      for (int64_t o = 0; o < n_orb; ++o) {
+        bx[sc * n_orb + o] = S.body_x ? S.body_x[o] : 0.0;
+        by[sc * n_orb + o] = S.body_y ? S.body_y[o] : 0.0;
+        sh[sc * n_orb + o] = S.shift[o];
+      }
+      PROM_REQUIRE(S.n_constituents >= 0 && (S.n_constituents == 0 || S.constituents), "transit: constituents");
+      for (int32_t k = 0; k < S.n_constituents; ++k) {
+        const prom_constituent& C = S.constituents[k];
+        prom::TermDev t{};
+        t.scenario = sc;
+        t.is_molecule = C.is_molecule ? 1 : 0;
+        t.table = C.table_id;
+        t.chi = C.chi;
+        if (t.is_molecule) {
+          PROM_REQUIRE(false, "transit: molecular constituents need the molecular fused kernel "
+                              "(not in this build); use prom_molecular_sigma");
+          t.slot = n_mol++;
+        } else {
+          PROM_REQUIRE(C.table_id >= 0 && C.table_id < (int32_t)ctx->tables.size(), "transit: unknown table id");
+          t.slot = n_atoms++;
+          const prom::AtomTable& tb = ctx->tables[C.table_id];
+          tr.atom_sigma_max.push_back((std::pow(10.0, tb.ymax) - tb.offset) * (1.0 + 1e-9));
+        }
+        tr.terms.push_back(t);
+      }
+    }
+    tr.n_atoms = n_atoms;
+    tr.n_mol = n_mol;
+    tr.n_terms = (int32_t)tr.terms.size();
+    // uploads
+    upload(tr.wav, pb->wavelength, tr.n_wav, s);
+    upload(tr.cy, pb->chord_y, tr.n_pr, s);
+    upload(tr.cz, pb->chord_z, tr.n_pr, s);
+    upload(tr.cfout, pb->chord_fout, tr.n_pr, s);
+    upload(tr.x, pb->x, tr.n_x, s);
+    upload(tr.planet_y, pb->planet_y, n_orb, s);
+    upload(tr.moon_y, pb->moon_y, (int64_t)tr.n_moons * n_orb, s);
+    upload(tr.moon_R, pb->moon_R, tr.n_moons, s);
+    upload(tr.body_x, bx.data(), (int64_t)bx.size(), s);
+    upload(tr.body_y, by.data(), (int64_t)by.size(), s);
+    upload(tr.shift, sh.data(), (int64_t)sh.size(), s);
+    upload(tr.terms_dev, tr.terms.data(), (int64_t)tr.terms.size(), s);
+    upload(tr.sigma_max_dev, tr.atom_sigma_max.data(), (int64_t)tr.atom_sigma_max.size(), s);
+    tr.tab.ensure(sizeof(double) * std::max<int64_t>(tab_total, 1));
+    for (int32_t sc = 0; sc < tr.n_sc; ++sc)
+      if (tr.tab_off[sc] >= 0)
+        PROM_HIP(hipMemcpyAsync(tr.tab.as<double>() + tr.tab_off[sc], pb->scenarios[sc].n_tabulated,
+                                sizeof(double) * n_orb * tr.n_pr * tr.n_x, hipMemcpyHostToDevice, s));
+    // work buffers
+    const int64_t nc = n_orb * tr.n_pr;
+    tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
+    tr.ncol.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * nc);
+    tr.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
+    tr.flags.ensure(sizeof(int32_t) * nc);
+    tr.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
+    tr.act_ip.ensure(sizeof(int32_t) * nc);
+    tr.counts.ensure(sizeof(int32_t) * n_orb * 3);
+    tr.tsum.ensure(sizeof(double) * n_orb);
+    tr.fsum.ensure(sizeof(double) * n_orb);
+    tr.sigma.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * n_orb * tr.n_wav);
+    tr.R.ensure(sizeof(double) * n_orb * tr.n_wav);
+    PROM_HIP(hipStreamSynchronize(s));
+    tr.ready = true;
+  });
+}
+
+int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
+  return guarded(ctx, [&] {
+    prom::TransitDev& tr = ctx->tr;
+    if (!tr.ready) throw Error(PROM_E_STATE, "prom_transit_run: call prom_transit_set first");
+    int variant = 0;
+    hipEvent_t* ev = ctx->ev;
+    if (ctx->timing) {
+      const size_t need = 4 * (size_t)(ctx->timed_runs + 1);
+      while (ctx->tev.size() < need) {
+        hipEvent_t e;
+        PROM_HIP(hipEventCreate(&e));
+        ctx->tev.push_back(e);
+      }
+      ev = &ctx->tev[4 * (size_t)ctx->timed_runs];
+      ++ctx->timed_runs;
+    }
+    prom::launch_transit(ctx->stream, tr, ctx->tables, ctx->mtables, ev, &variant);
+
+    tr.ran = true;
+    if (stats) {
+      std::memset(stats, 0, sizeof(*stats));
+      PROM_HIP(hipEventSynchronize(ev[3]));
+      float a = 0, b = 0, c = 0, t = 0;
+      PROM_HIP(hipEventElapsedTime(&a, ev[0], ev[1]));
+      PROM_HIP(hipEventElapsedTime(&b, ev[1], ev[2]));
+      PROM_HIP(hipEventElapsedTime(&c, ev[2], ev[3]));
+      PROM_HIP(hipEventElapsedTime(&t, ev[0], ev[3]));
+      stats->ms_density = a;
+      stats->ms_sigma = b;
+      stats->ms_tau = c;
+      stats->ms_total = t;
+      std::vector<int32_t> cnt(tr.n_orb * 3);
+      download(cnt.data(), tr.counts, (int64_t)cnt.size(), ctx->stream);
+      PROM_HIP(hipStreamSynchronize(ctx->stream));
+      for (int32_t o = 0; o < tr.n_orb; ++o) {
+        stats->active_chords += cnt[o * 3];
+        stats->transparent_chords += cnt[o * 3 + 1];
+        stats->blocked_chords += cnt[o * 3 + 2];
+      }
+      stats->chord_lambda_evals = stats->active_chords * tr.n_wav;
+      stats->tau_kernel_variant = variant;
+    }
+  });
+}
+
+int32_t prom_transit_result(prom_ctx* ctx, double* R_out) {
+  return guarded(ctx, [&] {
+    prom::TransitDev& tr = ctx->tr;
+    if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_result: no completed run");
+    PROM_REQUIRE(R_out, "prom_transit_result: null output");
+    download(R_out, tr.R, (int64_t)tr.n_orb * tr.n_wav, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int32_t prom_transit_columns(prom_ctx* ctx, double* N_out) {
+  return guarded(ctx, [&] {
+    prom::TransitDev& tr = ctx->tr;
+    if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_columns: no completed run");
+    PROM_REQUIRE(N_out, "prom_transit_columns: null output");
+    download(N_out, tr.ncol, (int64_t)tr.n_atoms * tr.n_orb * tr.n_pr, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int32_t prom_timing_begin(prom_ctx* ctx) {
+  return guarded(ctx, [&] {
+    ctx->timing = true;
+    ctx->timed_runs = 0;
+  });
+}
+
+int32_t prom_timing_end(prom_ctx* ctx, int32_t max_runs, double* ms, int32_t* n_runs) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(n_runs && (max_runs <= 0 || ms), "prom_timing_end: bad arguments");
+    ctx->timing = false;
+    const int32_t n = std::min(ctx->timed_runs, std::max(max_runs, 0));
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+    for (int32_t r = 0; r < n; ++r) {
+      hipEvent_t* e = &ctx->tev[4 * (size_t)r];
+      float v[4];
+      PROM_HIP(hipEventElapsedTime(&v[0], e[0], e[1]));
+      PROM_HIP(hipEventElapsedTime(&v[1], e[1], e[2]));
+      PROM_HIP(hipEventElapsedTime(&v[2], e[2], e[3]));
+      PROM_HIP(hipEventElapsedTime(&v[3], e[0], e[3]));
+      for (int i = 0; i < 4; ++i) ms[4 * r + i] = v[i];
+    }
+    *n_runs = ctx->timed_runs;
+    ctx->timed_runs = 0;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,156 @@
+// Internal declarations shared by the C-ABI layer (prom_api.hip) and the kernels (prom_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/prom_hip.h"
+
+namespace prom {
+
+struct Error : std::runtime_error {
+  int32_t code;
+  Error(int32_t c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define PROM_HIP(expr)                                                                      \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      throw ::prom::Error(PROM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+  } while (0)
+
+#define PROM_REQUIRE(cond, msg)                                     \
+  do {                                                              \
+    if (!(cond)) throw ::prom::Error(PROM_E_ARG, std::string(msg)); \
+  } while (0)
+
+// Grow-only device buffer owned by a context.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+  ~DevBuf() { release(); }
+  void ensure(size_t bytes) {
+    if (bytes <= cap) return;
+    release();
+    if (bytes == 0) return;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      p = nullptr;
+      throw Error(PROM_E_NOMEM, "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+    }
+    cap = bytes;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Device-side view of one density model (the prom_density_model scalars).
+struct DensityDev {
+  int32_t kind;
+  int32_t pad;
+  double p[8];
+};
+
+// Device-side descriptor of one absorbing constituent inside the transit problem.
+struct TermDev {
+  int32_t scenario;     // index of its density scenario
+  int32_t is_molecule;
+  int32_t slot;         // atomic: index into N / sigma arrays;  molecular: molecular slot
+  int32_t table;        // table id
+  double chi;
+};
+
+struct AtomTable {
+  DevBuf x, y;
+  int64_t n = 0;
+  double offset = 0.0;
+  double ymax = 0.0;     // max of y (log10 sigma): sigma_max = 10^ymax - offset
+};
+
+struct MolTable {
+  DevBuf P, T, W, V;
+  int32_t n_p = 0, n_t = 0;
+  int64_t n_w = 0;
+  double offset = 0.0;
+  double vmax = 0.0;
+};
+
+// Everything the transit kernels need, as device pointers.
+struct TransitDev {
+  int64_t n_wav = 0;
+  int32_t n_pr = 0, n_orb = 0, n_x = 0, n_sc = 0, n_moons = 0;
+  int32_t n_atoms = 0, n_mol = 0, n_terms = 0;
+  double delta_x = 0.0, planet_R = 0.0, cull_tau = 0.0;
+  bool ready = false;
+  bool ran = false;
+  std::vector<TermDev> terms;               // host copy, scenario/constituent order
+  std::vector<DensityDev> dens;             // host copy
+  std::vector<double> atom_sigma_max;       // per atomic slot
+  std::vector<double> mol_T;                // per molecular slot
+  // device buffers
+  DevBuf wav, cy, cz, cfout, x, planet_y, moon_y, moon_R;
+  DevBuf body_x, body_y, shift;             // [n_sc][n_orb]
+  DevBuf dens_dev;                          // [n_sc] DensityDev
+  DevBuf terms_dev;                         // [n_terms] TermDev
+  DevBuf tab;                               // tabulated densities, raw host order, concatenated
+  DevBuf ntot;                              // [n_sc][n_orb][n_pr][n_x]
+  DevBuf ncol;                              // [n_atoms][n_orb][n_pr]
+  DevBuf molcol;                            // [n_mol][n_orb][n_pr] sum_x n_abs*dx (for the bound)
+  DevBuf flags;                             // [n_orb][n_pr] int32: 0 active, 1 transparent, 2 blocked
+  DevBuf recs;                              // [n_orb][n_pr][1 + n_atoms] packed active-chord records
+  DevBuf act_ip;                            // [n_orb][n_pr] int32 chord positions of active chords
+  DevBuf counts;                            // [n_orb][3] int32: active, transparent, blocked
+  DevBuf tsum;                              // [n_orb] transparent flux sum
+  DevBuf fsum;                              // [n_orb] F_out sum
+  DevBuf sigma;                             // [n_atoms][n_orb][n_wav]
+  DevBuf sigma_max_dev;                     // [n_atoms]
+  DevBuf R;                                 // [n_orb][n_wav]
+  std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
+};
+
+}  // namespace prom
+
+struct prom_ctx {
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  std::string err;
+  std::vector<prom::AtomTable> tables;
+  std::vector<prom::MolTable> mtables;
+  prom::TransitDev tr;
+  prom::DevBuf scratch[6];
+  bool timing = false;
+  std::vector<hipEvent_t> tev;   // pool, 4 per timed run
+  int32_t timed_runs = 0;
+};
+
+namespace prom {
+
+// ---- kernel launchers (prom_kernels.hip) ----
+void launch_table_lookup(hipStream_t s, const double* x, const double* y, int64_t n, double offset,
+                         const double* targets, int64_t nt, double* out);
+void launch_voigt(hipStream_t s, const double* x, int64_t n, const double* lw, const double* lg,
+                  const double* lc, int32_t nl, double sigma_v, double c_light, double offset,
+                  int log_table, double* out);
+void launch_density(hipStream_t s, const DensityDev& m, const double* x, int32_t n_x, const double* y,
+                    const double* z, const double* bx, const double* by, int64_t n_chords, double* out);
+void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, int32_t n_x,
+                            const double* P, double T, int64_t n_wav, const double* wav, double* out);
+void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>& tables,
+                    const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant);
+double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
+
+}  // namespace prom

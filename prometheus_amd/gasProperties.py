@@ -1,0 +1,625 @@
+"""Gas properties and the transit integrator (mirrors ``pythonScripts/gasProperties.py``).
+
+Same classes, method names and argument meanings as the reference, so scripts written for
+``pythonScripts.gasProperties`` run unchanged against ``prometheus_amd.gasProperties``.  What
+changes is where the arithmetic runs:
+
+* density plugins, Voigt cross-section tables, sigma lookups and the whole
+  ``Transit.sumOverChords`` integral run as HIP kernels on MI355X through the C-ABI of
+  ``libprom_hip.so`` (``_native.py``); there is no CPU fallback -- without the library or a
+  GPU these calls raise ``NativeUnavailable``;
+* host code does what the reference's host code does and nothing heavier: it parses the line
+  list, builds the wavelength nodes with the same numpy ``arange``/``sort`` calls (so every node
+  is bit-identical), and evaluates O(n_orbphase) / O(n_chord-positions) scalars (orbital
+  positions, Doppler factors, limb darkening) with numpy.
+
+Wavelength sharding: ``sumOverChords(devices=[...])`` splits the wavelength axis into
+contiguous shards, one host thread per GPU, and gathers R on the host (no collective).
+Per-wavelength arithmetic does not depend on the split, so R is bitwise identical for any
+number of devices.
+"""
+from __future__ import annotations
+
+import math
+import os
+import threading
+from copy import deepcopy
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native
+from . import constants as const
+from . import geometryHandler as geom
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+lineListPath: str = os.path.join(_HERE, "resources", "LineList.txt")
+LINE_LIST = np.loadtxt(lineListPath, dtype=str, usecols=(0, 1, 2, 3, 4), skiprows=1)
+# the reference looks for <parent of the checkout>/molecularResources/<name>.h5 (gasProperties.py:31-32)
+molecularLookupPath: str = os.environ.get(
+    "PROMETHEUS_MOLECULAR_PATH", os.path.join(os.path.dirname(os.path.dirname(_HERE)), "molecularResources"))
+
+_MOLECULAR_TABLES: Dict[str, dict] = {}
+
+
+def register_molecular_table(name: str, table: dict) -> None:
+    """Provide an ExoMol/TauREx-layout table in memory: keys p [Pa], t [K], bin_edges [cm^-1],
+    xsecarr[p][t][nu] [cm^2].  Takes precedence over files in ``molecularLookupPath``."""
+    _MOLECULAR_TABLES[name] = table
+
+
+def _device(dev=None):
+    return _native.get_device(_native.default_device() if dev is None else dev)
+
+
+class LookupTable:
+    """Host copy of a log10-sigma table (the reference keeps an interp1d with .x/.y) plus its
+    device-resident copies, one per GPU, uploaded on first use."""
+
+    def __init__(self, x: np.ndarray, y: np.ndarray, offset: float, ids: Optional[Dict[int, int]] = None):
+        self.x = x
+        self.y = y
+        self.offset = offset
+        self._ids: Dict[int, int] = dict(ids or {})
+        self._lock = threading.Lock()
+
+    def table_id(self, dev: "_native.Device") -> int:
+        with self._lock:
+            tid = self._ids.get(dev.device)
+            if tid is None:
+                tid = dev.table_upload(self.x, self.y, self.offset)
+                self._ids[dev.device] = tid
+            return tid
+
+
+def n_interp_log(x_targets, x_grid, y_grid_log, offset):
+    """10^interp(x_targets; x_grid, y_grid_log) - offset on the GPU (gasProperties.py:34-51)."""
+    dev = _device()
+    with dev.lock:
+        tid = dev.table_upload(x_grid, y_grid_log, offset)
+        t = np.asarray(x_targets, dtype=np.float64)
+        return dev.table_lookup(tid, t.ravel()).reshape(t.shape)
+
+
+# ============================================================================== density scenarios
+class CollisionalAtmosphere:
+    """Isothermal atmosphere with temperature T [K] and reference pressure P_0 [dyn cm^-2]."""
+
+    def __init__(self, T: float, P_0: float):
+        self.T = T
+        self.P_0 = P_0
+        self.constituents: List[Any] = []
+        self.hasMoon = False
+
+    def getReferenceNumberDensity(self) -> float:
+        return self.P_0 / (const.k_B * self.T)
+
+    def getVelDispersion(self, m: float) -> float:
+        return np.sqrt(self.T * const.k_B / m)
+
+    def addConstituent(self, speciesName: str, chi: float) -> None:
+        species = const.AvailableSpecies().findSpecies(speciesName)
+        self.constituents.append(AtmosphericConstituent(species, chi, self.getVelDispersion(species.mass)))
+
+    def addMolecularConstituent(self, speciesName: str, chi: float) -> None:
+        self.constituents.append(MolecularConstituent(speciesName, chi))
+
+    # --- device side ---
+    def densityModel(self) -> Tuple[int, List[float], Any]:
+        """(prom_density_kind, scalar parameters, body whose getPosition centres the profile)."""
+        raise NotImplementedError
+
+    def calculateNumberDensity(self, x, phi, rho, orbphase):
+        return _device_density(self, x, phi, rho, orbphase)
+
+
+def _device_density(model, x, phi, rho, orbphase):
+    """calculateNumberDensity of a built-in scenario, evaluated by prom_number_density."""
+    kind, params, body = model.densityModel()
+    x = np.asarray(x, dtype=np.float64)
+    scalar = np.ndim(phi) == 0 and np.ndim(rho) == 0 and np.ndim(orbphase) == 0
+    phi_, rho_, orb_ = np.broadcast_arrays(np.atleast_1d(phi), np.atleast_1d(rho), np.atleast_1d(orbphase))
+    y, z = geom.Grid.getCartesianFromCylinder(phi_, rho_)
+    bx, by = body.getPosition(orb_)
+    dev = _device()
+    with dev.lock:
+        n = dev.number_density(kind, params, x, y, z, np.broadcast_to(bx, y.shape), np.broadcast_to(by, y.shape))
+    return n[0] if scalar else n
+
+
+class BarometricAtmosphere(CollisionalAtmosphere):
+    """n = n_0 exp((R - r)/H) Heaviside(r - R),  H = k_B T R^2 / (G mu M)  (gasProperties.py:122-161)."""
+
+    def __init__(self, T: float, P_0: float, mu: float, planet: Any):
+        super().__init__(T, P_0)
+        self.mu = mu
+        self.planet = planet
+
+    def densityModel(self):
+        n0 = self.getReferenceNumberDensity()
+        H = const.k_B * self.T * self.planet.R ** 2 / (const.G * self.mu * self.planet.M)
+        return _native.DENSITY_BAROMETRIC, [n0, self.planet.R, H], self.planet
+
+
+class HydrostaticAtmosphere(CollisionalAtmosphere):
+    """n = n_0 exp(J(r) Heaviside(r - R) - J_0),  J = G mu M / (k_B T r)  (gasProperties.py:164-204)."""
+
+    def __init__(self, T: float, P_0: float, mu: float, planet: Any):
+        super().__init__(T, P_0)
+        self.mu = mu
+        self.planet = planet
+
+    def densityModel(self):
+        n0 = self.getReferenceNumberDensity()
+        gmm = const.G * self.mu * self.planet.M
+        kt = const.k_B * self.T
+        j0 = const.G * self.mu * self.planet.M / (const.k_B * self.T * self.planet.R)
+        return _native.DENSITY_HYDROSTATIC, [n0, self.planet.R, gmm, kt, j0], self.planet
+
+
+class PowerLawAtmosphere(CollisionalAtmosphere):
+    """n = n_0 (R/r)^q Heaviside(r - R), pressure-normalised  (gasProperties.py:207-244)."""
+
+    def __init__(self, T: float, P_0: float, q: float, planet: Any):
+        super().__init__(T, P_0)
+        self.q = q
+        self.planet = planet
+
+    def densityModel(self):
+        return _native.DENSITY_POWERLAW, [self.getReferenceNumberDensity(), self.planet.R, self.q], self.planet
+
+
+class EvaporativeExosphere:
+    """Exosphere normalised by its total particle number N; one absorber (gasProperties.py:247-288)."""
+
+    def __init__(self, N: float):
+        self.N = N
+        self.hasMoon = False
+
+    def addConstituent(self, speciesName: str, sigma_v: float) -> None:
+        species = const.AvailableSpecies().findSpecies(speciesName)
+        self.constituents = [AtmosphericConstituent(species, 1., sigma_v)]
+
+    def addMolecularConstituent(self, speciesName: str, T: float) -> None:
+        self.constituents = [MolecularConstituent(speciesName, 1.0)]
+        self.T = T
+
+    def densityModel(self):
+        raise NotImplementedError
+
+    def calculateNumberDensity(self, x, phi, rho, orbphase):
+        return _device_density(self, x, phi, rho, orbphase)
+
+
+class PowerLawExosphere(EvaporativeExosphere):
+    """n = (q-3)/(4 pi R^3) N (R/r)^q Heaviside(r - R)  (gasProperties.py:291-330)."""
+
+    def __init__(self, N: float, q: float, planet: Any):
+        super().__init__(N)
+        self.q = q
+        self.planet = planet
+
+    def densityModel(self):
+        n0 = (self.q - 3.) / (4. * np.pi * self.planet.R ** 3) * self.N
+        return _native.DENSITY_POWERLAW, [n0, self.planet.R, self.q], self.planet
+
+
+class MoonExosphere(EvaporativeExosphere):
+    """Power law about an exomoon; the moon also blocks light (gasProperties.py:333-374)."""
+
+    def __init__(self, N: float, q: float, moon: Any):
+        super().__init__(N)
+        self.q = q
+        self.moon = moon
+        self.hasMoon = True
+        self.planet = moon.hostPlanet
+
+    def densityModel(self):
+        n0 = (self.q - 3.) / (4. * np.pi * self.moon.R ** 3) * self.N
+        return _native.DENSITY_POWERLAW, [n0, self.moon.R, self.q], self.moon
+
+
+class TidallyHeatedMoon(EvaporativeExosphere):
+    """Moon exosphere with a phase-dependent source rate (gasProperties.py:377-461).
+
+    Not a built-in device scenario: its density is evaluated on the host by the plugin itself
+    (``calculateNumberDensity``) and handed to the device as a tabulated n(c, x)."""
+
+    def __init__(self, q: float, moon: Any):
+        self.q = q
+        self.moon = moon
+        self.hasMoon = True
+        self.planet = moon.hostPlanet
+
+    def addSourceRateFunction(self, filename: str, tau_photoionization: float, mass_absorber: float) -> None:
+        mdot = np.loadtxt(filename)
+        mdot = np.concatenate((mdot, mdot[::-1]))
+        self._phi_src = np.linspace(0., 2. * np.pi, len(mdot))
+        self._logN_src = np.log10(mdot * tau_photoionization / mass_absorber)
+
+    def calculateAbsorberNumber(self, orbphase):
+        om = self.moon.getOrbphase(orbphase) % (2. * np.pi)
+        return 10 ** np.interp(om, self._phi_src, self._logN_src)
+
+    def calculateNumberDensity(self, x, phi, rho, orbphase):
+        N = np.asarray(self.calculateAbsorberNumber(orbphase))
+        r = self.moon.getDistanceFromMoon(x, phi, rho, orbphase)
+        if N.ndim > 0:
+            N = N[:, np.newaxis]
+        n0 = (self.q - 3.) / (4. * np.pi * self.moon.R ** 3) * N
+        return n0 * (self.moon.R / r) ** self.q * np.heaviside(r - self.moon.R, 1.)
+
+
+class TorusExosphere(EvaporativeExosphere):
+    """Gaussian torus of radius a_torus and scale height a v_ej / v_orbit (gasProperties.py:464-516)."""
+
+    def __init__(self, N: float, a_torus: float, v_ej: float, planet: Any):
+        super().__init__(N)
+        self.a_torus = a_torus
+        self.v_ej = v_ej
+        self.planet = planet
+
+    def densityModel(self):
+        v_orbit = np.sqrt(const.G * self.planet.M / self.a_torus)
+        H = self.a_torus * self.v_ej / v_orbit
+        t1 = 8. * H ** 2 * np.exp(-self.a_torus ** 2 / (16. * H ** 2))
+        t2 = 2. * np.sqrt(np.pi) * self.a_torus * H * (math.erf(self.a_torus / (4. * H)) + 1.)
+        n0 = 1. / (2. * np.pi ** 1.5 * H * (t1 + t2)) * self.N
+        return _native.DENSITY_TORUS, [n0, self.a_torus, 4. * H, H], self.planet
+
+
+class SerpensExosphere(EvaporativeExosphere):
+    """SERPENS particle-cloud density (gasProperties.py:519-601).  Out of the fused path's scope
+    (SURVEY.md §8f rank 3): it is a host plugin, tabulated onto the device like any user plugin."""
+
+    def __init__(self, filename: str, N: float, planet: Any, sigmaSmoothing: float):
+        super().__init__(N)
+        self.filename = filename
+        self.planet = planet
+        self.sigmaSmoothing = sigmaSmoothing
+
+    def densityModel(self):
+        raise NotImplementedError
+
+    def calculateNumberDensity(self, x, phi, rho, orbphase):
+        raise NotImplementedError("SerpensExosphere needs the SERPENS particle file and a 3-D density "
+                                  "sampler; not part of this build (SURVEY.md §8f rank 3)")
+
+
+# ============================================================================== cross sections
+class AtmosphericConstituent:
+    """Atom/ion absorber; its sigma(lambda) is a sum of Voigt lines from the NIST list
+    (gasProperties.py:609-735).  The table is built on the GPU."""
+
+    def __init__(self, species: Any, chi: float, sigma_v: float):
+        self.isMolecule = False
+        self.species = species
+        self.chi = chi
+        self.sigma_v = sigma_v
+        self.wavelengthGridRefinement = 10.
+        self.wavelengthGridExtension = 0.01
+        self.lookupOffset = 1e-50
+
+    def getLineParameters(self, wavelength) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Lines of this species strictly inside (min, max) of ``wavelength``: centre [cm],
+        gamma = A/(4 pi), oscillator strength (gasProperties.py:640-670)."""
+        ll = LINE_LIST
+        mine = (ll[:, 0] == self.species.element) & (ll[:, 1] == self.species.ionizationState) & \
+            (ll[:, 2] != '') & (ll[:, 3] != '') & (ll[:, 4] != '')
+        lam = ll[mine, 2].astype(float) * 1e-8
+        gam = ll[mine, 3].astype(float) / (4. * np.pi)
+        f = ll[mine, 4].astype(float)
+        inside = (lam > min(wavelength)) & (lam < max(wavelength))
+        return lam[inside], gam[inside], f[inside]
+
+    def _lines(self, wavelength):
+        lam, gam, f = self.getLineParameters(wavelength)
+        # (pi e^2 / (m_e c)) * f, evaluated left to right as in gasProperties.py:689-691
+        coef = np.array([np.pi * const.e ** 2 / (const.m_e * const.c) * fi for fi in f], dtype=np.float64)
+        return lam, gam, coef
+
+    def calculateVoigtProfile(self, wavelength) -> np.ndarray:
+        w = np.asarray(wavelength, dtype=np.float64)
+        lam, gam, coef = self._lines(w)
+        dev = _device()
+        with dev.lock:
+            return dev.voigt_sigma(w.ravel(), lam, gam, coef, self.sigma_v, const.c).reshape(w.shape)
+
+    def constructLookupFunction(self, wavelengthGrid: "WavelengthGrid") -> LookupTable:
+        refined = deepcopy(wavelengthGrid)
+        refined.resolutionHigh /= self.wavelengthGridRefinement
+        refined.lower_w *= (1. - self.wavelengthGridExtension)
+        refined.upper_w *= (1. + self.wavelengthGridExtension)
+        x = refined.constructWavelengthGridSingle(self)
+        lam, gam, coef = self._lines(x)
+        dev = _device()
+        with dev.lock:
+            tid, y = dev.table_build_voigt(x, lam, gam, coef, self.sigma_v, const.c, self.lookupOffset)
+        return LookupTable(x, y, self.lookupOffset, {dev.device: tid})
+
+    def addLookupFunctionToConstituent(self, wavelengthGrid: "WavelengthGrid") -> None:
+        self.lookupFunction = self.constructLookupFunction(wavelengthGrid)
+
+    def getSigmaAbs(self, wavelength) -> np.ndarray:
+        w = np.asarray(wavelength, dtype=np.float64)
+        dev = _device()
+        with dev.lock:
+            return dev.table_lookup(self.lookupFunction.table_id(dev), w.ravel()).reshape(w.shape)
+
+
+class MolecularTable:
+    """(P [dyn cm^-2], T [K], lambda [cm], log10(xsec + offset)) after the reference's conversions
+    (gasProperties.py:774-781), with per-device uploaded copies."""
+
+    def __init__(self, P, T, W, V, offset):
+        self.P, self.T, self.W, self.V, self.offset = P, T, W, V, offset
+        self.grid = (P, T, W)
+        self._ids: Dict[int, int] = {}
+        self._lock = threading.Lock()
+
+    def table_id(self, dev) -> int:
+        with self._lock:
+            tid = self._ids.get(dev.device)
+            if tid is None:
+                tid = dev.molecular_upload(self.P, self.T, self.W, self.V, self.offset)
+                self._ids[dev.device] = tid
+            return tid
+
+
+def _read_molecular_source(name: str) -> dict:
+    if name in _MOLECULAR_TABLES:
+        return _MOLECULAR_TABLES[name]
+    base = os.path.join(molecularLookupPath, name)
+    if os.path.exists(base + ".npz"):
+        with np.load(base + ".npz", allow_pickle=False) as d:
+            return {k: d[k] for k in ("p", "t", "bin_edges", "xsecarr")}
+    if os.path.exists(base + ".h5"):
+        import h5py  # optional dependency, as in the reference
+        with h5py.File(base + ".h5", "r") as f:
+            return {k: f[k][:] for k in ("p", "t", "bin_edges", "xsecarr")}
+    raise FileNotFoundError("no molecular table %r (register_molecular_table, %s.npz or %s.h5)" % (name, base, base))
+
+
+class MolecularConstituent:
+    """Molecule with a (P, T, lambda) cross-section table (gasProperties.py:738-818)."""
+
+    def __init__(self, moleculeName: str, chi: float):
+        self.isMolecule = True
+        self.lookupOffset = 1e-50
+        self.moleculeName = moleculeName
+        self.chi = chi
+
+    def constructLookupFunction(self) -> MolecularTable:
+        src = _read_molecular_source(self.moleculeName)
+        P = np.asarray(src["p"], dtype=np.float64) * 10.
+        T = np.asarray(src["t"], dtype=np.float64)
+        W = 1. / np.asarray(src["bin_edges"], dtype=np.float64)[::-1]
+        V = np.log10(np.asarray(src["xsecarr"], dtype=np.float64)[:, :, ::-1] + self.lookupOffset)
+        return MolecularTable(P, T, np.ascontiguousarray(W), np.ascontiguousarray(V), self.lookupOffset)
+
+    def addLookupFunctionToConstituent(self) -> None:
+        self.lookupFunction = self.constructLookupFunction()
+
+    def getSigmaAbs(self, P, T, wavelength) -> np.ndarray:
+        dev = _device()
+        with dev.lock:
+            return dev.molecular_sigma(self.lookupFunction.table_id(dev), np.asarray(P, np.float64), T,
+                                       np.asarray(wavelength, np.float64))
+
+
+# ============================================================================== atmosphere
+class Atmosphere:
+    """All density distributions of a run (gasProperties.py:821-956)."""
+
+    def __init__(self, densityDistributionList: List[Any], hasOrbitalDopplerShift: bool):
+        self.densityDistributionList = densityDistributionList
+        self.hasOrbitalDopplerShift = hasOrbitalDopplerShift
+
+    @staticmethod
+    def getAbsorberNumberDensity(densityDistribution, chi, x, phi, rho, orbphase):
+        return densityDistribution.calculateNumberDensity(x, phi, rho, orbphase) * chi
+
+    def getAbsorberVelocityField(self, densityDistribution, x, phi, rho, orbphase):
+        v = np.zeros_like(x)
+        if self.hasOrbitalDopplerShift:
+            body = densityDistribution.moon if densityDistribution.hasMoon else densityDistribution.planet
+            v += body.getLOSvelocity(orbphase)
+        return v
+
+    def shifts(self, densityDistribution, orbphase) -> np.ndarray:
+        """Per-phase Doppler factor of one distribution (gasProperties.py:907-917)."""
+        orbphase = np.asarray(orbphase, dtype=np.float64)
+        if self.hasOrbitalDopplerShift:
+            body = densityDistribution.moon if densityDistribution.hasMoon else densityDistribution.planet
+            v = body.getLOSvelocity(orbphase)
+        else:
+            v = np.zeros(len(orbphase))
+        return const.calculateDopplerShift(-v)
+
+
+# ============================================================================== wavelength grid
+class WavelengthGrid:
+    """Non-uniform wavelength grid: resolutionHigh inside windows of width widthHighRes around each
+    line, resolutionLow elsewhere (gasProperties.py:959-1071).  Node generation keeps the
+    reference's sequence of numpy ``arange`` calls, which fixes every node to the bit."""
+
+    def __init__(self, lower_w: float, upper_w: float, widthHighRes: float, resolutionLow: float,
+                 resolutionHigh: float):
+        self.lower_w = lower_w
+        self.upper_w = upper_w
+        self.widthHighRes = widthHighRes
+        self.resolutionLow = resolutionLow
+        self.resolutionHigh = resolutionHigh
+
+    def arangeWavelengthGrid(self, linesList) -> np.ndarray:
+        peaks = np.sort(np.unique(linesList))
+        if len(peaks) == 0:
+            print('WARNING: No absorption lines from atoms/ions in the specified wavelength range!')
+            return np.arange(self.lower_w, self.upper_w, self.resolutionLow)
+        w = self.widthHighRes
+        gaps = np.concatenate(([np.inf], np.diff(peaks), [np.inf]))
+        lo_edges = [p - w / 2. for i, p in enumerate(peaks) if gaps[i] > w]
+        hi_edges = [p + w / 2. for i, p in enumerate(peaks) if gaps[i + 1] > w]
+        segs = []
+        last = len(lo_edges) - 1
+        for i in range(len(lo_edges)):
+            segs.append(np.arange(lo_edges[i], hi_edges[i], self.resolutionHigh))
+            if i == 0:
+                if self.lower_w < lo_edges[0]:
+                    segs.append(np.arange(self.lower_w, lo_edges[0], self.resolutionLow))
+                if last == 0 and self.upper_w > hi_edges[-1]:
+                    segs.append(np.arange(hi_edges[0], self.upper_w, self.resolutionLow))
+                continue
+            segs.append(np.arange(hi_edges[i - 1], lo_edges[i], self.resolutionLow))
+            if i == last and self.upper_w > hi_edges[-1]:
+                segs.append(np.arange(hi_edges[-1], self.upper_w, self.resolutionLow))
+        return np.sort(np.concatenate(segs))
+
+    def constructWavelengthGridSingle(self, constituent: AtmosphericConstituent) -> np.ndarray:
+        return self.arangeWavelengthGrid(constituent.getLineParameters(np.array([self.lower_w, self.upper_w]))[0])
+
+    def constructWavelengthGrid(self, densityDistributionList: List[Any]) -> np.ndarray:
+        lines: List[float] = []
+        for dist in densityDistributionList:
+            for con in dist.constituents:
+                if not con.isMolecule:
+                    lines.extend(con.getLineParameters(np.array([self.lower_w, self.upper_w]))[0])
+        if len(lines) == 0:
+            return np.arange(self.lower_w, self.upper_w, self.resolutionLow)
+        return self.arangeWavelengthGrid(lines)
+
+
+# ============================================================================== transit
+def _split(n: int, parts: int) -> List[Tuple[int, int]]:
+    edges = np.linspace(0, n, parts + 1).round().astype(np.int64)
+    return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+
+
+class Transit:
+    """Transit depth R(orbital phase, wavelength) (gasProperties.py:1074-1258)."""
+
+    def __init__(self, atmosphere: Atmosphere, wavelengthGrid: WavelengthGrid, spatialGrid: geom.Grid):
+        self.atmosphere = atmosphere
+        self.wavelengthGrid = wavelengthGrid
+        self.spatialGrid = spatialGrid
+        self.planet = self.atmosphere.densityDistributionList[0].planet
+        self.last_stats: List[dict] = []
+
+    def addWavelength(self) -> None:
+        self.wavelength = self.wavelengthGrid.constructWavelengthGrid(self.atmosphere.densityDistributionList)
+
+    def checkBlock(self, phi: float, rho: float, orbphase: float) -> bool:
+        """Scalar blocking test (gasProperties.py:1107-1130; the moon test uses R_moon^2 here,
+        as the batched path does, not R_moon)."""
+        y, z = geom.Grid.getCartesianFromCylinder(phi, rho)
+        if np.sqrt((y - self.planet.getPosition(orbphase)[1]) ** 2 + z ** 2) < self.planet.R:
+            return True
+        for d in self.atmosphere.densityDistributionList:
+            if d.hasMoon and (y - d.moon.getPosition(orbphase)[1]) ** 2 + z ** 2 < d.moon.R ** 2:
+                return True
+        return False
+
+    # ---- host-side set-up: O(n_phase + n_chord-positions) scalars, numpy as in the reference ----
+    def _host_inputs(self) -> dict:
+        g = self.spatialGrid
+        star = self.planet.hostStar
+        if star.Fstar_function is not None:
+            raise NotImplementedError("stellar spectrum / RM path (gasProperties.py:1210-1219) is not in this "
+                                      "build (SURVEY.md §8f rank 2)")
+        phi, rho = g.getChordPositions()
+        y, z = rho * np.sin(phi), rho * np.cos(phi)
+        mu = np.sqrt(np.clip(1. - rho ** 2 / star.R ** 2, 0, 1))
+        clv = 1. - star.CLV_u1 * (1. - mu) - star.CLV_u2 * (1. - mu) ** 2
+        fout = rho * (np.ones_like(clv) * clv)
+        orb = g.constructOrbphaseAxis()
+        moons = [d.moon for d in self.atmosphere.densityDistributionList if d.hasMoon]
+        scen = []
+        need_tab = []
+        for d in self.atmosphere.densityDistributionList:
+            entry = {"dist": d, "shift": self.atmosphere.shifts(d, orb), "T": float(getattr(d, "T", 0.0) or 0.0)}
+            try:
+                kind, params, body = d.densityModel()
+                bx, by = body.getPosition(orb)
+                entry.update(kind=kind, params=params, body_x=np.asarray(bx, float), body_y=np.asarray(by, float))
+            except NotImplementedError:
+                entry.update(kind=_native.DENSITY_TABULATED, params=[])
+                need_tab.append(entry)
+            scen.append(entry)
+        if need_tab:
+            cg = g.getChordGrid()
+            x = g.constructXaxis()
+            for e in need_tab:
+                e["n_tabulated"] = np.asarray(e["dist"].calculateNumberDensity(x, cg[:, 0], cg[:, 1], cg[:, 2]),
+                                              dtype=np.float64).reshape(len(cg), len(x))
+        return {"y": y, "z": z, "fout": fout, "orb": orb, "x": g.constructXaxis(), "dx": g.getDeltaX(),
+                "planet_y": self.planet.a * np.sin(orb), "planet_R": self.planet.R,
+                "moon_y": np.array([m.getPosition(orb)[1] for m in moons]).reshape(len(moons), len(orb)),
+                "moon_R": np.array([m.R for m in moons], dtype=np.float64), "scenarios": scen}
+
+    def _problem(self, dev, host: dict, w0: int, w1: int, cull_tau: float) -> "_native.TransitInputs":
+        scs = []
+        for e in host["scenarios"]:
+            cons = []
+            for con in e["dist"].constituents:
+                cons.append({"table_id": con.lookupFunction.table_id(dev), "is_molecule": con.isMolecule,
+                             "chi": con.chi})
+            scs.append({"kind": e["kind"], "params": e["params"], "body_x": e.get("body_x"),
+                        "body_y": e.get("body_y"), "shift": e["shift"], "n_tabulated": e.get("n_tabulated"),
+                        "T": e["T"], "constituents": cons})
+        return _native.TransitInputs(
+            wavelength=self.wavelength[w0:w1], chord_y=host["y"], chord_z=host["z"], chord_fout=host["fout"],
+            n_orb=len(host["orb"]), x=host["x"], delta_x=host["dx"], planet_y=host["planet_y"],
+            planet_R=host["planet_R"], moon_y=host["moon_y"], moon_R=host["moon_R"], scenarios=scs,
+            cull_tau=cull_tau)
+
+    def sumOverChords(self, max_memory_gb: float = 2.0, devices: Optional[Sequence[int]] = None,
+                      cull_tau: float = 0.0) -> np.ndarray:
+        """R[n_orb, n_wav] = sum_chords F_out exp(-tau) / sum_chords F_out, on the GPU(s).
+
+        ``devices``: GPU ids to shard the wavelength axis over (default: all visible GPUs when
+        there are >= 65,536 wavelengths per GPU, else GPU 0).  ``max_memory_gb`` bounds the
+        device working set of one shard step; larger shards are processed in several steps."""
+        if not hasattr(self, "wavelength"):
+            self.addWavelength()
+        host = self._host_inputs()
+        n_wav, n_orb = len(self.wavelength), len(host["orb"])
+        if devices is None:
+            avail = _native.device_count()
+            if avail == 0:
+                raise _native.NativeUnavailable("no HIP device visible")
+            devices = list(range(min(avail, max(1, n_wav // 65536))))
+        devices = list(devices)
+        n_atoms = sum(1 for d in self.atmosphere.densityDistributionList for c in d.constituents
+                      if not c.isMolecule)
+        per_wav = 8 * n_orb * (2 + max(1, n_atoms))
+        chunk = max(4096, int(max_memory_gb * 1e9) // per_wav)
+        R = np.empty((n_orb, n_wav))
+        shards = _split(n_wav, len(devices))
+        errors: List[BaseException] = []
+        self.last_stats = []
+
+        def work(dev_id: int, lo: int, hi: int):
+            try:
+                dev = _native.get_device(dev_id)
+                with dev.lock:
+                    for a in range(lo, hi, chunk):
+                        b = min(hi, a + chunk)
+                        dev.transit_set(self._problem(dev, host, a, b, cull_tau))
+                        st = dev.transit_run(stats=True)
+                        R[:, a:b] = dev.transit_result()
+                        st.update(device=dev_id, w0=a, w1=b)
+                        self.last_stats.append(st)
+            except BaseException as ex:  # re-raised in the caller
+                errors.append(ex)
+
+        if len(shards) == 1:
+            work(devices[0], *shards[0])
+        else:
+            th = [threading.Thread(target=work, args=(devices[i], a, b)) for i, (a, b) in enumerate(shards)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        if errors:
+            raise errors[0]
+        return R

@@ -1,0 +1,52 @@
+"""CPU-side checks of the C-ABI boundary: the library loads, exports every symbol declared in
+include/prom_hip.h, and the product fails loudly (no CPU fallback) when no GPU is visible."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "prom_hip.h")).read()
+    return sorted(set(re.findall(r"\b(prom_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_header():
+    from prometheus_amd import _native
+    lib = _native.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 18
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_native.SIGNATURES), set(syms) ^ set(_native.SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (prom_\w+)", out))
+    assert set(syms) <= exported
+
+
+def test_abi_version_and_no_device_here():
+    from prometheus_amd import _native
+    lib = _native.load_library()
+    assert lib.prom_abi_version() == 1
+    if _native.device_count() == 0:
+        with pytest.raises(_native.NativeUnavailable):
+            _native.Device(0)
+
+
+def test_product_fails_loudly_without_gpu():
+    from prometheus_amd import _native
+    if _native.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    from prometheus_amd import configs, setupfile
+    with pytest.raises(_native.NativeUnavailable):
+        setupfile.build_transit(configs.get("C1"))
+
+
+def test_missing_library_is_an_error(tmp_path):
+    from prometheus_amd import _native
+    with pytest.raises(_native.NativeUnavailable):
+        _native.load_library(str(tmp_path / "nope.so"))
