@@ -151,7 +151,13 @@ typedef struct prom_transit_problem {
   const prom_scenario* scenarios;
   double cull_tau;             /* chords whose tau upper bound is below this are transparent
                                   (exp(-tau) == 1 to the last ulp); <= 0 selects 2^-60       */
+  int32_t options;             /* PROM_OPT_* bit set                                          */
+  int32_t reserved2;
 } prom_transit_problem;
+
+/* prom_transit_problem.options */
+#define PROM_OPT_OCML_EXP 1    /* use the ocml exp() in the tau kernel instead of the table-driven exp */
+#define PROM_OPT_NO_MERGE 2    /* integrate every active chord (no merging of equal-column chords) */
 
 typedef struct prom_transit_stats {
   double ms_total;             /* device time of the last prom_transit_run (hipEvents)        */
@@ -161,9 +167,12 @@ typedef struct prom_transit_stats {
   int64_t active_chords;       /* chord-phase pairs integrated (all phases)                   */
   int64_t transparent_chords;  /* chord-phase pairs folded in as exp(-tau) = 1                */
   int64_t blocked_chords;
-  int64_t chord_lambda_evals;  /* active_chords * n_wav: exp evaluations of the fused kernel  */
+  int64_t chord_lambda_evals;  /* active_chords * n_wav                                        */
+  int64_t tau_records;         /* chord records the tau kernel integrates (after merging)     */
+  int64_t exp_evals;           /* tau_records * n_wav: exp evaluations of the fused kernel    */
   int32_t tau_kernel_variant;
-  int32_t reserved;
+  int32_t tau_kernel_variant_exact_phases;  /* phases integrated on the exact (ocml) path because a
+                                               column density was not finite                      */
 } prom_transit_stats;
 
 /* Copy a problem to the device (all host arrays are read during the call). */

@@ -57,14 +57,19 @@ class TransitProblem(C.Structure):
                 ("n_scenarios", C.c_int32), ("x", _dp), ("delta_x", C.c_double), ("planet_y", _dp),
                 ("planet_R", C.c_double), ("n_moons", C.c_int32), ("reserved", C.c_int32),
                 ("moon_y", _dp), ("moon_R", _dp), ("scenarios", C.POINTER(Scenario)),
-                ("cull_tau", C.c_double)]
+                ("cull_tau", C.c_double), ("options", C.c_int32), ("reserved2", C.c_int32)]
+
+
+OPT_OCML_EXP = 1
+OPT_NO_MERGE = 2
 
 
 class TransitStats(C.Structure):
     _fields_ = [("ms_total", C.c_double), ("ms_density", C.c_double), ("ms_sigma", C.c_double),
                 ("ms_tau", C.c_double), ("active_chords", C.c_int64), ("transparent_chords", C.c_int64),
                 ("blocked_chords", C.c_int64), ("chord_lambda_evals", C.c_int64),
-                ("tau_kernel_variant", C.c_int32), ("reserved", C.c_int32)]
+                ("tau_records", C.c_int64), ("exp_evals", C.c_int64),
+                ("tau_kernel_variant", C.c_int32), ("exact_phases", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
@@ -278,7 +283,7 @@ class TransitInputs:
     """Owns the numpy arrays behind one prom_transit_problem (kept alive while in use)."""
 
     def __init__(self, *, wavelength, chord_y, chord_z, chord_fout, n_orb, x, delta_x, planet_y, planet_R,
-                 moon_y, moon_R, scenarios, cull_tau=0.0):
+                 moon_y, moon_R, scenarios, cull_tau=0.0, options=0):
         keep = []
 
         def arr(a):
@@ -326,6 +331,7 @@ class TransitInputs:
         s.n_scenarios = len(scenarios)
         s.scenarios = scs
         s.cull_tau = float(cull_tau)
+        s.options = int(options)
         self.struct = s
         self.keepalive = keep
         self.n_atoms = n_atoms

@@ -8,7 +8,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/prom_api.hip", "csrc/prom_kernels.hip"]
-HEADERS = ["csrc/prom_internal.h", "csrc/faddeeva.h", "../include/prom_hip.h"]
+HEADERS = ["csrc/prom_internal.h", "csrc/faddeeva.h", "csrc/exp2_table.h", "csrc/exp2_table_body.h",
+           "../include/prom_hip.h"]
 OUT = os.path.join(HERE, "libprom_hip.so")
 ARCH = os.environ.get("PROM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=" + ARCH, "-ffp-contract=off", "-fPIC", "-shared", "-Wall",

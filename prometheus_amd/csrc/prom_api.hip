@@ -277,6 +277,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.delta_x = pb->delta_x;
     tr.planet_R = pb->planet_R;
     tr.cull_tau = pb->cull_tau > 0.0 ? pb->cull_tau : std::ldexp(1.0, -60);
+    tr.exp_mode = (pb->options & PROM_OPT_OCML_EXP) ? 0 : 1;
+    tr.merge = (pb->options & PROM_OPT_NO_MERGE) == 0;
     tr.terms.clear();
     tr.dens.clear();
     tr.atom_sigma_max.clear();
@@ -341,6 +343,16 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     upload(tr.shift, sh.data(), (int64_t)sh.size(), s);
     upload(tr.terms_dev, tr.terms.data(), (int64_t)tr.terms.size(), s);
     upload(tr.sigma_max_dev, tr.atom_sigma_max.data(), (int64_t)tr.atom_sigma_max.size(), s);
+    {
+      std::vector<prom::SigTabDev> st;
+      for (const auto& t : tr.terms) {
+        if (t.is_molecule) continue;
+        const prom::AtomTable& tb = ctx->tables[t.table];
+        st.push_back({tb.x.as<double>(), tb.y.as<double>(), tb.n, tb.offset,
+                      tr.shift.as<double>() + (int64_t)t.scenario * n_orb});
+      }
+      upload(tr.sigtab, st.data(), (int64_t)st.size(), s);
+    }
     tr.tab.ensure(sizeof(double) * std::max<int64_t>(tab_total, 1));
     for (int32_t sc = 0; sc < tr.n_sc; ++sc)
       if (tr.tab_off[sc] >= 0)
@@ -354,10 +366,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.flags.ensure(sizeof(int32_t) * nc);
     tr.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
     tr.act_ip.ensure(sizeof(int32_t) * nc);
-    tr.counts.ensure(sizeof(int32_t) * n_orb * 3);
+    tr.counts.ensure(sizeof(int32_t) * n_orb * 5);
+    tr.mrecs.ensure(sizeof(double) * nc * (1 + n_atoms));
     tr.tsum.ensure(sizeof(double) * n_orb);
     tr.fsum.ensure(sizeof(double) * n_orb);
-    tr.sigma.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * n_orb * tr.n_wav);
     tr.R.ensure(sizeof(double) * n_orb * tr.n_wav);
     PROM_HIP(hipStreamSynchronize(s));
     tr.ready = true;
@@ -395,15 +407,19 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
       stats->ms_sigma = b;
       stats->ms_tau = c;
       stats->ms_total = t;
-      std::vector<int32_t> cnt(tr.n_orb * 3);
+      std::vector<int32_t> cnt(tr.n_orb * 5);
       download(cnt.data(), tr.counts, (int64_t)cnt.size(), ctx->stream);
       PROM_HIP(hipStreamSynchronize(ctx->stream));
       for (int32_t o = 0; o < tr.n_orb; ++o) {
-        stats->active_chords += cnt[o * 3];
-        stats->transparent_chords += cnt[o * 3 + 1];
-        stats->blocked_chords += cnt[o * 3 + 2];
+        const bool exact_phase = cnt[o * 5 + 3] != 0 || !tr.exp_mode;
+        stats->active_chords += cnt[o * 5];
+        stats->transparent_chords += cnt[o * 5 + 1];
+        stats->blocked_chords += cnt[o * 5 + 2];
+        stats->tau_records += exact_phase ? cnt[o * 5] : cnt[o * 5 + 4];
+        if (cnt[o * 5 + 3]) stats->tau_kernel_variant_exact_phases += 1;
       }
       stats->chord_lambda_evals = stats->active_chords * tr.n_wav;
+      stats->exp_evals = stats->tau_records * tr.n_wav;
       stats->tau_kernel_variant = variant;
     }
   });

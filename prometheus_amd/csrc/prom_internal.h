@@ -73,6 +73,15 @@ struct TermDev {
   double chi;
 };
 
+// Per atomic slot of a transit problem: its table and its scenario's per-phase Doppler factors.
+struct SigTabDev {
+  const double* x;
+  const double* y;
+  int64_t n;
+  double offset;
+  const double* shift;   // [n_orb]
+};
+
 struct AtomTable {
   DevBuf x, y;
   int64_t n = 0;
@@ -110,13 +119,17 @@ struct TransitDev {
   DevBuf ncol;                              // [n_atoms][n_orb][n_pr]
   DevBuf molcol;                            // [n_mol][n_orb][n_pr] sum_x n_abs*dx (for the bound)
   DevBuf flags;                             // [n_orb][n_pr] int32: 0 active, 1 transparent, 2 blocked
-  DevBuf recs;                              // [n_orb][n_pr][1 + n_atoms] packed active-chord records
+  DevBuf recs;                              // [n_orb][n_pr][1 + n_atoms] {log2(F/Fsum)*2048, N_s}
   DevBuf act_ip;                            // [n_orb][n_pr] int32 chord positions of active chords
-  DevBuf counts;                            // [n_orb][3] int32: active, transparent, blocked
-  DevBuf tsum;                              // [n_orb] transparent flux sum
+  DevBuf counts;                            // [n_orb][5] int32: active, transparent, blocked, nonfinite, records
+  DevBuf tsum;                              // [n_orb] transparent flux sum / F_out sum
   DevBuf fsum;                              // [n_orb] F_out sum
   DevBuf sigma;                             // [n_atoms][n_orb][n_wav]
   DevBuf sigma_max_dev;                     // [n_atoms]
+  DevBuf sigtab;                            // [n_atoms] SigTabDev
+  int32_t exp_mode = 1;                     // 1: table-driven exp in k_tau, 0: ocml exp
+  bool merge = true;                        // merge chords with equal (2^-40) column densities
+  DevBuf mrecs;                             // merged records [n_orb][n_pr][1 + n_atoms]
   DevBuf R;                                 // [n_orb][n_wav]
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
 };

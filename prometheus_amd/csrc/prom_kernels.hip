@@ -14,14 +14,20 @@
 //                 tau upper bound per chord -> active / transparent / blocked
 //     k_compact   per phase, in chord order: packed records of the active chords, transparent
 //                 and total F_out sums
-//     k_sigma     sigma[s][o][w] = 10^interp(shift_o * lambda_w) - offset  (HBM-streaming)
-//     k_tau<NS>   per (phase, wavelength): tau over active chords, exp(-tau), disk sum, ratio
+//     k_tau<NS>   per (phase, wavelength): sigma_s = 10^interp(shift_o * lambda_w) - offset for each
+//                 species, then tau over the active chords, exp(-tau), disk sum, ratio
+#include "exp2_table.h"
 #include "faddeeva.h"
 #include "prom_internal.h"
 
 namespace prom {
 
 constexpr int kBlock = 256;
+
+__constant__ double kExp2TableDev[PROM_EXP2_TABLE_N] = {
+#define PROM_EXP2_TABLE_BODY
+#include "exp2_table_body.h"
+};
 
 static inline unsigned grid_for(int64_t n, int block = kBlock, int64_t cap = 1 << 20) {
   int64_t g = (n + block - 1) / block;
@@ -361,7 +367,12 @@ __global__ void k_columns(const TermDev* __restrict__ terms, int32_t n_terms,
   }
 }
 
-// One workgroup per phase: stream compaction of the active chords in chord order.
+// One workgroup per phase.  Pass 1: F_out sum, transparent sum and the counts.  Pass 2: stream
+// compaction of the active chords in chord order into packed records
+//   {F_out / F_out_sum, N_0, .., N_{S-1}}
+// (so R = sum_active w_c exp(-tau_c) + transparent fraction), their chord positions, and a flag
+// for non-finite column densities (the tau kernel then takes the exact ocml path for that phase).
+// counts[o] = {active, transparent, blocked, nonfinite, records}; tfrac[o] = transparent sum / F_out sum.
 __global__ void __launch_bounds__(kBlock) k_compact(const int32_t* __restrict__ flags,
                                                     const double* __restrict__ fout,
                                                     const double* __restrict__ ncol, int32_t n_atoms,
@@ -369,25 +380,47 @@ __global__ void __launch_bounds__(kBlock) k_compact(const int32_t* __restrict__ 
                                                     double* __restrict__ recs,
                                                     int32_t* __restrict__ act_ip,
                                                     int32_t* __restrict__ counts,
-                                                    double* __restrict__ tsum,
+                                                    double* __restrict__ tfrac,
                                                     double* __restrict__ fsum) {
   const int32_t o = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __shared__ int32_t wcount[kBlock / 64];
   __shared__ double red[2][kBlock];
-  int32_t base = 0, ntr = 0, nbl = 0;
+  __shared__ int32_t cnt[3][kBlock];
+  int32_t ntr = 0, nbl = 0, nnf = 0;
   double tpart = 0.0, fpart = 0.0;
+  for (int32_t ip = threadIdx.x; ip < n_pr; ip += kBlock) {
+    const int32_t f = flags[(int64_t)o * n_pr + ip];
+    const double fo = fout[ip];
+    fpart += fo;
+    if (f == 1) { tpart += fo; ++ntr; }
+    if (f == 2) ++nbl;
+    if (f == 0)
+      for (int32_t s = 0; s < n_atoms; ++s)
+        if (!__builtin_isfinite(ncol[((int64_t)s * n_orb + o) * n_pr + ip])) { ++nnf; break; }
+  }
+  red[0][threadIdx.x] = tpart;
+  red[1][threadIdx.x] = fpart;
+  cnt[0][threadIdx.x] = ntr;
+  cnt[1][threadIdx.x] = nbl;
+  cnt[2][threadIdx.x] = nnf;
+  __syncthreads();
+  for (int s = kBlock / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+      cnt[0][threadIdx.x] += cnt[0][threadIdx.x + s];
+      cnt[1][threadIdx.x] += cnt[1][threadIdx.x + s];
+      cnt[2][threadIdx.x] += cnt[2][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  const double fs = red[1][0];
   const int32_t stride = 1 + n_atoms;
+  int32_t base = 0;
   for (int32_t chunk = 0; chunk < n_pr; chunk += kBlock) {
     const int32_t ip = chunk + threadIdx.x;
-    const int32_t f = ip < n_pr ? flags[(int64_t)o * n_pr + ip] : 3;
-    if (ip < n_pr) {
-      const double fo = fout[ip];
-      fpart += fo;
-      if (f == 1) { tpart += fo; ++ntr; }
-      if (f == 2) ++nbl;
-    }
-    const bool act = (f == 0);
+    const bool act = ip < n_pr && flags[(int64_t)o * n_pr + ip] == 0;
     const unsigned long long mask = __ballot(act);
     const int32_t before = __popcll(mask & ((1ull << lane) - 1ull));
     if (lane == 0) wcount[wid] = __popcll(mask);
@@ -401,92 +434,225 @@ __global__ void __launch_bounds__(kBlock) k_compact(const int32_t* __restrict__ 
       const int32_t pos = base + wbase + before;
       act_ip[(int64_t)o * n_pr + pos] = ip;
       double* r = recs + ((int64_t)o * n_pr + pos) * stride;
-      r[0] = fout[ip];
+      r[0] = fout[ip] / fs;
       for (int32_t s = 0; s < n_atoms; ++s) r[1 + s] = ncol[((int64_t)s * n_orb + o) * n_pr + ip];
     }
     base += tot;
     __syncthreads();
   }
-  red[0][threadIdx.x] = tpart;
-  red[1][threadIdx.x] = fpart;
-  __shared__ int32_t cnt[2][kBlock];
-  cnt[0][threadIdx.x] = ntr;
-  cnt[1][threadIdx.x] = nbl;
+  if (threadIdx.x == 0) {
+    tfrac[o] = red[0][0] / fs;
+    fsum[o] = fs;
+    counts[o * 5 + 0] = base;
+    counts[o * 5 + 1] = cnt[0][0];
+    counts[o * 5 + 2] = cnt[1][0];
+    counts[o * 5 + 3] = cnt[2][0];
+    counts[o * 5 + 4] = base;   // records the tau kernel integrates (k_merge may lower it)
+  }
+}
+
+// ---- chord merging ----------------------------------------------------------------------------
+// Active chords of one phase whose column densities agree to 2^-40 relative in every species are
+// integrated once with their summed weight.  Key of a chord: the IEEE bits of N_s shifted right by
+// 12 (same key => same binade and |dN/N| < 2^-40).  For any merged chord, |tau' - tau| <= 2^-40 tau,
+// so its term changes by at most w * 2^-40 * max_tau(tau e^-tau) = w * 2^-40 / e: the whole R moves
+// by <= 3.4e-13.  Mirror-image chords (z -> -z about a body on the y axis, all built-in scenarios)
+// merge pairwise; the central phase of a symmetric grid merges whole rings.
+// One workgroup per phase; bitonic sort of (key_0, key_1, chord index) in LDS; phases with more
+// than kMergeMax active chords, or non-finite columns, are left unmerged.
+constexpr int kMergeBlock = 1024;
+constexpr int kMergeMax = 4096;
+
+__device__ __forceinline__ unsigned long long mkey(double v) {
+  return __builtin_bit_cast(unsigned long long, v) >> 12;
+}
+
+__global__ void __launch_bounds__(kMergeBlock) k_merge(const double* __restrict__ recs, int32_t n_atoms,
+                                                       int32_t n_pr, int32_t* __restrict__ counts,
+                                                       double* __restrict__ mrecs) {
+  __shared__ unsigned long long k0[kMergeMax];
+  __shared__ unsigned long long k1[kMergeMax];
+  __shared__ int32_t idx[kMergeMax];
+  __shared__ int32_t gid[kMergeMax];
+  __shared__ int32_t wsum[kMergeBlock / 64];
+  const int32_t o = blockIdx.x;
+  const int32_t n = counts[o * 5 + 0];
+  const int32_t stride = 1 + n_atoms;
+  const double* rec = recs + (int64_t)o * n_pr * stride;
+  double* out = mrecs + (int64_t)o * n_pr * stride;
+  if (n > kMergeMax || counts[o * 5 + 3] != 0 || n < 2) {
+    for (int64_t i = threadIdx.x; i < (int64_t)n * stride; i += kMergeBlock) out[i] = rec[i];
+    if (threadIdx.x == 0) counts[o * 5 + 4] = n;
+    return;
+  }
+  int32_t P = 1;
+  while (P < n) P <<= 1;
+  for (int32_t i = threadIdx.x; i < P; i += kMergeBlock) {
+    const bool v = i < n;
+    k0[i] = v ? mkey(rec[(int64_t)i * stride + 1]) : ~0ull;
+    k1[i] = (v && n_atoms > 1) ? mkey(rec[(int64_t)i * stride + 2]) : (v ? 0ull : ~0ull);
+    idx[i] = v ? i : 0x7fffffff;
+  }
   __syncthreads();
-  for (int s = kBlock / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-      cnt[0][threadIdx.x] += cnt[0][threadIdx.x + s];
-      cnt[1][threadIdx.x] += cnt[1][threadIdx.x + s];
+  for (int32_t size = 2; size <= P; size <<= 1) {
+    for (int32_t stride_ = size >> 1; stride_ > 0; stride_ >>= 1) {
+      for (int32_t t = threadIdx.x; t < P / 2; t += kMergeBlock) {
+        const int32_t i = 2 * t - (t & (stride_ - 1));
+        const int32_t j = i + stride_;
+        const bool up = (i & size) == 0;
+        const bool gt = (k0[i] > k0[j]) || (k0[i] == k0[j] && (k1[i] > k1[j] || (k1[i] == k1[j] && idx[i] > idx[j])));
+        if (gt == up) {
+          unsigned long long a = k0[i]; k0[i] = k0[j]; k0[j] = a;
+          a = k1[i]; k1[i] = k1[j]; k1[j] = a;
+          const int32_t b = idx[i]; idx[i] = idx[j]; idx[j] = b;
+        }
+      }
+      __syncthreads();
     }
+  }
+  // group heads: first of a run of equal keys in every species
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t base = 0;
+  for (int32_t c0 = 0; c0 < n; c0 += kMergeBlock) {
+    const int32_t i = c0 + threadIdx.x;
+    bool head = false;
+    if (i < n) {
+      head = (i == 0) || k0[i] != k0[i - 1] || k1[i] != k1[i - 1];
+      if (!head) {
+        const double* a = rec + (int64_t)idx[i] * stride;
+        const double* b = rec + (int64_t)idx[i - 1] * stride;
+        for (int32_t s = 2; s < n_atoms && !head; ++s) head = mkey(a[1 + s]) != mkey(b[1 + s]);
+      }
+    }
+    const unsigned long long m = __ballot(head);
+    if (lane == 0) wsum[wid] = __popcll(m);
+    __syncthreads();
+    int32_t wb = 0, tot = 0;
+    for (int w = 0; w < kMergeBlock / 64; ++w) {
+      if (w < wid) wb += wsum[w];
+      tot += wsum[w];
+    }
+    if (i < n) gid[i] = base + wb + __popcll(m & ((1ull << lane) - 1ull)) + (head ? 0 : -1);
+    base += tot;
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    tsum[o] = red[0][0];
-    fsum[o] = red[1][0];
-    counts[o * 3 + 0] = base;
-    counts[o * 3 + 1] = cnt[0][0];
-    counts[o * 3 + 2] = cnt[1][0];
+  // each head sums the weights of its run (sorted order) and writes the merged record
+  for (int32_t i = threadIdx.x; i < n; i += kMergeBlock) {
+    if (i > 0 && gid[i] == gid[i - 1]) continue;
+    const double* a = rec + (int64_t)idx[i] * stride;
+    double F = a[0];
+    for (int32_t j = i + 1; j < n && gid[j] == gid[i]; ++j) F += rec[(int64_t)idx[j] * stride];
+    double* r = out + (int64_t)gid[i] * stride;
+    r[0] = F;
+    for (int32_t s = 0; s < n_atoms; ++s) r[1 + s] = a[1 + s];
   }
+  if (threadIdx.x == 0) counts[o * 5 + 4] = base;
 }
 
-// sigma[slot][o][w] = 10^interp(shift[o] * lambda[w]) - offset     (gasProperties.py:916-917, :941-953)
-__global__ void k_sigma(const double* __restrict__ xp, const double* __restrict__ fp, int64_t n,
-                        double offset, const double* __restrict__ shift, const double* __restrict__ wav,
-                        int64_t n_wav, double* __restrict__ sig) {
-  const int32_t o = blockIdx.y;
-  const double s = shift[o];
-  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_wav;
-       w += (int64_t)gridDim.x * blockDim.x) {
-    sig[(int64_t)o * n_wav + w] = pow(10.0, np_interp(s * wav[w], xp, fp, n)) - offset;
-  }
+// ---- fast exp: acc + F * 2^(y/2048) with a 2048-entry table in LDS --------------------------------
+// y = -tau * 2048/ln2.  k = rint(y), d = y - k in [-1/2, 1/2],
+//   2^(y/2048) = 2^(k >> 11) * T[k & 2047] * exp(d ln2/2048),
+// exp(d c) = 1 + d (c + d (c^2/2 + d c^3/6)) with c = ln2/2048: truncation (c/2)^4/24 = 3.5e-17.
+// Finite y only (non-finite column densities take the exact path); y below -2^31 saturates the
+// integer conversion and ldexp flushes the term to 0, which is exp's own answer there.
+constexpr double kExpC1 = 0.0003384507717577858;     // ln2 / 2048
+constexpr double kExpC2 = 5.727446245172041e-08;     // c^2 / 2
+constexpr double kExpC3 = 6.461528672932366e-12;     // c^3 / 6
+constexpr double kMinus2048OverLn2 = -2954.639443740597;
+
+__device__ __forceinline__ double acc_exp2k(double acc, double F, double y, const double* __restrict__ tab) {
+  const double k = __builtin_rint(y);
+  const int ki = (int)k;
+  const double d = y - k;
+  double t = __builtin_fma(d, kExpC3, kExpC2);
+  t = __builtin_fma(d, t, kExpC1);
+  const double e = __builtin_fma(d, t, 1.0);
+  const double S = __builtin_amdgcn_ldexp(tab[ki & (PROM_EXP2_TABLE_N - 1)], ki >> 11);
+  return __builtin_fma(F * S, e, acc);
 }
 
-// Fused tau -> exp(-tau) -> disk sum -> ratio.  One thread per (phase o, wavelength w); the chord
-// loop is uniform across the workgroup (all threads share the phase), so the packed chord records
-// are read with scalar loads.  NS = number of atomic constituents (0 = runtime count via LDS).
-template <int NS>
-__global__ void __launch_bounds__(kBlock) k_tau(const double* __restrict__ sig,
+// sigma of one atomic slot at (phase o, wavelength w): n_interp_log at shift_o * lambda_w.
+__device__ __forceinline__ double slot_sigma(const SigTabDev& t, int32_t o, double lam) {
+  return exp10(np_interp(t.shift[o] * lam, t.x, t.y, t.n)) - t.offset;
+}
+
+__device__ __forceinline__ void fill_exp_table(double* etab) {
+  for (int i = threadIdx.x; i < PROM_EXP2_TABLE_N; i += kBlock) etab[i] = kExp2TableDev[i];
+}
+
+// Fused sigma lookup -> tau -> exp(-tau) -> disk sum -> ratio.  One thread per (phase o,
+// wavelength w); the chord loop is uniform across the workgroup (all threads share the phase), so
+// the packed chord records {lF, N_0..N_{S-1}} are read with scalar loads.
+// NS: number of atomic slots (0 = runtime count, per-thread sigma in LDS).
+// EXPK 1: table exp (exact ocml path for phases flagged non-finite);  0: ocml exp everywhere.
+template <int NS, int EXPK>
+__global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ tabs,
+                                                const double* __restrict__ wav,
                                                 const double* __restrict__ recs,
+                                                const double* __restrict__ mrecs,
+                                                const int32_t* __restrict__ act_ip,
+                                                const double* __restrict__ fout,
                                                 const int32_t* __restrict__ counts,
-                                                const double* __restrict__ tsum,
+                                                const double* __restrict__ tfrac,
                                                 const double* __restrict__ fsum, int32_t n_atoms_rt,
-                                                int32_t n_pr, int32_t n_orb, int64_t n_wav,
-                                                double* __restrict__ R) {
+                                                int32_t n_pr, int64_t n_wav, double* __restrict__ R) {
+  extern __shared__ double lds[];   // [2048] exp table | NS == 0: [n_atoms][kBlock] sigma
+  double* etab = lds;
+  double* sgl = lds + (EXPK ? PROM_EXP2_TABLE_N : 0);
+  if (EXPK) fill_exp_table(etab);
   const int32_t o = blockIdx.y;
   const int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x;
   const bool live = w < n_wav;
-  const int64_t wc = live ? w : n_wav - 1;
-  const int32_t n_act = counts[o * 3];
+  const double lam = wav[live ? w : n_wav - 1];
+  const bool exact = !EXPK || counts[o * 5 + 3] != 0;
+  const int32_t n_act = counts[o * 5 + (exact ? 0 : 4)];
+  const int32_t ns = NS > 0 ? NS : n_atoms_rt;
+  const int32_t stride = 1 + ns;
+  const double* __restrict__ rec = (exact ? recs : mrecs) + (int64_t)o * n_pr * stride;
+  const double scale = exact ? 1.0 : kMinus2048OverLn2;
   double acc = 0.0;
+  double sp[NS > 0 ? NS : 1];
   if constexpr (NS > 0) {
-    constexpr int stride = 1 + NS;
-    double sg[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) sg[s] = sig[((int64_t)s * n_orb + o) * n_wav + wc];
-    const double* __restrict__ rec = recs + (int64_t)o * n_pr * stride;
-    for (int32_t i = 0; i < n_act; ++i) {
-      const double* r = rec + (int64_t)i * stride;
-      double tau = r[1] * sg[0];
-#pragma unroll
-      for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[s];
-      acc = acc + r[0] * exp(-tau);
-    }
+    for (int s = 0; s < NS; ++s) sp[s] = slot_sigma(tabs[s], o, lam) * scale;
   } else {
-    extern __shared__ double sgl[];  // [n_atoms][kBlock]
-    const int32_t ns = n_atoms_rt;
-    const int32_t stride = 1 + ns;
-    for (int32_t s = 0; s < ns; ++s) sgl[s * kBlock + threadIdx.x] = sig[((int64_t)s * n_orb + o) * n_wav + wc];
-    const double* __restrict__ rec = recs + (int64_t)o * n_pr * stride;
+    for (int32_t s = 0; s < ns; ++s) sgl[s * kBlock + threadIdx.x] = slot_sigma(tabs[s], o, lam) * scale;
+  }
+  __syncthreads();
+  if (!exact) {
     for (int32_t i = 0; i < n_act; ++i) {
       const double* r = rec + (int64_t)i * stride;
-      double tau = r[1] * sgl[threadIdx.x];
-      for (int32_t s = 1; s < ns; ++s) tau = tau + r[1 + s] * sgl[s * kBlock + threadIdx.x];
-      acc = acc + r[0] * exp(-tau);
+      double y;
+      if constexpr (NS > 0) {
+        y = r[1] * sp[0];
+#pragma unroll
+        for (int s = 1; s < NS; ++s) y = __builtin_fma(r[1 + s], sp[s], y);
+      } else {
+        y = r[1] * sgl[threadIdx.x];
+        for (int32_t s = 1; s < ns; ++s) y = __builtin_fma(r[1 + s], sgl[s * kBlock + threadIdx.x], y);
+      }
+      acc = acc_exp2k(acc, r[0], y, etab);
     }
+    if (live) R[(int64_t)o * n_wav + w] = acc + tfrac[o];
+  } else {
+    // exact path: tau in the reference's order (products then sums), ocml exp, F_out weights
+    const int32_t* ipl = act_ip + (int64_t)o * n_pr;
+    for (int32_t i = 0; i < n_act; ++i) {
+      const double* r = rec + (int64_t)i * stride;
+      double tau;
+      if constexpr (NS > 0) {
+        tau = r[1] * sp[0];
+#pragma unroll
+        for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sp[s];
+      } else {
+        tau = r[1] * sgl[threadIdx.x];
+        for (int32_t s = 1; s < ns; ++s) tau = tau + r[1 + s] * sgl[s * kBlock + threadIdx.x];
+      }
+      acc = acc + fout[ipl[i]] * exp(-tau);
+    }
+    if (live) R[(int64_t)o * n_wav + w] = (acc + tfrac[o] * fsum[o]) / fsum[o];
+    (void)rec;
   }
-  if (live) R[(int64_t)o * n_wav + w] = (acc + tsum[o]) / fsum[o];
 }
 
 void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>& tables,
@@ -519,37 +685,45 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
                      tr.recs.as<double>(), tr.act_ip.as<int32_t>(), tr.counts.as<int32_t>(),
                      tr.tsum.as<double>(), tr.fsum.as<double>());
   PROM_HIP(hipGetLastError());
-  PROM_HIP(hipEventRecord(ev[1], s));
-  // 2. sigma resample
-  for (const auto& t : tr.terms) {
-    if (t.is_molecule) continue;
-    const AtomTable& tb = tables[t.table];
-    dim3 g(grid_for(tr.n_wav, kBlock, 65535), tr.n_orb);
-    hipLaunchKernelGGL(k_sigma, g, dim3(kBlock), 0, s, tb.x.as<double>(), tb.y.as<double>(), tb.n, tb.offset,
-                       tr.shift.as<double>() + (int64_t)t.scenario * tr.n_orb, tr.wav.as<double>(), tr.n_wav,
-                       tr.sigma.as<double>() + (int64_t)t.slot * tr.n_orb * tr.n_wav);
+  if (tr.merge && tr.exp_mode) {
+    hipLaunchKernelGGL(k_merge, dim3(tr.n_orb), dim3(kMergeBlock), 0, s, tr.recs.as<double>(), tr.n_atoms,
+                       tr.n_pr, tr.counts.as<int32_t>(), tr.mrecs.as<double>());
     PROM_HIP(hipGetLastError());
   }
+  PROM_HIP(hipEventRecord(ev[1], s));
+  // 2. (sigma is fused into the tau kernel; the event pair brackets nothing since round 1.2)
   PROM_HIP(hipEventRecord(ev[2], s));
-  // 3. fused tau kernel
+  // 3. fused sigma -> tau -> exp -> disk-sum kernel
   dim3 g((unsigned)((tr.n_wav + kBlock - 1) / kBlock), tr.n_orb);
-  const double* sig = tr.sigma.as<double>();
+  const SigTabDev* tabs = tr.sigtab.as<SigTabDev>();
+  const double* wav = tr.wav.as<double>();
   const double* recs = tr.recs.as<double>();
+  const double* mrecs = (tr.merge && tr.exp_mode) ? tr.mrecs.as<double>() : recs;
+  const int32_t* aip = tr.act_ip.as<int32_t>();
+  const double* fo = tr.cfout.as<double>();
   const int32_t* counts = tr.counts.as<int32_t>();
-  const double* ts = tr.tsum.as<double>();
+  const double* tf = tr.tsum.as<double>();
   const double* fs = tr.fsum.as<double>();
   double* R = tr.R.as<double>();
-  switch (tr.n_atoms) {
-    case 1: hipLaunchKernelGGL(k_tau<1>, g, dim3(kBlock), 0, s, sig, recs, counts, ts, fs, 1, tr.n_pr, tr.n_orb, tr.n_wav, R); break;
-    case 2: hipLaunchKernelGGL(k_tau<2>, g, dim3(kBlock), 0, s, sig, recs, counts, ts, fs, 2, tr.n_pr, tr.n_orb, tr.n_wav, R); break;
-    case 3: hipLaunchKernelGGL(k_tau<3>, g, dim3(kBlock), 0, s, sig, recs, counts, ts, fs, 3, tr.n_pr, tr.n_orb, tr.n_wav, R); break;
-    case 4: hipLaunchKernelGGL(k_tau<4>, g, dim3(kBlock), 0, s, sig, recs, counts, ts, fs, 4, tr.n_pr, tr.n_orb, tr.n_wav, R); break;
-    default:
-      hipLaunchKernelGGL(k_tau<0>, g, dim3(kBlock), (size_t)tr.n_atoms * kBlock * sizeof(double), s, sig, recs,
-                         counts, ts, fs, tr.n_atoms, tr.n_pr, tr.n_orb, tr.n_wav, R);
+  const int na = tr.n_atoms;
+#define PROM_TAU(NSV, EK)                                                                              \
+  hipLaunchKernelGGL((k_tau<NSV, EK>), g, dim3(kBlock),                                                \
+                     ((EK) ? PROM_EXP2_TABLE_N * sizeof(double) : 0) +                                  \
+                         ((NSV) == 0 ? (size_t)na * kBlock * sizeof(double) : 0),                      \
+                     s, tabs, wav, recs, mrecs, aip, fo, counts, tf, fs, na, tr.n_pr, tr.n_wav, R)
+#define PROM_TAU_NS(EK)                 \
+  switch (na) {                         \
+    case 1: PROM_TAU(1, EK); break;     \
+    case 2: PROM_TAU(2, EK); break;     \
+    case 3: PROM_TAU(3, EK); break;     \
+    case 4: PROM_TAU(4, EK); break;     \
+    default: PROM_TAU(0, EK);           \
   }
+  if (tr.exp_mode) { PROM_TAU_NS(1) } else { PROM_TAU_NS(0) }
+#undef PROM_TAU_NS
+#undef PROM_TAU
   PROM_HIP(hipGetLastError());
-  *variant = tr.n_atoms <= 4 ? tr.n_atoms : 0;
+  *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? 10 : 0);
   PROM_HIP(hipEventRecord(ev[3], s));
 }
 

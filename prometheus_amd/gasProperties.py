@@ -556,7 +556,8 @@ class Transit:
                 "moon_y": np.array([m.getPosition(orb)[1] for m in moons]).reshape(len(moons), len(orb)),
                 "moon_R": np.array([m.R for m in moons], dtype=np.float64), "scenarios": scen}
 
-    def _problem(self, dev, host: dict, w0: int, w1: int, cull_tau: float) -> "_native.TransitInputs":
+    def _problem(self, dev, host: dict, w0: int, w1: int, cull_tau: float,
+                 options: int = 0) -> "_native.TransitInputs":
         scs = []
         for e in host["scenarios"]:
             cons = []
@@ -570,10 +571,10 @@ class Transit:
             wavelength=self.wavelength[w0:w1], chord_y=host["y"], chord_z=host["z"], chord_fout=host["fout"],
             n_orb=len(host["orb"]), x=host["x"], delta_x=host["dx"], planet_y=host["planet_y"],
             planet_R=host["planet_R"], moon_y=host["moon_y"], moon_R=host["moon_R"], scenarios=scs,
-            cull_tau=cull_tau)
+            cull_tau=cull_tau, options=options)
 
     def sumOverChords(self, max_memory_gb: float = 2.0, devices: Optional[Sequence[int]] = None,
-                      cull_tau: float = 0.0) -> np.ndarray:
+                      cull_tau: float = 0.0, options: int = 0) -> np.ndarray:
         """R[n_orb, n_wav] = sum_chords F_out exp(-tau) / sum_chords F_out, on the GPU(s).
 
         ``devices``: GPU ids to shard the wavelength axis over (default: all visible GPUs when
@@ -604,7 +605,7 @@ class Transit:
                 with dev.lock:
                     for a in range(lo, hi, chunk):
                         b = min(hi, a + chunk)
-                        dev.transit_set(self._problem(dev, host, a, b, cull_tau))
+                        dev.transit_set(self._problem(dev, host, a, b, cull_tau, options))
                         st = dev.transit_run(stats=True)
                         R[:, a:b] = dev.transit_result()
                         st.update(device=dev_id, w0=a, w1=b)

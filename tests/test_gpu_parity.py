@@ -126,6 +126,36 @@ def test_transit_golden(dev, name):
     assert err < R_TOL
 
 
+@pytest.mark.parametrize("name", ["C2r", "C3r", "C4r"])
+def test_transit_ocml_exp_mode(dev, name):
+    """The validation build of the tau kernel (ocml exp) agrees with the table exp and the reference."""
+    from prometheus_amd import _native
+    d = load("transit_" + name)
+    tr = _product_transit(json.loads(str(d["config"])))
+    R_tab = tr.sumOverChords(devices=[0])
+    R_ocml = tr.sumOverChords(devices=[0], options=_native.OPT_OCML_EXP)
+    assert rel(R_ocml, d["R"]) < R_TOL and rel(R_tab, d["R"]) < R_TOL
+    assert rel(R_tab, R_ocml) < 1e-13
+
+
+@pytest.mark.parametrize("name", ["C1", "C2r", "C4r", "exomoon"])
+def test_chord_merging(dev, name):
+    """Merging chords with equal (2^-40) column densities moves R by <= 2^-40/e."""
+    from prometheus_amd import _native
+    d = load("transit_" + name)
+    tr = _product_transit(json.loads(str(d["config"])))
+    R_m = tr.sumOverChords(devices=[0])
+    st_m = tr.last_stats[-1]
+    R_n = tr.sumOverChords(devices=[0], options=_native.OPT_NO_MERGE)
+    st_n = tr.last_stats[-1]
+    assert np.max(np.abs(R_m - R_n)) <= 2.0 ** -40 / np.e + 1e-15
+    assert st_n["tau_records"] == st_n["active_chords"]
+    assert st_m["tau_records"] <= st_m["active_chords"]
+    print(name, "records merged %d -> %d" % (st_m["active_chords"], st_m["tau_records"]))
+    if name == "C1":   # one phase with the planet at the disk centre: whole rings merge
+        assert st_m["tau_records"] * 10 < st_m["active_chords"]
+
+
 def test_sharding_bitwise(dev):
     """Wavelength shards (1, 2, 3 ways; emulated on one GPU) give bitwise-identical R."""
     d = load("transit_C2r")
