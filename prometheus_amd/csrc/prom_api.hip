@@ -145,7 +145,7 @@ int32_t prom_table_build_voigt(prom_ctx* ctx, int64_t n, const double* x, int32_
     prom::launch_voigt(ctx->stream, t.x.as<double>(), n, ctx->scratch[1].as<double>(),
                        ctx->scratch[2].as<double>(), ctx->scratch[3].as<double>(), n_lines, sigma_v, c_light,
                        offset, 1, t.y.as<double>());
-    ctx->scratch[4].ensure(sizeof(double));
+    ctx->scratch[4].ensure(sizeof(double) * 1024);
     t.ymax = prom::reduce_max(ctx->stream, t.y.as<double>(), n, ctx->scratch[4].as<double>());
     t.n = n;
     t.offset = offset;
@@ -354,6 +354,14 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       upload(tr.sigtab, st.data(), (int64_t)st.size(), s);
     }
     tr.tab.ensure(sizeof(double) * std::max<int64_t>(tab_total, 1));
+    {
+      std::vector<prom::ScDevHost> sd(tr.n_sc);
+      for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
+        sd[sc].m = tr.dens[sc];
+        sd[sc].tab = tr.tab_off[sc] >= 0 ? tr.tab.as<double>() + tr.tab_off[sc] : nullptr;
+      }
+      upload(tr.scdev, sd.data(), (int64_t)sd.size(), s);
+    }
     for (int32_t sc = 0; sc < tr.n_sc; ++sc)
       if (tr.tab_off[sc] >= 0)
         PROM_HIP(hipMemcpyAsync(tr.tab.as<double>() + tr.tab_off[sc], pb->scenarios[sc].n_tabulated,
@@ -366,7 +374,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.flags.ensure(sizeof(int32_t) * nc);
     tr.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
     tr.act_ip.ensure(sizeof(int32_t) * nc);
-    tr.counts.ensure(sizeof(int32_t) * n_orb * 5);
+    tr.counts.ensure(sizeof(int32_t) * n_orb * 6);
     tr.mrecs.ensure(sizeof(double) * nc * (1 + n_atoms));
     tr.tsum.ensure(sizeof(double) * n_orb);
     tr.fsum.ensure(sizeof(double) * n_orb);
@@ -407,16 +415,16 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
       stats->ms_sigma = b;
       stats->ms_tau = c;
       stats->ms_total = t;
-      std::vector<int32_t> cnt(tr.n_orb * 5);
+      std::vector<int32_t> cnt(tr.n_orb * 6);
       download(cnt.data(), tr.counts, (int64_t)cnt.size(), ctx->stream);
       PROM_HIP(hipStreamSynchronize(ctx->stream));
       for (int32_t o = 0; o < tr.n_orb; ++o) {
-        const bool exact_phase = cnt[o * 5 + 3] != 0 || !tr.exp_mode;
-        stats->active_chords += cnt[o * 5];
-        stats->transparent_chords += cnt[o * 5 + 1];
-        stats->blocked_chords += cnt[o * 5 + 2];
-        stats->tau_records += exact_phase ? cnt[o * 5] : cnt[o * 5 + 4];
-        if (cnt[o * 5 + 3]) stats->tau_kernel_variant_exact_phases += 1;
+        const bool merged = cnt[o * 6 + 5] != 0;
+        stats->active_chords += cnt[o * 6];
+        stats->transparent_chords += cnt[o * 6 + 1];
+        stats->blocked_chords += cnt[o * 6 + 2];
+        stats->tau_records += merged ? cnt[o * 6 + 4] : cnt[o * 6];
+        if (cnt[o * 6 + 3]) stats->tau_kernel_variant_exact_phases += 1;
       }
       stats->chord_lambda_evals = stats->active_chords * tr.n_wav;
       stats->exp_evals = stats->tau_records * tr.n_wav;

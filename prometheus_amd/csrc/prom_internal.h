@@ -64,6 +64,12 @@ struct DensityDev {
   double p[8];
 };
 
+// Per-scenario view for the streaming column kernel (layout shared with prom_kernels.hip's ScDev).
+struct ScDevHost {
+  DensityDev m;
+  const double* tab;
+};
+
 // Device-side descriptor of one absorbing constituent inside the transit problem.
 struct TermDev {
   int32_t scenario;     // index of its density scenario
@@ -113,6 +119,7 @@ struct TransitDev {
   DevBuf wav, cy, cz, cfout, x, planet_y, moon_y, moon_R;
   DevBuf body_x, body_y, shift;             // [n_sc][n_orb]
   DevBuf dens_dev;                          // [n_sc] DensityDev
+  DevBuf scdev;                             // [n_sc] ScDev (density + tabulated pointer)
   DevBuf terms_dev;                         // [n_terms] TermDev
   DevBuf tab;                               // tabulated densities, raw host order, concatenated
   DevBuf ntot;                              // [n_sc][n_orb][n_pr][n_x]
@@ -121,7 +128,8 @@ struct TransitDev {
   DevBuf flags;                             // [n_orb][n_pr] int32: 0 active, 1 transparent, 2 blocked
   DevBuf recs;                              // [n_orb][n_pr][1 + n_atoms] {log2(F/Fsum)*2048, N_s}
   DevBuf act_ip;                            // [n_orb][n_pr] int32 chord positions of active chords
-  DevBuf counts;                            // [n_orb][5] int32: active, transparent, blocked, nonfinite, records
+  DevBuf counts;                            // [n_orb][6] int32: active, transparent, blocked, nonfinite,
+                                            //   records, merged
   DevBuf tsum;                              // [n_orb] transparent flux sum / F_out sum
   DevBuf fsum;                              // [n_orb] F_out sum
   DevBuf sigma;                             // [n_atoms][n_orb][n_wav]

@@ -9,11 +9,11 @@
 //   k_mol_sigma      MolecularConstituent.getSigmaAbs        gasProperties.py:789-818
 //   transit pipeline Transit.sumOverChords + getLOSopticalDepth_Batch (gasProperties.py:885-956,
 //                    :1160-1258):
-//     k_ntot      n(c, x) for every scenario, chord and line-of-sight sample
-//     k_columns   blocking masks, column densities N = sum_x(n chi) dx (numpy pairwise order),
-//                 tau upper bound per chord -> active / transparent / blocked
-//     k_compact   per phase, in chord order: packed records of the active chords, transparent
-//                 and total F_out sums
+//     k_columns_lanes   blocking masks, densities evaluated on the fly, column densities
+//                 N = sum_x(n chi) dx (numpy pairwise order), tau upper bound -> active /
+//                 transparent / blocked  (k_ntot + k_columns when densities must be stored)
+//     k_chords    per phase: F_out and transparent sums, compaction of the active chords in chord
+//                 order, merging of chords with equal (2^-40) column densities
 //     k_tau<NS>   per (phase, wavelength): sigma_s = 10^interp(shift_o * lambda_w) - offset for each
 //                 species, then tau over the active chords, exp(-tau), disk sum, ratio
 #include "exp2_table.h"
@@ -49,6 +49,45 @@ __device__ __forceinline__ double np_interp(double t, const double* __restrict__
     const int64_t mid = (lo + hi) >> 1;
     if (xp[mid] <= t) lo = mid; else hi = mid;
   }
+  if (xp[lo] == t) return fp[lo];
+  const double slope = (fp[lo + 1] - fp[lo]) / (xp[lo + 1] - xp[lo]);
+  double r = slope * (t - xp[lo]) + fp[lo];
+  if (r != r) {
+    r = slope * (t - xp[lo + 1]) + fp[lo + 1];
+    if (r != r && fp[lo] == fp[lo + 1]) r = fp[lo];
+  }
+  return r;
+}
+
+// np_interp with a bracket hint: the same index j (largest j <= n-2 with xp[j] <= t, the unique
+// bracket numpy's search returns) found by galloping from the previous target's bracket.  Used when
+// one thread interpolates a sequence of nearby targets (the same wavelength at successive phases).
+__device__ __forceinline__ double np_interp_hint(double t, const double* __restrict__ xp,
+                                                 const double* __restrict__ fp, int64_t n, int64_t& hint) {
+  if (t != t) return t;
+  if (n == 1) return fp[0];
+  if (t < xp[0]) return fp[0];
+  if (t > xp[n - 1]) return fp[n - 1];
+  if (t == xp[n - 1]) return fp[n - 1];
+  int64_t lo, hi;   // invariant xp[lo] <= t < xp[hi]
+  if (hint < 0 || hint > n - 2) {
+    lo = 0; hi = n - 1;
+  } else if (xp[hint] <= t) {
+    lo = hint;
+    int64_t step = 1;
+    hi = lo + 1;
+    while (hi < n - 1 && xp[hi] <= t) { lo = hi; step <<= 1; hi = lo + step; if (hi > n - 1) hi = n - 1; }
+  } else {
+    hi = hint;
+    int64_t step = 1;
+    lo = hi - 1;
+    while (lo > 0 && xp[lo] > t) { hi = lo; step <<= 1; lo = hi - step; if (lo < 0) lo = 0; }
+  }
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (xp[mid] <= t) lo = mid; else hi = mid;
+  }
+  hint = lo;
   if (xp[lo] == t) return fp[lo];
   const double slope = (fp[lo + 1] - fp[lo]) / (xp[lo + 1] - xp[lo]);
   double r = slope * (t - xp[lo]) + fp[lo];
@@ -273,7 +312,7 @@ void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, 
 __global__ void k_max(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
   __shared__ double sm[kBlock];
   double m = -INFINITY;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const double a = v[i];
     m = (a > m || a != a) ? a : m;
   }
@@ -286,16 +325,20 @@ __global__ void k_max(const double* __restrict__ v, int64_t n, double* __restric
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *out = sm[0];
+  if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
 }
 
+// max (NaN-propagating) of a device array; scratch_dev must hold 1024 doubles
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev) {
-  hipLaunchKernelGGL(k_max, dim3(1), dim3(kBlock), 0, s, v, n, scratch_dev);
+  const unsigned g = grid_for(n, kBlock, 1024);
+  hipLaunchKernelGGL(k_max, dim3(g), dim3(kBlock), 0, s, v, n, scratch_dev);
   PROM_HIP(hipGetLastError());
-  double h = 0.0;
-  PROM_HIP(hipMemcpyAsync(&h, scratch_dev, sizeof(double), hipMemcpyDeviceToHost, s));
+  std::vector<double> h(g);
+  PROM_HIP(hipMemcpyAsync(h.data(), scratch_dev, sizeof(double) * g, hipMemcpyDeviceToHost, s));
   PROM_HIP(hipStreamSynchronize(s));
-  return h;
+  double m = -INFINITY;
+  for (double a : h) m = (a > m || a != a) ? a : m;
+  return m;
 }
 
 // ------------------------------------------------------------------ transit pipeline
@@ -367,88 +410,75 @@ __global__ void k_columns(const TermDev* __restrict__ terms, int32_t n_terms,
   }
 }
 
-// One workgroup per phase.  Pass 1: F_out sum, transparent sum and the counts.  Pass 2: stream
-// compaction of the active chords in chord order into packed records
-//   {F_out / F_out_sum, N_0, .., N_{S-1}}
-// (so R = sum_active w_c exp(-tau_c) + transparent fraction), their chord positions, and a flag
-// for non-finite column densities (the tau kernel then takes the exact ocml path for that phase).
-// counts[o] = {active, transparent, blocked, nonfinite, records}; tfrac[o] = transparent sum / F_out sum.
-__global__ void __launch_bounds__(kBlock) k_compact(const int32_t* __restrict__ flags,
-                                                    const double* __restrict__ fout,
-                                                    const double* __restrict__ ncol, int32_t n_atoms,
-                                                    int32_t n_pr, int32_t n_orb,
-                                                    double* __restrict__ recs,
-                                                    int32_t* __restrict__ act_ip,
-                                                    int32_t* __restrict__ counts,
-                                                    double* __restrict__ tfrac,
-                                                    double* __restrict__ fsum) {
-  const int32_t o = blockIdx.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  __shared__ int32_t wcount[kBlock / 64];
-  __shared__ double red[2][kBlock];
-  __shared__ int32_t cnt[3][kBlock];
-  int32_t ntr = 0, nbl = 0, nnf = 0;
-  double tpart = 0.0, fpart = 0.0;
-  for (int32_t ip = threadIdx.x; ip < n_pr; ip += kBlock) {
-    const int32_t f = flags[(int64_t)o * n_pr + ip];
-    const double fo = fout[ip];
-    fpart += fo;
-    if (f == 1) { tpart += fo; ++ntr; }
-    if (f == 2) ++nbl;
-    if (f == 0)
-      for (int32_t s = 0; s < n_atoms; ++s)
-        if (!__builtin_isfinite(ncol[((int64_t)s * n_orb + o) * n_pr + ip])) { ++nnf; break; }
+// Per-scenario device view for the streaming column kernel (tab: TABULATED n[(ip*n_orb+o)*n_x+ix]).
+using ScDev = ScDevHost;
+
+// Blocking masks + column densities + transparency culling in one pass for atomic-only problems with
+// n_x <= 64: a group of L = pow2 >= n_x lanes owns one chord, lane i evaluates n(x_i) * chi into LDS,
+// lanes 0..7 form numpy's eight pairwise partial sums, lane 0 combines them (loops_utils.h.src order)
+// -> N = (0.0 + pairwise_x(n chi)) * delta_x exactly as gasProperties.py:940.  The k_ntot + k_columns
+// pair handles molecular terms and n_x > 64.
+template <int L>
+__global__ void __launch_bounds__(kBlock) k_columns_lanes(const TermDev* __restrict__ terms, int32_t n_terms,
+                                 const ScDev* __restrict__ scs, const double* __restrict__ x, int32_t n_x,
+                                 int32_t n_pr, int32_t n_orb, double delta_x, const double* __restrict__ cy,
+                                 const double* __restrict__ cz, const double* __restrict__ bx,
+                                 const double* __restrict__ by, const double* __restrict__ planet_y,
+                                 double planet_R, int32_t n_moons, const double* __restrict__ moon_y,
+                                 const double* __restrict__ moon_R, const double* __restrict__ sig_max,
+                                 double cull, double* __restrict__ ncol, int32_t* __restrict__ flags) {
+  constexpr int G = kBlock / L;         // chords per workgroup
+  __shared__ double av[G][L];
+  __shared__ double part[G][8];
+  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
+  const int64_t nc = (int64_t)n_orb * n_pr;
+  const int64_t c = (int64_t)blockIdx.x * G + grp;
+  const bool valid = c < nc;
+  const int32_t ip = valid ? (int32_t)(c % n_pr) : 0;
+  const int32_t o = valid ? (int32_t)(c / n_pr) : 0;
+  const double y = cy[ip], z = cz[ip];
+  const double dyp = y - planet_y[o];
+  bool blocked = sqrt(dyp * dyp + z * z) < planet_R;
+  for (int32_t m = 0; m < n_moons; ++m) {
+    const double dym = y - moon_y[m * n_orb + o];
+    blocked = blocked || ((dym * dym + z * z) < moon_R[m] * moon_R[m]);
   }
-  red[0][threadIdx.x] = tpart;
-  red[1][threadIdx.x] = fpart;
-  cnt[0][threadIdx.x] = ntr;
-  cnt[1][threadIdx.x] = nbl;
-  cnt[2][threadIdx.x] = nnf;
-  __syncthreads();
-  for (int s = kBlock / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
-      cnt[0][threadIdx.x] += cnt[0][threadIdx.x + s];
-      cnt[1][threadIdx.x] += cnt[1][threadIdx.x + s];
-      cnt[2][threadIdx.x] += cnt[2][threadIdx.x + s];
+  const int32_t lim = n_x - (n_x % 8);
+  double bound = 0.0;
+  for (int32_t t = 0; t < n_terms; ++t) {
+    const TermDev td = terms[t];
+    const ScDev sc = scs[td.scenario];
+    double a = 0.0;
+    if (valid && !blocked && lane < n_x) {
+      const double nv = sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + lane]
+                               : density_at(sc.m, x[lane], y, z, bx[td.scenario * n_orb + o], by[td.scenario * n_orb + o]);
+      a = nv * td.chi;
+    }
+    av[grp][lane] = a;
+    __syncthreads();
+    if (lane < 8 && n_x >= 8) {
+      double r = av[grp][lane];
+      for (int32_t i = 8 + lane; i < lim; i += 8) r += av[grp][i];
+      part[grp][lane] = r;
+    }
+    __syncthreads();
+    if (lane == 0 && valid) {
+      double res;
+      if (n_x < 8) {
+        res = 0.0;
+        for (int32_t i = 0; i < n_x; ++i) res += av[grp][i];
+      } else {
+        res = ((part[grp][0] + part[grp][1]) + (part[grp][2] + part[grp][3])) +
+              ((part[grp][4] + part[grp][5]) + (part[grp][6] + part[grp][7]));
+        for (int32_t i = lim; i < n_x; ++i) res += av[grp][i];
+      }
+      const double N = blocked ? 0.0 : (0.0 + res) * delta_x;
+      ncol[((int64_t)td.slot * n_orb + o) * n_pr + ip] = N;
+      bound += N * sig_max[td.slot];
     }
     __syncthreads();
   }
-  const double fs = red[1][0];
-  const int32_t stride = 1 + n_atoms;
-  int32_t base = 0;
-  for (int32_t chunk = 0; chunk < n_pr; chunk += kBlock) {
-    const int32_t ip = chunk + threadIdx.x;
-    const bool act = ip < n_pr && flags[(int64_t)o * n_pr + ip] == 0;
-    const unsigned long long mask = __ballot(act);
-    const int32_t before = __popcll(mask & ((1ull << lane) - 1ull));
-    if (lane == 0) wcount[wid] = __popcll(mask);
-    __syncthreads();
-    int32_t wbase = 0, tot = 0;
-    for (int w = 0; w < kBlock / 64; ++w) {
-      if (w < wid) wbase += wcount[w];
-      tot += wcount[w];
-    }
-    if (act) {
-      const int32_t pos = base + wbase + before;
-      act_ip[(int64_t)o * n_pr + pos] = ip;
-      double* r = recs + ((int64_t)o * n_pr + pos) * stride;
-      r[0] = fout[ip] / fs;
-      for (int32_t s = 0; s < n_atoms; ++s) r[1 + s] = ncol[((int64_t)s * n_orb + o) * n_pr + ip];
-    }
-    base += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    tfrac[o] = red[0][0] / fs;
-    fsum[o] = fs;
-    counts[o * 5 + 0] = base;
-    counts[o * 5 + 1] = cnt[0][0];
-    counts[o * 5 + 2] = cnt[1][0];
-    counts[o * 5 + 3] = cnt[2][0];
-    counts[o * 5 + 4] = base;   // records the tau kernel integrates (k_merge may lower it)
-  }
+  if (lane == 0 && valid) flags[c] = blocked ? 2 : ((bound <= cull) ? 1 : 0);
 }
 
 // ---- chord merging ----------------------------------------------------------------------------
@@ -460,93 +490,202 @@ __global__ void __launch_bounds__(kBlock) k_compact(const int32_t* __restrict__ 
 // merge pairwise; the central phase of a symmetric grid merges whole rings.
 // One workgroup per phase; bitonic sort of (key_0, key_1, chord index) in LDS; phases with more
 // than kMergeMax active chords, or non-finite columns, are left unmerged.
-constexpr int kMergeBlock = 1024;
-constexpr int kMergeMax = 4096;
-
 __device__ __forceinline__ unsigned long long mkey(double v) {
   return __builtin_bit_cast(unsigned long long, v) >> 12;
 }
 
-__global__ void __launch_bounds__(kMergeBlock) k_merge(const double* __restrict__ recs, int32_t n_atoms,
-                                                       int32_t n_pr, int32_t* __restrict__ counts,
-                                                       double* __restrict__ mrecs) {
-  __shared__ unsigned long long k0[kMergeMax];
-  __shared__ unsigned long long k1[kMergeMax];
-  __shared__ int32_t idx[kMergeMax];
-  __shared__ int32_t gid[kMergeMax];
-  __shared__ int32_t wsum[kMergeBlock / 64];
-  const int32_t o = blockIdx.x;
-  const int32_t n = counts[o * 5 + 0];
-  const int32_t stride = 1 + n_atoms;
-  const double* rec = recs + (int64_t)o * n_pr * stride;
-  double* out = mrecs + (int64_t)o * n_pr * stride;
-  if (n > kMergeMax || counts[o * 5 + 3] != 0 || n < 2) {
-    for (int64_t i = threadIdx.x; i < (int64_t)n * stride; i += kMergeBlock) out[i] = rec[i];
-    if (threadIdx.x == 0) counts[o * 5 + 4] = n;
-    return;
-  }
-  int32_t P = 1;
-  while (P < n) P <<= 1;
-  for (int32_t i = threadIdx.x; i < P; i += kMergeBlock) {
-    const bool v = i < n;
-    k0[i] = v ? mkey(rec[(int64_t)i * stride + 1]) : ~0ull;
-    k1[i] = (v && n_atoms > 1) ? mkey(rec[(int64_t)i * stride + 2]) : (v ? 0ull : ~0ull);
-    idx[i] = v ? i : 0x7fffffff;
+// ---- per-phase chord bookkeeping: compaction + merging in one workgroup ----------------------------
+// Pass 1: F_out sum, transparent sum, counts, non-finite check.  Pass 2: compaction of the active
+// chords in chord order into records {F_out / F_out_sum, N_0..N_{S-1}} (recs, act_ip: the exact path
+// and the unmerged fast path).  Pass 3 (merging, see k_merge's comment for the bound): LDS bitonic sort
+// of (key_0, key_1, position), group heads, one merged record per group (mrecs).
+// counts[o] = {active, transparent, blocked, nonfinite, records, merged}.
+constexpr int kChordBlock = 1024;
+constexpr int kChordMergeMax = 2048;
+
+// inclusive/exclusive scan of v over the workgroup; returns the exclusive prefix, *total = sum
+__device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* wsum, int32_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t inc = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t u = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += u;
   }
   __syncthreads();
-  for (int32_t size = 2; size <= P; size <<= 1) {
-    for (int32_t stride_ = size >> 1; stride_ > 0; stride_ >>= 1) {
-      for (int32_t t = threadIdx.x; t < P / 2; t += kMergeBlock) {
-        const int32_t i = 2 * t - (t & (stride_ - 1));
-        const int32_t j = i + stride_;
-        const bool up = (i & size) == 0;
-        const bool gt = (k0[i] > k0[j]) || (k0[i] == k0[j] && (k1[i] > k1[j] || (k1[i] == k1[j] && idx[i] > idx[j])));
-        if (gt == up) {
-          unsigned long long a = k0[i]; k0[i] = k0[j]; k0[j] = a;
-          a = k1[i]; k1[i] = k1[j]; k1[j] = a;
-          const int32_t b = idx[i]; idx[i] = idx[j]; idx[j] = b;
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  int32_t wb = 0, tot = 0;
+  for (int w = 0; w < kChordBlock / 64; ++w) {
+    if (w < wid) wb += wsum[w];
+    tot += wsum[w];
+  }
+  *total = tot;
+  return wb + inc - v;
+}
+
+constexpr int kChordPer = 4;   // chords per thread held in registers (n_pr <= 4096 in one sweep)
+
+__global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restrict__ flags,
+                                                        const double* __restrict__ fout,
+                                                        const double* __restrict__ ncol, int32_t n_atoms,
+                                                        int32_t n_pr, int32_t n_orb, int32_t merge,
+                                                        double* __restrict__ recs,
+                                                        int32_t* __restrict__ act_ip,
+                                                        double* __restrict__ mrecs,
+                                                        int32_t* __restrict__ counts,
+                                                        double* __restrict__ tfrac,
+                                                        double* __restrict__ fsum) {
+  __shared__ double redd[2][kChordBlock / 64];
+  __shared__ int32_t redi[kChordBlock / 64];
+  __shared__ int32_t redc[3][kChordBlock / 64];
+  __shared__ double Fl[kChordMergeMax];
+  __shared__ unsigned long long k0[kChordMergeMax];
+  __shared__ unsigned long long k1[kChordMergeMax];
+  __shared__ int32_t idx[kChordMergeMax];
+  __shared__ int32_t gid[kChordMergeMax];
+  const int32_t o = blockIdx.x;
+  const int32_t stride = 1 + n_atoms;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // this thread's contiguous chords: [c_lo, c_hi); sweeps of kChordBlock*kChordPer chords
+  const int32_t per_sweep = kChordBlock * kChordPer;
+  double fpart = 0.0, tpart = 0.0;
+  int32_t ntr = 0, nbl = 0, nnf = 0;
+  for (int32_t sw = 0; sw < n_pr; sw += per_sweep) {
+    const int32_t lo = sw + threadIdx.x * kChordPer;
+#pragma unroll
+    for (int k = 0; k < kChordPer; ++k) {
+      const int32_t ip = lo + k;
+      if (ip >= n_pr || ip >= sw + per_sweep) break;
+      const int32_t f = flags[(int64_t)o * n_pr + ip];
+      const double fo = fout[ip];
+      fpart += fo;
+      if (f == 1) { tpart += fo; ++ntr; }
+      if (f == 2) ++nbl;
+      if (f == 0)
+        for (int32_t s = 0; s < n_atoms; ++s)
+          if (!__builtin_isfinite(ncol[((int64_t)s * n_orb + o) * n_pr + ip])) { ++nnf; break; }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    fpart += __shfl_down(fpart, off, 64);
+    tpart += __shfl_down(tpart, off, 64);
+    ntr += __shfl_down(ntr, off, 64);
+    nbl += __shfl_down(nbl, off, 64);
+    nnf += __shfl_down(nnf, off, 64);
+  }
+  if (lane == 0) {
+    redd[0][wid] = fpart; redd[1][wid] = tpart;
+    redc[0][wid] = ntr; redc[1][wid] = nbl; redc[2][wid] = nnf;
+  }
+  __syncthreads();
+  double fs = 0.0, ts = 0.0;
+  ntr = nbl = nnf = 0;
+  for (int w = 0; w < kChordBlock / 64; ++w) {
+    fs += redd[0][w]; ts += redd[1][w];
+    ntr += redc[0][w]; nbl += redc[1][w]; nnf += redc[2][w];
+  }
+  // compaction in chord order
+  int32_t base = 0;
+  for (int32_t sw = 0; sw < n_pr; sw += per_sweep) {
+    const int32_t lo = sw + threadIdx.x * kChordPer;
+    int32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < kChordPer; ++k) {
+      const int32_t ip = lo + k;
+      if (ip < n_pr && flags[(int64_t)o * n_pr + ip] == 0) ++mine;
+    }
+    int32_t tot;
+    int32_t pos = base + block_excl_scan(mine, redi, &tot);
+#pragma unroll
+    for (int k = 0; k < kChordPer; ++k) {
+      const int32_t ip = lo + k;
+      if (ip >= n_pr || flags[(int64_t)o * n_pr + ip] != 0) continue;
+      act_ip[(int64_t)o * n_pr + pos] = ip;
+      double* r = recs + ((int64_t)o * n_pr + pos) * stride;
+      const double F = fout[ip] / fs;
+      r[0] = F;
+      double n0 = 0.0, n1 = 0.0;
+      for (int32_t s = 0; s < n_atoms; ++s) {
+        const double v = ncol[((int64_t)s * n_orb + o) * n_pr + ip];
+        r[1 + s] = v;
+        if (s == 0) n0 = v;
+        if (s == 1) n1 = v;
+      }
+      if (pos < kChordMergeMax) {
+        Fl[pos] = F;
+        k0[pos] = mkey(n0);
+        k1[pos] = n_atoms > 1 ? mkey(n1) : 0ull;
+        idx[pos] = pos;
+      }
+      ++pos;
+    }
+    base += tot;
+  }
+  const int32_t n = base;
+  const bool do_merge = merge && n >= 2 && n <= kChordMergeMax && nnf == 0;
+  int32_t G = n;
+  if (do_merge) {
+    int32_t P = 1;
+    while (P < n) P <<= 1;
+    for (int32_t i = n + threadIdx.x; i < P; i += kChordBlock) { k0[i] = ~0ull; k1[i] = ~0ull; idx[i] = 0x7fffffff; }
+    __syncthreads();
+    for (int32_t size = 2; size <= P; size <<= 1) {
+      for (int32_t st = size >> 1; st > 0; st >>= 1) {
+        for (int32_t t = threadIdx.x; t < P / 2; t += kChordBlock) {
+          const int32_t i = 2 * t - (t & (st - 1));
+          const int32_t j = i + st;
+          const bool up = (i & size) == 0;
+          const unsigned long long a0 = k0[i], b0 = k0[j], a1 = k1[i], b1 = k1[j];
+          const int32_t ai = idx[i], bi = idx[j];
+          const bool gt = (a0 > b0) || (a0 == b0 && (a1 > b1 || (a1 == b1 && ai > bi)));
+          if (gt == up) {
+            k0[i] = b0; k0[j] = a0; k1[i] = b1; k1[j] = a1; idx[i] = bi; idx[j] = ai;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    const double* orec = recs + (int64_t)o * n_pr * stride;
+    int32_t gbase = 0;
+    for (int32_t c0 = 0; c0 < n; c0 += kChordBlock) {
+      const int32_t i = c0 + threadIdx.x;
+      bool head = false;
+      if (i < n) {
+        head = (i == 0) || k0[i] != k0[i - 1] || k1[i] != k1[i - 1];
+        if (!head && n_atoms > 2) {
+          const double* a = orec + (int64_t)idx[i] * stride;
+          const double* b = orec + (int64_t)idx[i - 1] * stride;
+          for (int32_t s = 2; s < n_atoms && !head; ++s) head = mkey(a[1 + s]) != mkey(b[1 + s]);
         }
       }
-      __syncthreads();
+      int32_t tot;
+      const int32_t rank = block_excl_scan(head ? 1 : 0, redi, &tot);
+      if (i < n) gid[i] = gbase + rank + (head ? 0 : -1);
+      gbase += tot;
     }
-  }
-  // group heads: first of a run of equal keys in every species
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int32_t base = 0;
-  for (int32_t c0 = 0; c0 < n; c0 += kMergeBlock) {
-    const int32_t i = c0 + threadIdx.x;
-    bool head = false;
-    if (i < n) {
-      head = (i == 0) || k0[i] != k0[i - 1] || k1[i] != k1[i - 1];
-      if (!head) {
-        const double* a = rec + (int64_t)idx[i] * stride;
-        const double* b = rec + (int64_t)idx[i - 1] * stride;
-        for (int32_t s = 2; s < n_atoms && !head; ++s) head = mkey(a[1 + s]) != mkey(b[1 + s]);
-      }
-    }
-    const unsigned long long m = __ballot(head);
-    if (lane == 0) wsum[wid] = __popcll(m);
     __syncthreads();
-    int32_t wb = 0, tot = 0;
-    for (int w = 0; w < kMergeBlock / 64; ++w) {
-      if (w < wid) wb += wsum[w];
-      tot += wsum[w];
+    G = gbase;
+    double* mo = mrecs + (int64_t)o * n_pr * stride;
+    for (int32_t i = threadIdx.x; i < n; i += kChordBlock) {
+      if (i > 0 && gid[i] == gid[i - 1]) continue;
+      double F = Fl[idx[i]];
+      for (int32_t j = i + 1; j < n && gid[j] == gid[i]; ++j) F += Fl[idx[j]];
+      const double* a = orec + (int64_t)idx[i] * stride;
+      double* r = mo + (int64_t)gid[i] * stride;
+      r[0] = F;
+      for (int32_t s = 0; s < n_atoms; ++s) r[1 + s] = a[1 + s];
     }
-    if (i < n) gid[i] = base + wb + __popcll(m & ((1ull << lane) - 1ull)) + (head ? 0 : -1);
-    base += tot;
-    __syncthreads();
   }
-  // each head sums the weights of its run (sorted order) and writes the merged record
-  for (int32_t i = threadIdx.x; i < n; i += kMergeBlock) {
-    if (i > 0 && gid[i] == gid[i - 1]) continue;
-    const double* a = rec + (int64_t)idx[i] * stride;
-    double F = a[0];
-    for (int32_t j = i + 1; j < n && gid[j] == gid[i]; ++j) F += rec[(int64_t)idx[j] * stride];
-    double* r = out + (int64_t)gid[i] * stride;
-    r[0] = F;
-    for (int32_t s = 0; s < n_atoms; ++s) r[1 + s] = a[1 + s];
+  if (threadIdx.x == 0) {
+    tfrac[o] = ts / fs;
+    fsum[o] = fs;
+    counts[o * 6 + 0] = n;
+    counts[o * 6 + 1] = ntr;
+    counts[o * 6 + 2] = nbl;
+    counts[o * 6 + 3] = nnf;
+    counts[o * 6 + 4] = G;
+    counts[o * 6 + 5] = do_merge ? 1 : 0;
   }
-  if (threadIdx.x == 0) counts[o * 5 + 4] = base;
 }
 
 // ---- fast exp: acc + F * 2^(y/2048) with a 2048-entry table in LDS --------------------------------
@@ -571,20 +710,17 @@ __device__ __forceinline__ double acc_exp2k(double acc, double F, double y, cons
   return __builtin_fma(F * S, e, acc);
 }
 
-// sigma of one atomic slot at (phase o, wavelength w): n_interp_log at shift_o * lambda_w.
-__device__ __forceinline__ double slot_sigma(const SigTabDev& t, int32_t o, double lam) {
-  return exp10(np_interp(t.shift[o] * lam, t.x, t.y, t.n)) - t.offset;
-}
-
 __device__ __forceinline__ void fill_exp_table(double* etab) {
   for (int i = threadIdx.x; i < PROM_EXP2_TABLE_N; i += kBlock) etab[i] = kExp2TableDev[i];
 }
 
-// Fused sigma lookup -> tau -> exp(-tau) -> disk sum -> ratio.  One thread per (phase o,
-// wavelength w); the chord loop is uniform across the workgroup (all threads share the phase), so
-// the packed chord records {lF, N_0..N_{S-1}} are read with scalar loads.
-// NS: number of atomic slots (0 = runtime count, per-thread sigma in LDS).
-// EXPK 1: table exp (exact ocml path for phases flagged non-finite);  0: ocml exp everywhere.
+// Fused sigma lookup -> tau -> exp(-tau) -> disk sum -> ratio.
+// Grid: (wavelength tiles of kBlock, phase groups).  A thread owns one wavelength and walks the
+// phases of its group: per phase it refreshes sigma_s = 10^interp(shift_o lambda) - offset (only
+// when the phase's Doppler factor changed; the table bracket gallops from the previous phase's), then
+// integrates the phase's chord records -- uniform across the workgroup, so scalar loads -- and writes
+// R[o][w].  NS: atomic slots (0 = runtime count, sigma in LDS).  EXPK 1: table exp (the exact ocml
+// path for phases flagged non-finite); 0: ocml exp everywhere (validation).
 template <int NS, int EXPK>
 __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ tabs,
                                                 const double* __restrict__ wav,
@@ -595,63 +731,97 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
                                                 const int32_t* __restrict__ counts,
                                                 const double* __restrict__ tfrac,
                                                 const double* __restrict__ fsum, int32_t n_atoms_rt,
-                                                int32_t n_pr, int64_t n_wav, double* __restrict__ R) {
-  extern __shared__ double lds[];   // [2048] exp table | NS == 0: [n_atoms][kBlock] sigma
+                                                int32_t n_pr, int32_t n_orb, int32_t phases_per_group,
+                                                int64_t n_wav, double* __restrict__ R) {
+  extern __shared__ double lds[];   // [2048] exp table | NS == 0: [3][n_atoms][kBlock]
   double* etab = lds;
   double* sgl = lds + (EXPK ? PROM_EXP2_TABLE_N : 0);
   if (EXPK) fill_exp_table(etab);
-  const int32_t o = blockIdx.y;
+  __syncthreads();
   const int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
-  const bool exact = !EXPK || counts[o * 5 + 3] != 0;
-  const int32_t n_act = counts[o * 5 + (exact ? 0 : 4)];
+  const int32_t o0 = blockIdx.y * phases_per_group;
+  const int32_t o1 = min(n_orb, o0 + phases_per_group);
   const int32_t ns = NS > 0 ? NS : n_atoms_rt;
   const int32_t stride = 1 + ns;
-  const double* __restrict__ rec = (exact ? recs : mrecs) + (int64_t)o * n_pr * stride;
-  const double scale = exact ? 1.0 : kMinus2048OverLn2;
-  double acc = 0.0;
-  double sp[NS > 0 ? NS : 1];
-  if constexpr (NS > 0) {
+  constexpr int NR = NS > 0 ? NS : 1;
+  double sg[NR];            // sigma_s at the current phase (NS > 0)
+  double shv[NR];           // Doppler factor sg was computed for
+  int64_t hint[NR];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) sp[s] = slot_sigma(tabs[s], o, lam) * scale;
-  } else {
-    for (int32_t s = 0; s < ns; ++s) sgl[s * kBlock + threadIdx.x] = slot_sigma(tabs[s], o, lam) * scale;
+  for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); hint[s] = -1; }
+  double* sg_l = sgl;                                  // NS == 0: [ns][kBlock]
+  double* sh_l = sgl + (int64_t)ns * kBlock;           // NS == 0: [ns][kBlock]
+  int64_t* hi_l = reinterpret_cast<int64_t*>(sgl + 2 * (int64_t)ns * kBlock);
+  if constexpr (NS == 0) {
+    for (int32_t s = 0; s < ns; ++s) { sh_l[s * kBlock + threadIdx.x] = __builtin_nan(""); hi_l[s * kBlock + threadIdx.x] = -1; }
   }
-  __syncthreads();
-  if (!exact) {
-    for (int32_t i = 0; i < n_act; ++i) {
-      const double* r = rec + (int64_t)i * stride;
-      double y;
-      if constexpr (NS > 0) {
-        y = r[1] * sp[0];
+  for (int32_t o = o0; o < o1; ++o) {
+    const bool exact = !EXPK || counts[o * 6 + 3] != 0;
+    const bool merged = !exact && counts[o * 6 + 5] != 0;
+    const int32_t n_act = counts[o * 6 + (merged ? 4 : 0)];
+    const double* __restrict__ rec = (merged ? mrecs : recs) + (int64_t)o * n_pr * stride;
+    double acc = 0.0;
+    if constexpr (NS > 0) {
 #pragma unroll
-        for (int s = 1; s < NS; ++s) y = __builtin_fma(r[1 + s], sp[s], y);
-      } else {
-        y = r[1] * sgl[threadIdx.x];
-        for (int32_t s = 1; s < ns; ++s) y = __builtin_fma(r[1 + s], sgl[s * kBlock + threadIdx.x], y);
+      for (int s = 0; s < NS; ++s) {
+        const double sh = tabs[s].shift[o];
+        if (!(sh == shv[s])) {
+          sg[s] = exp10(np_interp_hint(sh * lam, tabs[s].x, tabs[s].y, tabs[s].n, hint[s])) - tabs[s].offset;
+          shv[s] = sh;
+        }
       }
-      acc = acc_exp2k(acc, r[0], y, etab);
-    }
-    if (live) R[(int64_t)o * n_wav + w] = acc + tfrac[o];
-  } else {
-    // exact path: tau in the reference's order (products then sums), ocml exp, F_out weights
-    const int32_t* ipl = act_ip + (int64_t)o * n_pr;
-    for (int32_t i = 0; i < n_act; ++i) {
-      const double* r = rec + (int64_t)i * stride;
-      double tau;
-      if constexpr (NS > 0) {
-        tau = r[1] * sp[0];
+      if (!exact) {
+        double sp[NS];
 #pragma unroll
-        for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sp[s];
+        for (int s = 0; s < NS; ++s) sp[s] = sg[s] * kMinus2048OverLn2;
+        for (int32_t i = 0; i < n_act; ++i) {
+          const double* r = rec + (int64_t)i * stride;
+          double y = r[1] * sp[0];
+#pragma unroll
+          for (int s = 1; s < NS; ++s) y = __builtin_fma(r[1 + s], sp[s], y);
+          acc = acc_exp2k(acc, r[0], y, etab);
+        }
       } else {
-        tau = r[1] * sgl[threadIdx.x];
-        for (int32_t s = 1; s < ns; ++s) tau = tau + r[1 + s] * sgl[s * kBlock + threadIdx.x];
+        const int32_t* ipl = act_ip + (int64_t)o * n_pr;
+        for (int32_t i = 0; i < n_act; ++i) {
+          const double* r = rec + (int64_t)i * stride;
+          double tau = r[1] * sg[0];
+#pragma unroll
+          for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[s];
+          acc = acc + fout[ipl[i]] * exp(-tau);
+        }
       }
-      acc = acc + fout[ipl[i]] * exp(-tau);
+    } else {
+      for (int32_t s = 0; s < ns; ++s) {
+        const int64_t li = (int64_t)s * kBlock + threadIdx.x;
+        const double sh = tabs[s].shift[o];
+        if (!(sh == sh_l[li])) {
+          int64_t h = hi_l[li];
+          sg_l[li] = exp10(np_interp_hint(sh * lam, tabs[s].x, tabs[s].y, tabs[s].n, h)) - tabs[s].offset;
+          hi_l[li] = h;
+          sh_l[li] = sh;
+        }
+      }
+      if (!exact) {
+        for (int32_t i = 0; i < n_act; ++i) {
+          const double* r = rec + (int64_t)i * stride;
+          double y = r[1] * (sg_l[threadIdx.x] * kMinus2048OverLn2);
+          for (int32_t s = 1; s < ns; ++s) y = __builtin_fma(r[1 + s], sg_l[s * kBlock + threadIdx.x] * kMinus2048OverLn2, y);
+          acc = acc_exp2k(acc, r[0], y, etab);
+        }
+      } else {
+        const int32_t* ipl = act_ip + (int64_t)o * n_pr;
+        for (int32_t i = 0; i < n_act; ++i) {
+          const double* r = rec + (int64_t)i * stride;
+          double tau = r[1] * sg_l[threadIdx.x];
+          for (int32_t s = 1; s < ns; ++s) tau = tau + r[1 + s] * sg_l[s * kBlock + threadIdx.x];
+          acc = acc + fout[ipl[i]] * exp(-tau);
+        }
+      }
     }
-    if (live) R[(int64_t)o * n_wav + w] = (acc + tfrac[o] * fsum[o]) / fsum[o];
-    (void)rec;
+    if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
   }
 }
 
@@ -659,46 +829,65 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;
   PROM_HIP(hipEventRecord(ev[0], s));
-  // 1. densities
-  for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
-    const DensityDev& m = tr.dens[sc];
-    const double* tab = nullptr;
-    if (m.kind == PROM_DENSITY_TABULATED) tab = tr.tab.as<double>() + tr.tab_off[sc];
-    hipLaunchKernelGGL(k_ntot, dim3(grid_for(per)), dim3(kBlock), 0, s, m, sc, tr.x.as<double>(), tr.n_x,
-                       tr.cy.as<double>(), tr.cz.as<double>(), tr.n_pr, tr.n_orb, tr.body_x.as<double>(),
-                       tr.body_y.as<double>(), tab, tr.ntot.as<double>());
-    PROM_HIP(hipGetLastError());
-  }
-  double mol_max = 0.0;
-  for (const auto& t : tr.terms)
-    if (t.is_molecule) mol_max = std::max(mol_max, std::pow(10.0, mtables[t.table].vmax));
+  // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
-  hipLaunchKernelGGL(k_columns, dim3(grid_for(nc, 64)), dim3(64), 0, s, tr.terms_dev.as<TermDev>(),
-                     tr.n_terms, tr.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
-                     tr.cy.as<double>(), tr.cz.as<double>(), tr.planet_y.as<double>(), tr.planet_R,
-                     tr.n_moons, tr.moon_y.as<double>(), tr.moon_R.as<double>(),
-                     tr.sigma_max_dev.as<double>(), mol_max, tr.cull_tau, tr.ncol.as<double>(),
-                     tr.molcol.as<double>(), tr.flags.as<int32_t>());
-  PROM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_compact, dim3(tr.n_orb), dim3(kBlock), 0, s, tr.flags.as<int32_t>(),
-                     tr.cfout.as<double>(), tr.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
-                     tr.recs.as<double>(), tr.act_ip.as<int32_t>(), tr.counts.as<int32_t>(),
-                     tr.tsum.as<double>(), tr.fsum.as<double>());
-  PROM_HIP(hipGetLastError());
-  if (tr.merge && tr.exp_mode) {
-    hipLaunchKernelGGL(k_merge, dim3(tr.n_orb), dim3(kMergeBlock), 0, s, tr.recs.as<double>(), tr.n_atoms,
-                       tr.n_pr, tr.counts.as<int32_t>(), tr.mrecs.as<double>());
+  if (tr.n_mol == 0 && tr.n_x <= 64) {
+#define PROM_COLS(LV)                                                                                    \
+  hipLaunchKernelGGL(k_columns_lanes<LV>, dim3((unsigned)((nc + kBlock / (LV) - 1) / (kBlock / (LV)))),  \
+                     dim3(kBlock), 0, s, tr.terms_dev.as<TermDev>(), tr.n_terms, tr.scdev.as<ScDev>(),    \
+                     tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
+                     tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
+                     tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
+                     tr.moon_R.as<double>(), tr.sigma_max_dev.as<double>(), tr.cull_tau, tr.ncol.as<double>(), \
+                     tr.flags.as<int32_t>())
+    if (tr.n_x <= 8) PROM_COLS(8);
+    else if (tr.n_x <= 16) PROM_COLS(16);
+    else if (tr.n_x <= 32) PROM_COLS(32);
+    else PROM_COLS(64);
+#undef PROM_COLS
+    PROM_HIP(hipGetLastError());
+  } else {
+    for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
+      const DensityDev& m = tr.dens[sc];
+      const double* tab = nullptr;
+      if (m.kind == PROM_DENSITY_TABULATED) tab = tr.tab.as<double>() + tr.tab_off[sc];
+      hipLaunchKernelGGL(k_ntot, dim3(grid_for(per)), dim3(kBlock), 0, s, m, sc, tr.x.as<double>(), tr.n_x,
+                         tr.cy.as<double>(), tr.cz.as<double>(), tr.n_pr, tr.n_orb, tr.body_x.as<double>(),
+                         tr.body_y.as<double>(), tab, tr.ntot.as<double>());
+      PROM_HIP(hipGetLastError());
+    }
+    double mol_max = 0.0;
+    for (const auto& t : tr.terms)
+      if (t.is_molecule) mol_max = std::max(mol_max, std::pow(10.0, mtables[t.table].vmax));
+    hipLaunchKernelGGL(k_columns, dim3(grid_for(nc, 64)), dim3(64), 0, s, tr.terms_dev.as<TermDev>(),
+                       tr.n_terms, tr.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
+                       tr.cy.as<double>(), tr.cz.as<double>(), tr.planet_y.as<double>(), tr.planet_R,
+                       tr.n_moons, tr.moon_y.as<double>(), tr.moon_R.as<double>(),
+                       tr.sigma_max_dev.as<double>(), mol_max, tr.cull_tau, tr.ncol.as<double>(),
+                       tr.molcol.as<double>(), tr.flags.as<int32_t>());
     PROM_HIP(hipGetLastError());
   }
+  // 2. per-phase compaction (+ merging of equal-column chords)
+  hipLaunchKernelGGL(k_chords, dim3(tr.n_orb), dim3(kChordBlock), 0, s, tr.flags.as<int32_t>(),
+                     tr.cfout.as<double>(), tr.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
+                     (tr.merge && tr.exp_mode) ? 1 : 0, tr.recs.as<double>(), tr.act_ip.as<int32_t>(),
+                     tr.mrecs.as<double>(), tr.counts.as<int32_t>(), tr.tsum.as<double>(), tr.fsum.as<double>());
+  PROM_HIP(hipGetLastError());
   PROM_HIP(hipEventRecord(ev[1], s));
   // 2. (sigma is fused into the tau kernel; the event pair brackets nothing since round 1.2)
   PROM_HIP(hipEventRecord(ev[2], s));
   // 3. fused sigma -> tau -> exp -> disk-sum kernel
-  dim3 g((unsigned)((tr.n_wav + kBlock - 1) / kBlock), tr.n_orb);
+  // phase groups: enough waves for latency hiding (~8 per SIMD over 1024 SIMDs), few enough that
+  // each thread reuses its sigma bracket across several phases
+  const int64_t n_tiles = (tr.n_wav + kBlock - 1) / kBlock;
+  int32_t groups = (int32_t)std::max<int64_t>(1, std::min<int64_t>(tr.n_orb, (8192 + 4 * n_tiles - 1) / (4 * n_tiles)));
+  const int32_t ppg = (tr.n_orb + groups - 1) / groups;
+  groups = (tr.n_orb + ppg - 1) / ppg;
+  dim3 g((unsigned)n_tiles, (unsigned)groups);
   const SigTabDev* tabs = tr.sigtab.as<SigTabDev>();
   const double* wav = tr.wav.as<double>();
   const double* recs = tr.recs.as<double>();
-  const double* mrecs = (tr.merge && tr.exp_mode) ? tr.mrecs.as<double>() : recs;
+  const double* mrecs = tr.mrecs.as<double>();
   const int32_t* aip = tr.act_ip.as<int32_t>();
   const double* fo = tr.cfout.as<double>();
   const int32_t* counts = tr.counts.as<int32_t>();
@@ -709,8 +898,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
 #define PROM_TAU(NSV, EK)                                                                              \
   hipLaunchKernelGGL((k_tau<NSV, EK>), g, dim3(kBlock),                                                \
                      ((EK) ? PROM_EXP2_TABLE_N * sizeof(double) : 0) +                                  \
-                         ((NSV) == 0 ? (size_t)na * kBlock * sizeof(double) : 0),                      \
-                     s, tabs, wav, recs, mrecs, aip, fo, counts, tf, fs, na, tr.n_pr, tr.n_wav, R)
+                         ((NSV) == 0 ? (size_t)3 * na * kBlock * sizeof(double) : 0),                  \
+                     s, tabs, wav, recs, mrecs, aip, fo, counts, tf, fs, na, tr.n_pr, tr.n_orb, ppg, tr.n_wav, R)
 #define PROM_TAU_NS(EK)                 \
   switch (na) {                         \
     case 1: PROM_TAU(1, EK); break;     \
