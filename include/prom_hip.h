@@ -153,6 +153,8 @@ typedef struct prom_transit_problem {
                                   (exp(-tau) == 1 to the last ulp); <= 0 selects 2^-60       */
   int32_t options;             /* PROM_OPT_* bit set                                          */
   int32_t reserved2;
+  double k_B;                  /* Boltzmann constant for P = n k_B T of molecular lookups
+                                  (<= 0: the reference's 1.381e-16, constants.py:17)          */
 } prom_transit_problem;
 
 /* prom_transit_problem.options */

@@ -57,7 +57,8 @@ class TransitProblem(C.Structure):
                 ("n_scenarios", C.c_int32), ("x", _dp), ("delta_x", C.c_double), ("planet_y", _dp),
                 ("planet_R", C.c_double), ("n_moons", C.c_int32), ("reserved", C.c_int32),
                 ("moon_y", _dp), ("moon_R", _dp), ("scenarios", C.POINTER(Scenario)),
-                ("cull_tau", C.c_double), ("options", C.c_int32), ("reserved2", C.c_int32)]
+                ("cull_tau", C.c_double), ("options", C.c_int32), ("reserved2", C.c_int32),
+                ("k_B", C.c_double)]
 
 
 OPT_OCML_EXP = 1
@@ -283,7 +284,7 @@ class TransitInputs:
     """Owns the numpy arrays behind one prom_transit_problem (kept alive while in use)."""
 
     def __init__(self, *, wavelength, chord_y, chord_z, chord_fout, n_orb, x, delta_x, planet_y, planet_R,
-                 moon_y, moon_R, scenarios, cull_tau=0.0, options=0):
+                 moon_y, moon_R, scenarios, cull_tau=0.0, options=0, k_B=0.0):
         keep = []
 
         def arr(a):
@@ -332,6 +333,7 @@ class TransitInputs:
         s.scenarios = scs
         s.cull_tau = float(cull_tau)
         s.options = int(options)
+        s.k_B = float(k_B)
         self.struct = s
         self.keepalive = keep
         self.n_atoms = n_atoms

@@ -281,6 +281,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.merge = (pb->options & PROM_OPT_NO_MERGE) == 0;
     tr.terms.clear();
     tr.dens.clear();
+    tr.mslots.clear();
     tr.atom_sigma_max.clear();
     tr.tab_off.assign(tr.n_sc, -1);
     const hipStream_t s = ctx->stream;
@@ -314,9 +315,18 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         t.table = C.table_id;
         t.chi = C.chi;
         if (t.is_molecule) {
-          PROM_REQUIRE(false, "transit: molecular constituents need the molecular fused kernel "
-                              "(not in this build); use prom_molecular_sigma");
+          PROM_REQUIRE(C.table_id >= 0 && C.table_id < (int32_t)ctx->mtables.size(), "transit: unknown molecular table id");
           t.slot = n_mol++;
+          const prom::MolTable& mt = ctx->mtables[C.table_id];
+          prom::MolSlotDev md{};
+          md.P = mt.P.as<double>(); md.T = mt.T.as<double>(); md.W = mt.W.as<double>(); md.V = mt.V.as<double>();
+          md.n_p = mt.n_p; md.n_t = mt.n_t; md.n_w = mt.n_w;
+          md.offset = mt.offset;
+          md.fill = std::log10(mt.offset);
+          md.temp = S.T;
+          md.chi = C.chi;
+          md.scenario = sc;
+          tr.mslots.push_back(md);
         } else {
           PROM_REQUIRE(C.table_id >= 0 && C.table_id < (int32_t)ctx->tables.size(), "transit: unknown table id");
           t.slot = n_atoms++;
@@ -343,6 +353,11 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     upload(tr.shift, sh.data(), (int64_t)sh.size(), s);
     upload(tr.terms_dev, tr.terms.data(), (int64_t)tr.terms.size(), s);
     upload(tr.sigma_max_dev, tr.atom_sigma_max.data(), (int64_t)tr.atom_sigma_max.size(), s);
+    for (auto& md : tr.mslots) {
+      md.k_B = pb->k_B > 0.0 ? pb->k_B : 1.381 * std::pow(10.0, -16);
+      md.shift = tr.shift.as<double>() + (int64_t)md.scenario * n_orb;
+    }
+    upload(tr.molslot, tr.mslots.data(), (int64_t)tr.mslots.size(), s);
     {
       std::vector<prom::SigTabDev> st;
       for (const auto& t : tr.terms) {
@@ -371,6 +386,11 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
     tr.ncol.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * nc);
     tr.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
+    if (n_mol > 0) {
+      tr.mol_ip.ensure(sizeof(int32_t) * n_mol * nc * tr.n_x);
+      tr.mol_wp.ensure(sizeof(double) * n_mol * nc * tr.n_x);
+      tr.mol_na.ensure(sizeof(double) * n_mol * nc * tr.n_x);
+    }
     tr.flags.ensure(sizeof(int32_t) * nc);
     tr.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
     tr.act_ip.ensure(sizeof(int32_t) * nc);

@@ -88,6 +88,24 @@ struct SigTabDev {
   const double* shift;   // [n_orb]
 };
 
+// Per molecular slot of a transit problem.
+struct MolSlotDev {
+  const double* P;       // [n_p] dyn cm^-2
+  const double* T;       // [n_t]
+  const double* W;       // [n_w] cm
+  const double* V;       // [n_p][n_t][n_w] log10(xsec + offset)
+  int32_t n_p, n_t;
+  int64_t n_w;
+  double offset;
+  double fill;           // log10(offset): RegularGridInterpolator fill value
+  double temp;           // the scenario's T (lookup temperature; P = n k_B T)
+  double chi;
+  double k_B;
+  const double* shift;   // [n_orb] Doppler factors of its scenario
+  int32_t scenario;
+  int32_t pad;
+};
+
 struct AtomTable {
   DevBuf x, y;
   int64_t n = 0;
@@ -139,6 +157,11 @@ struct TransitDev {
   bool merge = true;                        // merge chords with equal (2^-40) column densities
   DevBuf mrecs;                             // merged records [n_orb][n_pr][1 + n_atoms]
   DevBuf R;                                 // [n_orb][n_wav]
+  DevBuf molslot;                           // [n_mol] MolSlotDev
+  DevBuf mol_ip;                            // [n_mol][n_orb][n_pr][n_x] int32 P bracket (-1: out of table)
+  DevBuf mol_wp;                            // [n_mol][n_orb][n_pr][n_x] P weight
+  DevBuf mol_na;                            // [n_mol][n_orb][n_pr][n_x] n_abs = n chi
+  std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
 };
 

@@ -571,7 +571,7 @@ class Transit:
             wavelength=self.wavelength[w0:w1], chord_y=host["y"], chord_z=host["z"], chord_fout=host["fout"],
             n_orb=len(host["orb"]), x=host["x"], delta_x=host["dx"], planet_y=host["planet_y"],
             planet_R=host["planet_R"], moon_y=host["moon_y"], moon_R=host["moon_R"], scenarios=scs,
-            cull_tau=cull_tau, options=options)
+            cull_tau=cull_tau, options=options, k_B=const.k_B)
 
     def sumOverChords(self, max_memory_gb: float = 2.0, devices: Optional[Sequence[int]] = None,
                       cull_tau: float = 0.0, options: int = 0) -> np.ndarray:

@@ -114,7 +114,7 @@ def _product_transit(cfg):
     return setupfile.build_transit(cfg)
 
 
-@pytest.mark.parametrize("name", ["C1", "C2r", "C3r", "C4r", "exomoon"])
+@pytest.mark.parametrize("name", ["C1", "C2r", "C3r", "C4r", "C5r", "exomoon"])
 def test_transit_golden(dev, name):
     d = load("transit_" + name)
     cfg = json.loads(str(d["config"]))
@@ -126,7 +126,7 @@ def test_transit_golden(dev, name):
     assert err < R_TOL
 
 
-@pytest.mark.parametrize("name", ["C2r", "C3r", "C4r"])
+@pytest.mark.parametrize("name", ["C2r", "C3r", "C4r", "C5r"])
 def test_transit_ocml_exp_mode(dev, name):
     """The validation build of the tau kernel (ocml exp) agrees with the table exp and the reference."""
     from prometheus_amd import _native
