@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-wavelengths", type=int, default=12288)
+    ap.add_argument("--cpu-sample-wavelengths", type=int, default=None,
+                    help="oracle sample size (default: ~10 s of reference-speed CPU work per config)")
     return ap.parse_args()
 
 
@@ -62,14 +63,11 @@ def global_config(name: str, world: int) -> dict:
     return cfg
 
 
-def kernel_flops_per_cle(n_atoms: int) -> int:
-    """Algorithmic FP64 operations per chord-wavelength evaluation of k_tau:
-    tau = sum_s N_s sigma_s (n_atoms mul + n_atoms-1 add), F_out * exp(-tau) (1 mul), += (1 add),
-    and exp counted as EXP_FLOPS (a table-driven 1-ulp FP64 exp = 11 FP64 ops)."""
-    return 2 * n_atoms + 1 + EXP_FLOPS
-
-
-EXP_FLOPS = 11
+def flops_per_eval(n_atoms: int) -> int:
+    """FP64 flops (FMA = 2, as the 78.6 TFLOP/s peak counts them) of one chord-wavelength evaluation
+    in k_tau ("Roofline"): y = -tau*2048/ln2 = N_0 s_0 (+ fma per further species) ->
+    2S - 1;  2^(y/2048): rint, d = y - k, 3 FMA polynomial, ldexp -> 9;  F * S -> 1;  acc fma -> 2."""
+    return 2 * n_atoms - 1 + 12
 
 
 def latest_profile_traffic():
@@ -84,11 +82,16 @@ def latest_profile_traffic():
         return None
 
 
+def describe(cfg: dict) -> str:
+    return "; ".join("%s: %s" % (k, "+".join(v.keys())) for k, v in cfg["Species"].items())
+
+
 def cpu_baseline(cfg: dict, n_sample: int):
     """The oracle (numpy restatement of the reference dataflow, single process) on a bounded sample:
     every phase and chord of the config, the first n_sample wavelengths of the grid."""
     from oracle import prom_oracle as O
-    scen, dop, grids = O.from_setup(cfg)
+    mol = {"H2O": O.synthetic_molecular_table()} if "H2O" in str(cfg["Species"]) else None
+    scen, dop, grids = O.from_setup(cfg, mol)
     tabs = O.build_tables(scen, grids)
     wav = O.simulation_wavelengths(grids, O.atomic_species(scen))
     sel = wav[:n_sample]
@@ -117,6 +120,9 @@ def main():
 
     cfg = global_config(args.config, world)
     cfg_name = args.config
+    if any(sp not in ("NaI", "KI", "CaII", "MgI") for sc in cfg["Species"].values() for sp in sc):
+        from prometheus_amd.configs import synthetic_molecular_table
+        gasProperties.register_molecular_table("H2O", synthetic_molecular_table())
     t_setup = time.perf_counter()
     tr = setupfile.build_transit(cfg)   # lambda grid + device Voigt tables on this rank's GPU
     dev = _native.get_device(local_rank)
@@ -170,7 +176,8 @@ def main():
     tau_ms = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
     n_atoms = prob.n_atoms
     cle = st["chord_lambda_evals"]
-    flops = cle * kernel_flops_per_cle(n_atoms)
+    evals = st["exp_evals"]
+    flops = evals * flops_per_eval(n_atoms)
     achieved_tflops = flops / (tau_ms * 1e-3) / 1e12
     traffic = latest_profile_traffic()
     # end-to-end (host prep + H2D + run + D2H) for reference, one call
@@ -190,30 +197,33 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (WASP-49b catalogue system, NIST line list bundled from the reference)",
-        "config": {"workload": "%s: barometric Na I + K I, %d wavelengths x %d phases x %d chords x %d samples"
-                               % (cfg_name, n_wav_global, n_orb, len(host["y"]), len(host["x"])),
+        "config": {"workload": "%s (%s), %d wavelengths x %d phases x %d chords x %d samples"
+                               % (cfg_name, describe(cfg), n_wav_global, n_orb, len(host["y"]), len(host["x"])),
                    "global_wavelengths": n_wav_global, "orbital_phases": n_orb,
                    "chords_per_phase": len(host["y"]), "los_samples": len(host["x"]),
                    "parallelism": "wavelength shards x%d (no collective)" % world},
         "roofline": {"bound": "valu", "kernel": "k_tau", "achieved": achieved_tflops,
                      "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tflops / FP64_VALU_PEAK_TFLOPS, "traffic": traffic,
-                     "tau_ms": tau_ms, "chord_lambda_evals": cle,
-                     "flops_per_cle": kernel_flops_per_cle(n_atoms),
-                     "exp_per_s": cle / (tau_ms * 1e-3)},
+                     "tau_ms": tau_ms, "chord_lambda_evals": cle, "exp_evals": evals,
+                     "flops_per_eval": flops_per_eval(n_atoms),
+                     "exp_per_s": evals / (tau_ms * 1e-3),
+                     "chord_lambda_per_s": cle / (tau_ms * 1e-3)},
         "stage_ms": {"density": float(np.mean(ms_runs[:, 0])) if len(ms_runs) else None,
                      "sigma": float(np.mean(ms_runs[:, 1])) if len(ms_runs) else None,
                      "tau": tau_ms,
                      "total": float(np.mean(ms_runs[:, 3])) if len(ms_runs) else None},
         "chords": {"active": st["active_chords"], "transparent": st["transparent_chords"],
-                   "blocked": st["blocked_chords"]},
+                   "blocked": st["blocked_chords"], "integrated_records": st["tau_records"]},
         "setup_s": setup_s,
         "end_to_end_s": e2e_s if R is not None else None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cfgc = dict(cfg)
         cfgc["_name"] = cfg_name
-        result["cpu_baseline"] = cpu_baseline(cfgc, args.cpu_sample_wavelengths)
+        n_cpu = args.cpu_sample_wavelengths or {"C1": 219, "C2": 12288, "C3": 6144, "C4": 12288,
+                                                 "C5": 16}.get(cfg_name, 4096)
+        result["cpu_baseline"] = cpu_baseline(cfgc, n_cpu)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

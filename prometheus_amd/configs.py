@@ -144,3 +144,14 @@ def fixture_configs():
         "C5r": reduced(c5(), orbphase_steps=3, res_low=2.5e-8),
         "exomoon": reduced(exomoon(), orbphase_steps=4),
     }
+
+
+def synthetic_molecular_table(n_p=22, n_t=27, n_nu=50001, nu_lo=5000., nu_hi=10000., seed=0):
+    """Seeded stand-in for an ExoMol/TauREx H2O table (no network, no ExoMol data in this image):
+    p [Pa] = logspace(-1, 8), t [K] = linspace(100, 3400), bin_edges [cm^-1] = linspace(nu_lo, nu_hi),
+    xsecarr[p][t][nu] = 1e-22 exp(N(0, 1))."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    return {"p": np.logspace(-1, 8, n_p), "t": np.linspace(100., 3400., n_t),
+            "bin_edges": np.linspace(nu_lo, nu_hi, n_nu),
+            "xsecarr": 1e-22 * np.exp(rng.standard_normal((n_p, n_t, n_nu)))}

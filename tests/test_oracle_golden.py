@@ -98,3 +98,11 @@ def test_transit_depth(name):
     # the reference's two reduction branches are bitwise identical (gasProperties.py:1243-1256)
     assert np.array_equal(d["R"], d["R_small_batches"])
     assert np.array_equal(R, d["R"]), np.max(np.abs(R / d["R"] - 1))
+
+
+def test_synthetic_table_matches_product_copy():
+    from prometheus_amd import configs
+    a = O.synthetic_molecular_table(n_nu=101)
+    b = configs.synthetic_molecular_table(n_nu=101)
+    for k in a:
+        assert np.array_equal(a[k], b[k])
