@@ -127,8 +127,8 @@ def main():
     tr = setupfile.build_transit(cfg)   # lambda grid + device Voigt tables on this rank's GPU
     dev = _native.get_device(local_rank)
     n_wav_global = len(tr.wavelength)
-    edges = np.linspace(0, n_wav_global, world + 1).round().astype(np.int64)
-    w0, w1 = int(edges[rank]), int(edges[rank + 1])
+    shards = gasProperties._split(n_wav_global, world)   # wavefront-aligned contiguous shards
+    w0, w1 = shards[rank] if rank < len(shards) else (n_wav_global, n_wav_global)
     host = tr._host_inputs()
     prob = tr._problem(dev, host, w0, w1, 0.0)
     dev.transit_set(prob)

@@ -160,6 +160,8 @@ typedef struct prom_transit_problem {
 /* prom_transit_problem.options */
 #define PROM_OPT_OCML_EXP 1    /* use the ocml exp() in the tau kernel instead of the table-driven exp */
 #define PROM_OPT_NO_MERGE 2    /* integrate every active chord (no merging of equal-column chords) */
+#define PROM_OPT_NO_WINDOW 4   /* evaluate exp(-tau) for every record at every wavelength (no saturated-
+                                  head skip, no tail moments; see DESIGN.md "windowed integration") */
 
 typedef struct prom_transit_stats {
   double ms_total;             /* device time of the last prom_transit_run (hipEvents)        */
@@ -171,7 +173,9 @@ typedef struct prom_transit_stats {
   int64_t blocked_chords;
   int64_t chord_lambda_evals;  /* active_chords * n_wav                                        */
   int64_t tau_records;         /* chord records the tau kernel integrates (after merging)     */
-  int64_t exp_evals;           /* tau_records * n_wav: exp evaluations of the fused kernel    */
+  int64_t exp_evals;           /* exp evaluations of the fused kernel (counted on the device:
+                                  the windowed kernel evaluates only the records of each
+                                  wavefront's tau window; tau_records * n_wav without windows) */
   int32_t tau_kernel_variant;
   int32_t tau_kernel_variant_exact_phases;  /* phases integrated on the exact (ocml) path because a
                                                column density was not finite                      */

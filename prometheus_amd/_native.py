@@ -63,6 +63,7 @@ class TransitProblem(C.Structure):
 
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
+OPT_NO_WINDOW = 4
 
 
 class TransitStats(C.Structure):

@@ -103,6 +103,24 @@ int32_t prom_synchronize(prom_ctx* ctx) {
 }
 
 // ------------------------------------------------------------------------------ tables
+// Bucket directory of a table's nodes: n_dir equal buckets over [x0, x[n-1]], dir[j] = number of
+// nodes <= x0 + j h.  The tau kernel starts its np.interp bracket search from buckets j, j+1 of a
+// target and verifies the bracket, so rounding in j only costs steps, never correctness.
+static void build_directory(prom_ctx* ctx, prom::AtomTable& t, const double* x, int64_t n) {
+  const int64_t nd = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)1 << 24));
+  const double x0 = x[0], span = x[n - 1] - x[0];
+  std::vector<int32_t> d(nd + 1);
+  const double h = span > 0.0 ? span / (double)nd : 1.0;
+  for (int64_t j = 0; j <= nd; ++j) {
+    const double b = x0 + (double)j * h;
+    d[j] = (int32_t)(std::upper_bound(x, x + n, b) - x);
+  }
+  upload(t.dir, d.data(), nd + 1, ctx->stream);
+  t.n_dir = (int32_t)nd;
+  t.dir_x0 = x0;
+  t.dir_inv_h = span > 0.0 ? 1.0 / h : 0.0;
+}
+
 int32_t prom_table_upload(prom_ctx* ctx, int64_t n, const double* x, const double* log_sigma,
                           double offset, int32_t* table_id) {
   return guarded(ctx, [&] {
@@ -116,6 +134,7 @@ int32_t prom_table_upload(prom_ctx* ctx, int64_t n, const double* x, const doubl
     double m = -INFINITY;
     for (int64_t i = 0; i < n; ++i) m = std::max(m, log_sigma[i]);
     t.ymax = m;
+    build_directory(ctx, t, x, n);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
     ctx->tables.push_back(std::move(t));
     *table_id = (int32_t)ctx->tables.size() - 1;
@@ -149,6 +168,8 @@ int32_t prom_table_build_voigt(prom_ctx* ctx, int64_t n, const double* x, int32_
     t.ymax = prom::reduce_max(ctx->stream, t.y.as<double>(), n, ctx->scratch[4].as<double>());
     t.n = n;
     t.offset = offset;
+    build_directory(ctx, t, x, n);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
     if (log_sigma_out) {
       download(log_sigma_out, t.y, n, ctx->stream);
       PROM_HIP(hipStreamSynchronize(ctx->stream));
@@ -279,6 +300,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.cull_tau = pb->cull_tau > 0.0 ? pb->cull_tau : std::ldexp(1.0, -60);
     tr.exp_mode = (pb->options & PROM_OPT_OCML_EXP) ? 0 : 1;
     tr.merge = (pb->options & PROM_OPT_NO_MERGE) == 0;
+    tr.window = (pb->options & PROM_OPT_NO_WINDOW) == 0;
+    PROM_REQUIRE(pb->n_pr < (1 << 24), "transit: n_pr must be < 2^24");
     tr.terms.clear();
     tr.dens.clear();
     tr.mslots.clear();
@@ -364,7 +387,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         if (t.is_molecule) continue;
         const prom::AtomTable& tb = ctx->tables[t.table];
         st.push_back({tb.x.as<double>(), tb.y.as<double>(), tb.n, tb.offset,
-                      tr.shift.as<double>() + (int64_t)t.scenario * n_orb});
+                      tr.shift.as<double>() + (int64_t)t.scenario * n_orb, tb.dir.as<int32_t>(), tb.n_dir, 0,
+                      tb.dir_x0, tb.dir_inv_h});
       }
       upload(tr.sigtab, st.data(), (int64_t)st.size(), s);
     }
@@ -394,8 +418,14 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.flags.ensure(sizeof(int32_t) * nc);
     tr.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
     tr.act_ip.ensure(sizeof(int32_t) * nc);
-    tr.counts.ensure(sizeof(int32_t) * n_orb * 6);
+    tr.counts.ensure(sizeof(int32_t) * n_orb * prom::kCnt);
     tr.mrecs.ensure(sizeof(double) * nc * (1 + n_atoms));
+    tr.nmax.ensure(sizeof(double) * n_orb * std::max<int64_t>(n_atoms, 1));
+    if (n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && n_mol == 0) {
+      tr.wenv.ensure(sizeof(int32_t) * n_orb * 2 * prom::kEnvN);
+      tr.wmom.ensure(sizeof(double) * n_orb * (tr.n_pr + 1) * prom::n_tail_moments(n_atoms));
+    }
+    tr.evals.ensure(sizeof(unsigned long long) * 64);
     tr.tsum.ensure(sizeof(double) * n_orb);
     tr.fsum.ensure(sizeof(double) * n_orb);
     tr.R.ensure(sizeof(double) * n_orb * tr.n_wav);
@@ -420,7 +450,10 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
       ev = &ctx->tev[4 * (size_t)ctx->timed_runs];
       ++ctx->timed_runs;
     }
+    tr.count_evals = stats != nullptr;
+    if (tr.count_evals) PROM_HIP(hipMemsetAsync(tr.evals.p, 0, sizeof(unsigned long long) * 64, ctx->stream));
     prom::launch_transit(ctx->stream, tr, ctx->tables, ctx->mtables, ev, &variant);
+    tr.count_evals = false;
 
     tr.ran = true;
     if (stats) {
@@ -435,19 +468,28 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
       stats->ms_sigma = b;
       stats->ms_tau = c;
       stats->ms_total = t;
-      std::vector<int32_t> cnt(tr.n_orb * 6);
+      const int K = prom::kCnt;
+      std::vector<int32_t> cnt(tr.n_orb * K);
       download(cnt.data(), tr.counts, (int64_t)cnt.size(), ctx->stream);
+      unsigned long long ev64[64];
+      download(ev64, tr.evals, 64, ctx->stream);
       PROM_HIP(hipStreamSynchronize(ctx->stream));
+      int64_t unwindowed = 0, counted = 0;
       for (int32_t o = 0; o < tr.n_orb; ++o) {
-        const bool merged = cnt[o * 6 + 5] != 0;
-        stats->active_chords += cnt[o * 6];
-        stats->transparent_chords += cnt[o * 6 + 1];
-        stats->blocked_chords += cnt[o * 6 + 2];
-        stats->tau_records += merged ? cnt[o * 6 + 4] : cnt[o * 6];
-        if (cnt[o * 6 + 3]) stats->tau_kernel_variant_exact_phases += 1;
+        const bool sorted = cnt[o * K + 5] != 0;
+        const bool exact = cnt[o * K + 3] != 0;
+        const int64_t recs = sorted ? cnt[o * K + 4] : cnt[o * K];
+        stats->active_chords += cnt[o * K];
+        stats->transparent_chords += cnt[o * K + 1];
+        stats->blocked_chords += cnt[o * K + 2];
+        stats->tau_records += recs;
+        if (exact) stats->tau_kernel_variant_exact_phases += 1;
+        // the device counters cover the non-exact phases of the atomic fast kernel
+        if (exact || tr.n_mol > 0 || !tr.exp_mode || tr.n_atoms > prom::kWinMaxSpecies) unwindowed += recs;
       }
+      for (int i = 0; i < 64; ++i) counted += (int64_t)ev64[i];
       stats->chord_lambda_evals = stats->active_chords * tr.n_wav;
-      stats->exp_evals = stats->tau_records * tr.n_wav;
+      stats->exp_evals = counted + unwindowed * tr.n_wav;
       stats->tau_kernel_variant = variant;
     }
   });

@@ -57,6 +57,16 @@ struct DevBuf {
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+constexpr int kCnt = 8;   // int32 counters per phase in TransitDev::counts
+
+// Windowed integration (prom_kernels.hip, "windowed integration"): per-phase ordering limit, the
+// size of the per-phase threshold -> record-index tables, and the number of tail moments for S
+// atomic species (monomials of total degree <= 3 in S variables).
+constexpr int kWinMax = 4096;
+constexpr int kEnvN = 2048;
+constexpr int kWinMaxSpecies = 4;
+inline int n_tail_moments(int S) { return (S + 1) * (S + 2) * (S + 3) / 6; }
+
 // Device-side view of one density model (the prom_density_model scalars).
 struct DensityDev {
   int32_t kind;
@@ -86,6 +96,10 @@ struct SigTabDev {
   int64_t n;
   double offset;
   const double* shift;   // [n_orb]
+  const int32_t* dir;    // [n_dir + 1] bucket directory of x (AtomTable::dir)
+  int32_t n_dir;
+  int32_t pad;
+  double dir_x0, dir_inv_h;
 };
 
 // Per molecular slot of a transit problem.
@@ -111,6 +125,11 @@ struct AtomTable {
   int64_t n = 0;
   double offset = 0.0;
   double ymax = 0.0;     // max of y (log10 sigma): sigma_max = 10^ymax - offset
+  // bucket directory for O(1) bracketing: dir[j] = #{i : x[i] <= x0 + j h}, j = 0 .. n_dir,
+  // h = (x[n-1] - x0) / n_dir (prom_api.hip build_directory)
+  DevBuf dir;
+  int32_t n_dir = 0;
+  double dir_x0 = 0.0, dir_inv_h = 0.0;
 };
 
 struct MolTable {
@@ -155,7 +174,13 @@ struct TransitDev {
   DevBuf sigtab;                            // [n_atoms] SigTabDev
   int32_t exp_mode = 1;                     // 1: table-driven exp in k_tau, 0: ocml exp
   bool merge = true;                        // merge chords with equal (2^-40) column densities
-  DevBuf mrecs;                             // merged records [n_orb][n_pr][1 + n_atoms]
+  DevBuf mrecs;                             // sorted (+ merged) records [n_orb][n_pr][1 + n_atoms]
+  bool window = true;                       // windowed integration with tail moments
+  DevBuf nmax;                              // [n_orb][n_atoms] max column density over active chords
+  DevBuf wenv;                              // [n_orb][2][kEnvN] int32 threshold -> record tables
+  DevBuf wmom;                              // [n_orb][n_pr + 1][K] suffix tail moments
+  DevBuf evals;                             // [64] uint64 exp-evaluation counters (stats runs)
+  bool count_evals = false;
   DevBuf R;                                 // [n_orb][n_wav]
   DevBuf molslot;                           // [n_mol] MolSlotDev
   DevBuf mol_ip;                            // [n_mol][n_orb][n_pr][n_x] int32 P bracket (-1: out of table)

@@ -24,6 +24,29 @@ namespace prom {
 
 constexpr int kBlock = 256;
 
+// Optional in-kernel timing (build with -DPROM_TRACE, tools/trace_kernels.py): wall-clock stamps
+// (100 MHz) of workgroup 0's steps and per-wavefront cycle counters in a device array.
+#ifdef PROM_TRACE
+__device__ unsigned long long g_trace[1 << 20];
+#define PROM_TS(slot)                                                   \
+  do {                                                                  \
+    __syncthreads();                                                    \
+    if (threadIdx.x == 0) g_trace[(slot)] = wall_clock64();             \
+  } while (0)
+#define PROM_ACC(slot, v)                                               \
+  do {                                                                  \
+    if ((threadIdx.x & 63) == 0) g_trace[(slot)] += (unsigned long long)(v); \
+  } while (0)
+#else
+#define PROM_TS(slot) do {} while (0)
+#define PROM_ACC(slot, v) do {} while (0)
+#endif
+#ifdef PROM_TRACE
+#define PROM_CLK(var) const long long var = clock64()
+#else
+#define PROM_CLK(var) do {} while (0)
+#endif
+
 __constant__ double kExp2TableDev[PROM_EXP2_TABLE_N] = {
 #define PROM_EXP2_TABLE_BODY
 #include "exp2_table_body.h"
@@ -59,43 +82,41 @@ __device__ __forceinline__ double np_interp(double t, const double* __restrict__
   return r;
 }
 
-// np_interp with a bracket hint: the same index j (largest j <= n-2 with xp[j] <= t, the unique
-// bracket numpy's search returns) found by galloping from the previous target's bracket.  Used when
-// one thread interpolates a sequence of nearby targets (the same wavelength at successive phases).
-__device__ __forceinline__ double np_interp_hint(double t, const double* __restrict__ xp,
-                                                 const double* __restrict__ fp, int64_t n, int64_t& hint) {
-  if (t != t) return t;
-  if (n == 1) return fp[0];
-  if (t < xp[0]) return fp[0];
-  if (t > xp[n - 1]) return fp[n - 1];
-  if (t == xp[n - 1]) return fp[n - 1];
-  int64_t lo, hi;   // invariant xp[lo] <= t < xp[hi]
-  if (hint < 0 || hint > n - 2) {
-    lo = 0; hi = n - 1;
-  } else if (xp[hint] <= t) {
-    lo = hint;
-    int64_t step = 1;
-    hi = lo + 1;
-    while (hi < n - 1 && xp[hi] <= t) { lo = hi; step <<= 1; hi = lo + step; if (hi > n - 1) hi = n - 1; }
-  } else {
-    hi = hint;
-    int64_t step = 1;
-    lo = hi - 1;
-    while (lo > 0 && xp[lo] > t) { hi = lo; step <<= 1; lo = hi - step; if (lo < 0) lo = 0; }
+// np_interp for one table of a transit problem, bracket from the bucket directory (same unique
+// bracket as numpy's search: the largest j <= n-2 with xp[j] <= t), then 10^v - offset.
+__device__ __forceinline__ double sigma_of(double t, const SigTabDev& tb) {
+  const double* __restrict__ xp = tb.x;
+  const double* __restrict__ fp = tb.y;
+  const int64_t n = tb.n;
+  double v;
+  if (t != t) v = t;
+  else if (n == 1 || !(t >= xp[0])) v = fp[0];
+  else if (t >= xp[n - 1]) v = fp[n - 1];
+  else {
+    double fj = (t - tb.dir_x0) * tb.dir_inv_h;
+    int32_t j = fj < 0.0 ? 0 : (fj >= (double)(tb.n_dir - 1) ? tb.n_dir - 1 : (int32_t)fj);
+    int64_t lo = tb.dir[j] - 1, hi = tb.dir[j + 1];
+    lo = lo < 0 ? 0 : (lo > n - 2 ? n - 2 : lo);
+    hi = hi > n - 1 ? n - 1 : hi;
+    hi = hi <= lo ? lo + 1 : hi;
+    // verify the bracket xp[lo] <= t < xp[hi]; widen by galloping if rounding moved j
+    for (int64_t step = 1; lo > 0 && xp[lo] > t; step <<= 1) { hi = lo; lo = lo - step > 0 ? lo - step : 0; }
+    for (int64_t step = 1; hi < n - 1 && xp[hi] <= t; step <<= 1) { lo = hi; hi = hi + step < n - 1 ? hi + step : n - 1; }
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (xp[mid] <= t) lo = mid; else hi = mid;
+    }
+    if (xp[lo] == t) v = fp[lo];
+    else {
+      const double slope = (fp[lo + 1] - fp[lo]) / (xp[lo + 1] - xp[lo]);
+      v = slope * (t - xp[lo]) + fp[lo];
+      if (v != v) {
+        v = slope * (t - xp[lo + 1]) + fp[lo + 1];
+        if (v != v && fp[lo] == fp[lo + 1]) v = fp[lo];
+      }
+    }
   }
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (xp[mid] <= t) lo = mid; else hi = mid;
-  }
-  hint = lo;
-  if (xp[lo] == t) return fp[lo];
-  const double slope = (fp[lo + 1] - fp[lo]) / (xp[lo + 1] - xp[lo]);
-  double r = slope * (t - xp[lo]) + fp[lo];
-  if (r != r) {
-    r = slope * (t - xp[lo + 1]) + fp[lo + 1];
-    if (r != r && fp[lo] == fp[lo + 1]) r = fp[lo];
-  }
-  return r;
+  return exp10(v) - tb.offset;
 }
 
 // numpy.heaviside(d, 1.0)
@@ -456,12 +477,15 @@ __global__ void __launch_bounds__(kBlock) k_columns_lanes(const TermDev* __restr
                                  double planet_R, int32_t n_moons, const double* __restrict__ moon_y,
                                  const double* __restrict__ moon_R, const double* __restrict__ sig_max,
                                  double cull, double* __restrict__ ncol, int32_t* __restrict__ flags) {
+  // a chord's L lanes sit inside one wavefront: the pairwise partial sums move by cross-lane
+  // shuffles, no LDS and no workgroup barrier
+  PROM_CLK(tk0);
   constexpr int G = kBlock / L;         // chords per workgroup
-  __shared__ double av[G][L];
-  __shared__ double part[G][8];
-  const int grp = threadIdx.x / L, lane = threadIdx.x % L;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane & (L - 1);        // lane within the chord's group
+  const int gbase = lane & ~(L - 1);    // the group's first lane in the wavefront
   const int64_t nc = (int64_t)n_orb * n_pr;
-  const int64_t c = (int64_t)blockIdx.x * G + grp;
+  const int64_t c = (int64_t)blockIdx.x * G + threadIdx.x / L;
   const bool valid = c < nc;
   const int32_t ip = valid ? (int32_t)(c % n_pr) : 0;
   const int32_t o = valid ? (int32_t)(c / n_pr) : 0;
@@ -472,42 +496,47 @@ __global__ void __launch_bounds__(kBlock) k_columns_lanes(const TermDev* __restr
     const double dym = y - moon_y[m * n_orb + o];
     blocked = blocked || ((dym * dym + z * z) < moon_R[m] * moon_R[m]);
   }
+  const bool live = valid && !blocked && gl < n_x;
   const int32_t lim = n_x - (n_x % 8);
-  double bound = 0.0;
+  double bound = 0.0, nv = 0.0;
+  int32_t cur_sc = -1;
   for (int32_t t = 0; t < n_terms; ++t) {
     const TermDev td = terms[t];
-    const ScDev sc = scs[td.scenario];
-    double a = 0.0;
-    if (valid && !blocked && lane < n_x) {
-      const double nv = sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + lane]
-                               : density_at(sc.m, x[lane], y, z, bx[td.scenario * n_orb + o], by[td.scenario * n_orb + o]);
-      a = nv * td.chi;
+    if (td.scenario != cur_sc) {   // one density evaluation per scenario, shared by its constituents
+      cur_sc = td.scenario;
+      const ScDev sc = scs[cur_sc];
+      nv = 0.0;
+      if (live)
+        nv = sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + gl]
+                    : density_at(sc.m, x[gl], y, z, bx[cur_sc * n_orb + o], by[cur_sc * n_orb + o]);
     }
-    av[grp][lane] = a;
-    __syncthreads();
-    if (lane < 8 && n_x >= 8) {
-      double r = av[grp][lane];
-      for (int32_t i = 8 + lane; i < lim; i += 8) r += av[grp][i];
-      part[grp][lane] = r;
+    const double a = live ? nv * td.chi : 0.0;
+    double res;
+    if (n_x < 8) {
+      res = 0.0;
+      for (int32_t i = 0; i < n_x; ++i) res += __shfl(a, gbase + i, 64);
+    } else {
+      double r = a;   // lanes gl < 8: numpy's r[gl] = a[gl] + a[gl + 8] + ... (i < lim)
+      for (int32_t i = 8; i < lim; i += 8) r += __shfl(a, (gbase + gl + i) & 63, 64);
+      const double r0 = __shfl(r, gbase + 0, 64), r1 = __shfl(r, gbase + 1, 64);
+      const double r2 = __shfl(r, gbase + 2, 64), r3 = __shfl(r, gbase + 3, 64);
+      const double r4 = __shfl(r, gbase + 4, 64), r5 = __shfl(r, gbase + 5, 64);
+      const double r6 = __shfl(r, gbase + 6, 64), r7 = __shfl(r, gbase + 7, 64);
+      res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+      for (int32_t i = lim; i < n_x; ++i) res += __shfl(a, gbase + i, 64);
     }
-    __syncthreads();
-    if (lane == 0 && valid) {
-      double res;
-      if (n_x < 8) {
-        res = 0.0;
-        for (int32_t i = 0; i < n_x; ++i) res += av[grp][i];
-      } else {
-        res = ((part[grp][0] + part[grp][1]) + (part[grp][2] + part[grp][3])) +
-              ((part[grp][4] + part[grp][5]) + (part[grp][6] + part[grp][7]));
-        for (int32_t i = lim; i < n_x; ++i) res += av[grp][i];
-      }
-      const double N = blocked ? 0.0 : (0.0 + res) * delta_x;
-      ncol[((int64_t)td.slot * n_orb + o) * n_pr + ip] = N;
-      bound += N * sig_max[td.slot];
-    }
-    __syncthreads();
+    const double N = blocked ? 0.0 : (0.0 + res) * delta_x;
+    if (gl == 0 && valid) ncol[((int64_t)td.slot * n_orb + o) * n_pr + ip] = N;
+    bound += N * sig_max[td.slot];
   }
-  if (lane == 0 && valid) flags[c] = blocked ? 2 : ((bound <= cull) ? 1 : 0);
+  if (gl == 0 && valid) flags[c] = blocked ? 2 : ((bound <= cull) ? 1 : 0);
+#ifdef PROM_TRACE
+  {
+    const int64_t wv = 600000 + 2 * ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    PROM_ACC(wv + 0, clock64() - tk0);
+    PROM_ACC(wv + 1, 1);
+  }
+#endif
 }
 
 // ---- chord merging ----------------------------------------------------------------------------
@@ -528,7 +557,7 @@ __device__ __forceinline__ unsigned long long mkey(double v) {
 // chords in chord order into records {F_out / F_out_sum, N_0..N_{S-1}} (recs, act_ip: the exact path
 // and the unmerged fast path).  Pass 3 (merging, see k_merge's comment for the bound): LDS bitonic sort
 // of (key_0, key_1, position), group heads, one merged record per group (mrecs).
-// counts[o] = {active, transparent, blocked, nonfinite, records, merged}.
+// counts[o * kCnt] = {active, transparent, blocked, nonfinite, records, sorted/merged, windowed, 0}.
 constexpr int kChordBlock = 1024;
 constexpr int kChordMergeMax = 2048;
 
@@ -708,13 +737,497 @@ __global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restric
   if (threadIdx.x == 0) {
     tfrac[o] = ts / fs;
     fsum[o] = fs;
-    counts[o * 6 + 0] = n;
-    counts[o * 6 + 1] = ntr;
-    counts[o * 6 + 2] = nbl;
-    counts[o * 6 + 3] = nnf;
-    counts[o * 6 + 4] = G;
-    counts[o * 6 + 5] = do_merge ? 1 : 0;
+    counts[o * kCnt + 0] = n;
+    counts[o * kCnt + 1] = ntr;
+    counts[o * kCnt + 2] = nbl;
+    counts[o * kCnt + 3] = nnf;
+    counts[o * kCnt + 4] = G;
+    counts[o * kCnt + 5] = do_merge ? 1 : 0;
+    counts[o * kCnt + 6] = 0;
+    counts[o * kCnt + 7] = 0;
   }
+}
+
+// ---- windowed integration: per-phase record order, envelopes, threshold tables, tail moments ----
+// For one phase and one wavelength, tau_i = sum_s N_si sigma_s.  With n_si = N_si / Nmax_s (Nmax_s:
+// max over the phase's active chords) and q_s = sigma_s Nmax_s, every record i satisfies
+//     a_i Q <= tau_i <= b_i Q,   a_i = min_s n_si,  b_i = max_s n_si,  Q = sum_s q_s.
+// Records are ordered by b descending (ties: chord index), equal-column chords merged, and two
+// envelopes kept: B_i = max_{j >= i} b_j and A_i = min_{j <= i} a_j (both non-increasing in i).
+// For a wavefront whose wavelengths have Q in [Q_lo, Q_hi]:
+//   * records j >= t with B_t Q_hi < eps have tau_j < eps: their sum of F e^-tau is the cubic Taylor
+//     polynomial sum_e q^e M_e(t), with suffix moments M_e(t) = c_e sum_{j >= t} F_j prod_s n_sj^e_s
+//     (|e| <= 3, c_e = (-1)^|e| / prod e_s!); truncation error <= eps^4/24 per unit weight;
+//   * records j < h with A_h Q_lo >= tau_sat have tau_j >= tau_sat: skipped, error <= e^-tau_sat each;
+//   * records h <= j < t are integrated exactly (table exp).
+// eps = 2^-10, tau_sat = 40: |dR| <= 2^-40/24 + e^-40 < 4e-14 (merging adds <= 2^-40/e).
+// t and h come from per-phase tables indexed by the threshold's binade and top three mantissa bits
+// (X_v = the double with bits v << 49): tab_t[v] = #{i : B_i >= X_v}, tab_h[v] = #{i : A_i >= X_v};
+// the tau kernel picks the conservative neighbour (X_v <= eps/Q_hi for t, X_v > tau_sat/Q_lo for h).
+constexpr int kWBlock = 512;
+constexpr int kWPer = kWinMax / kWBlock;           // sorted positions per thread
+constexpr int kEnvVmax = 8184;                     // bits(1.0) >> 49
+constexpr int kEnvVmin = kEnvVmax - kEnvN + 1;     // X_vmin = 2^-256
+constexpr double kTailEps = 0x1p-10;
+constexpr double kTauSat = 40.0;
+
+template <int NS>
+struct Monos {
+  static constexpr int K = (NS + 1) * (NS + 2) * (NS + 3) / 6;
+  int e[K][NS];
+  double c[K];
+  constexpr Monos() : e{}, c{} {
+    int total = 1;
+    for (int s = 0; s < NS; ++s) total *= 4;
+    int k = 0;
+    for (int j = 0; j <= 3; ++j)
+      for (int idx = 0; idx < total; ++idx) {
+        int d[NS] = {};
+        int r = idx, sum = 0;
+        for (int s = NS - 1; s >= 0; --s) { d[s] = r % 4; r /= 4; sum += d[s]; }
+        if (sum != j) continue;
+        double f = 1.0;
+        for (int s = 0; s < NS; ++s) {
+          e[k][s] = d[s];
+          for (int m = 2; m <= d[s]; ++m) f *= m;
+        }
+        c[k] = ((j & 1) ? -1.0 : 1.0) / f;
+        ++k;
+      }
+  }
+};
+
+// prod_s p[s][e_s] for monomial k (p[s][j] = x_s^j)
+template <int NS>
+__device__ __forceinline__ double mono_eval(const Monos<NS>& M, int k, const double (&p)[NS][4]) {
+  double r = 1.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (M.e[k][s]) r *= p[s][M.e[k][s]];
+  return r;
+}
+
+struct OpAdd { template <typename T> __device__ T operator()(T a, T b) const { return a + b; } };
+struct OpMax { __device__ double operator()(double a, double b) const { return a > b ? a : b; } };
+struct OpMin { __device__ double operator()(double a, double b) const { return a < b ? a : b; } };
+
+// Exclusive scans over the kWBlock threads of a workgroup (8 waves); wsum: NW slots of LDS.
+// *total (optional) receives the fold over all threads.
+template <typename T, typename Op>
+__device__ __forceinline__ T wg_excl_prefix(T v, Op op, T id, T* wsum, T* total = nullptr) {
+  constexpr int NW = kWBlock / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T inc = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const T u = __shfl_up(inc, off, 64);
+    if (lane >= off) inc = op(inc, u);
+  }
+  T exc = __shfl_up(inc, 1, 64);
+  if (lane == 0) exc = id;
+  __syncthreads();
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  T carry = id, all = id;
+  for (int w = 0; w < NW; ++w) {
+    if (w < wid) carry = op(carry, wsum[w]);
+    all = op(all, wsum[w]);
+  }
+  if (total) *total = all;
+  return op(carry, exc);
+}
+
+template <typename T, typename Op>
+__device__ __forceinline__ T wg_excl_suffix(T v, Op op, T id, T* wsum) {
+  constexpr int NW = kWBlock / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T inc = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const T u = __shfl_down(inc, off, 64);
+    if (lane + off < 64) inc = op(inc, u);
+  }
+  T exc = __shfl_down(inc, 1, 64);
+  if (lane == 63) exc = id;
+  __syncthreads();
+  if (lane == 0) wsum[wid] = inc;
+  __syncthreads();
+  T carry = id;
+  for (int w = NW - 1; w > wid; --w) carry = op(carry, wsum[w]);
+  return op(carry, exc);
+}
+
+// #{i in [0, n) : v[i] >= x} for a non-increasing v
+__device__ __forceinline__ int32_t count_ge(const double* v, int32_t n, double x) {
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (v[mid] >= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// One workgroup per phase, designed around few dependent memory round trips:
+//  1. each thread loads kCPT consecutive chords (flags, F_out, N_s) per sweep, all loads issued
+//     before use; F_out and transparent sums, counts and Nmax_s are reduced over the workgroup;
+//  2. either the chord-order compaction of k_chords (phases with non-finite columns -> exact path;
+//     more than kWinMax active chords; neither merging nor windows requested), or
+//  3. the sorted path: keys (b descending, chord index) bitonic-sorted in LDS; each thread then owns
+//     kWPer consecutive sorted positions, fetches their columns (one round trip), marks group heads
+//     (equal 2^-40 keys of every species when merge != 0) and keeps its groups -- a contiguous range
+//     of record indices -- in registers: summed weights, envelopes, suffix tail moments and the
+//     sorted records are produced from there; threshold tables are searched in LDS.
+// counts[o * kCnt] = {active, transparent, blocked, nonfinite, records, sorted, windowed, 0}.
+constexpr int kCPT = kWinMax / kWBlock;            // chords per thread and sweep
+
+template <int NS>
+__global__ void __launch_bounds__(kWBlock) k_chords_w(const int32_t* __restrict__ flags,
+                                                      const double* __restrict__ fout,
+                                                      const double* __restrict__ ncol, int32_t n_pr,
+                                                      int32_t n_orb, int32_t merge, int32_t window,
+                                                      double* __restrict__ recs,
+                                                      int32_t* __restrict__ act_ip,
+                                                      double* __restrict__ mrecs,
+                                                      int32_t* __restrict__ counts,
+                                                      double* __restrict__ tfrac,
+                                                      double* __restrict__ fsum,
+                                                      double* __restrict__ nmax_out,
+                                                      int32_t* __restrict__ wenv,
+                                                      double* __restrict__ wmom) {
+  constexpr Monos<NS> M{};
+  constexpr int K = Monos<NS>::K;
+  constexpr int NW = kWBlock / 64;
+  constexpr int ST = 1 + NS;
+  __shared__ unsigned long long skey[kWinMax];   // sort keys; later the B envelope (as double)
+  __shared__ double sF[kWinMax];                 // member weights; later the A envelope
+  __shared__ int32_t sgid[kWinMax];
+  __shared__ double rd[NW][2 + NS];
+  __shared__ int32_t ri[NW][4];
+  __shared__ int32_t wi[NW];
+  __shared__ double wd[NW];
+  __shared__ double rk[NW][K];
+  const int32_t o = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int32_t* fl = flags + (int64_t)o * n_pr;
+  const int64_t nstride = (int64_t)n_orb * n_pr;
+  const double* nc0 = ncol + (int64_t)o * n_pr;
+
+  PROM_TS(o * 16 + 0);
+  // ---- 1. sums, counts, Nmax
+  double fpart = 0.0, tpart = 0.0;
+  double nm[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) nm[s] = 0.0;
+  int32_t ntr = 0, nbl = 0, nact = 0, nnf = 0;
+  for (int32_t sw = 0; sw < n_pr; sw += kWinMax) {
+    const int32_t c0 = sw + tid * kCPT;
+    int32_t f[kCPT];
+    double fo[kCPT], nv[kCPT][NS];
+#pragma unroll
+    for (int k = 0; k < kCPT; ++k) {
+      const int32_t ip = c0 + k;
+      const bool in = ip < n_pr;
+      f[k] = in ? fl[ip] : 3;
+      fo[k] = in ? fout[ip] : 0.0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) nv[k][s] = in ? nc0[s * nstride + ip] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kCPT; ++k) {
+      if (f[k] == 3) continue;
+      fpart += fo[k];
+      if (f[k] == 1) { tpart += fo[k]; ++ntr; }
+      else if (f[k] == 2) ++nbl;
+      else {
+        ++nact;
+        bool fin = true;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if (!__builtin_isfinite(nv[k][s])) fin = false;
+          else nm[s] = nv[k][s] > nm[s] ? nv[k][s] : nm[s];
+        }
+        if (!fin) ++nnf;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    fpart += __shfl_down(fpart, off, 64);
+    tpart += __shfl_down(tpart, off, 64);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double u = __shfl_down(nm[s], off, 64);
+      nm[s] = u > nm[s] ? u : nm[s];
+    }
+    ntr += __shfl_down(ntr, off, 64);
+    nbl += __shfl_down(nbl, off, 64);
+    nact += __shfl_down(nact, off, 64);
+    nnf += __shfl_down(nnf, off, 64);
+  }
+  if (lane == 0) {
+    rd[wid][0] = fpart;
+    rd[wid][1] = tpart;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) rd[wid][2 + s] = nm[s];
+    ri[wid][0] = ntr; ri[wid][1] = nbl; ri[wid][2] = nact; ri[wid][3] = nnf;
+  }
+  __syncthreads();
+  double fs = 0.0, ts = 0.0;
+  ntr = nbl = nact = nnf = 0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) nm[s] = 0.0;
+  for (int w = 0; w < NW; ++w) {
+    fs += rd[w][0];
+    ts += rd[w][1];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) nm[s] = rd[w][2 + s] > nm[s] ? rd[w][2 + s] : nm[s];
+    ntr += ri[w][0]; nbl += ri[w][1]; nact += ri[w][2]; nnf += ri[w][3];
+  }
+  double inv[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) inv[s] = nm[s] > 0.0 ? 1.0 / nm[s] : 0.0;
+
+  PROM_TS(o * 16 + 1);
+  const bool sorted = nnf == 0 && nact <= kWinMax && (merge || window);
+  int32_t G = nact;
+  // ---- 2. compaction in chord order (records or sort keys)
+  {
+    int32_t base = 0;
+    for (int32_t sw = 0; sw < n_pr; sw += kWinMax) {
+      const int32_t c0 = sw + tid * kCPT;
+      int32_t f[kCPT];
+      int32_t mine = 0;
+#pragma unroll
+      for (int k = 0; k < kCPT; ++k) {
+        const int32_t ip = c0 + k;
+        f[k] = ip < n_pr ? fl[ip] : 3;
+        mine += f[k] == 0 ? 1 : 0;
+      }
+      int32_t tot;
+      int32_t pos = base + wg_excl_prefix<int32_t>(mine, OpAdd(), 0, wi, &tot);
+#pragma unroll
+      for (int k = 0; k < kCPT; ++k) {
+        if (f[k] != 0) continue;
+        const int32_t ip = c0 + k;
+        if (sorted) {
+          double b = 0.0;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const double v = nc0[s * nstride + ip] * inv[s];
+            b = v > b ? v : b;
+          }
+          b = b < 1.0 ? b : 1.0;
+          const unsigned long long d =
+              (__builtin_bit_cast(unsigned long long, 1.0) - __builtin_bit_cast(unsigned long long, b)) >> 22;
+          skey[pos] = (d << 24) | (unsigned long long)ip;
+        } else {
+          act_ip[(int64_t)o * n_pr + pos] = ip;
+          double* r = recs + ((int64_t)o * n_pr + pos) * ST;
+          r[0] = fout[ip] / fs;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) r[1 + s] = nc0[s * nstride + ip];
+        }
+        ++pos;
+      }
+      base += tot;
+    }
+  }
+  PROM_TS(o * 16 + 2);
+  if (sorted) {
+    // ---- 3a. bitonic sort of the keys
+    const int32_t n = nact;
+    int32_t P = 1;
+    while (P < n) P <<= 1;
+    for (int32_t i = n + tid; i < P; i += kWBlock) skey[i] = ~0ull;
+    __syncthreads();
+    for (int32_t size = 2; size <= P; size <<= 1) {
+      for (int32_t st = size >> 1; st > 0; st >>= 1) {
+        for (int32_t t = tid; t < P / 2; t += kWBlock) {
+          const int32_t i = 2 * t - (t & (st - 1));
+          const int32_t j = i + st;
+          const bool up = (i & size) == 0;
+          const unsigned long long a = skey[i], b = skey[j];
+          if ((a > b) == up) { skey[i] = b; skey[j] = a; }
+        }
+        __syncthreads();
+      }
+    }
+    PROM_TS(o * 16 + 3);
+    // ---- 3b. this thread's sorted positions [i0, i0 + cnt): columns, group heads
+    const int32_t i0 = min(n, tid * kWPer);
+    const int32_t cnt = min(n, i0 + kWPer) - i0;
+    double Nv[kWPer][NS], Fv[kWPer];
+    unsigned long long pk[NS];
+    {
+      const int32_t ipp = i0 > 0 ? (int32_t)(skey[i0 - 1] & 0xffffffull) : 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) pk[s] = (i0 > 0 && cnt > 0) ? mkey(nc0[s * nstride + ipp]) : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) {
+      const int32_t ip = k < cnt ? (int32_t)(skey[i0 + k] & 0xffffffull) : 0;
+      Fv[k] = k < cnt ? fout[ip] : 0.0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) Nv[k][s] = k < cnt ? nc0[s * nstride + ip] : 0.0;
+    }
+    uint32_t headbits = 0;
+    int32_t nheads = 0;
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) {
+      if (k >= cnt) break;
+      bool head = !merge || (i0 + k) == 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const unsigned long long kk = mkey(Nv[k][s]);
+        if ((i0 + k) > 0 && kk != pk[s]) head = true;
+        pk[s] = kk;
+      }
+      Fv[k] = Fv[k] / fs;
+      sF[i0 + k] = Fv[k];
+      if (head) { headbits |= 1u << k; ++nheads; }
+    }
+    int32_t gtot;
+    const int32_t gb = wg_excl_prefix<int32_t>(nheads, OpAdd(), 0, wi, &gtot);
+    {
+      int32_t g = gb - 1;
+      for (int k = 0; k < cnt; ++k) {
+        if ((headbits >> k) & 1u) ++g;
+        sgid[i0 + k] = g;
+      }
+    }
+    G = gtot;
+    __syncthreads();
+    PROM_TS(o * 16 + 4);
+    // ---- 3c. this thread's groups gb .. gb + nheads - 1: summed weight, head's columns, b, a
+    double* mo = mrecs + (int64_t)o * n_pr * ST;
+    double gF[kWPer], bb[kWPer], aa[kWPer];
+    double bmax = 0.0, amin = 1.0e308;
+    {
+      int h = 0;
+#pragma unroll
+      for (int k = 0; k < kWPer; ++k) {
+        gF[k] = 0.0; bb[k] = 0.0; aa[k] = 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < kWPer; ++k) {
+        if (!((headbits >> k) & 1u)) continue;
+        const int32_t i = i0 + k, gi = gb + h;
+        double F = Fv[k];
+        for (int32_t j = i + 1; j < n && sgid[j] == gi; ++j) F += sF[j];
+        double* r = mo + (int64_t)gi * ST;
+        r[0] = F;
+        double b = 0.0, a = 1.0e308;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          r[1 + s] = Nv[k][s];
+          const double v = Nv[k][s] * inv[s];
+          b = v > b ? v : b;
+          a = v < a ? v : a;
+        }
+        // compact the thread's groups to slots 0 .. nheads-1 (k >= h always)
+#pragma unroll
+        for (int m = 0; m < kWPer; ++m)
+          if (m == h) {
+            gF[m] = F; bb[m] = b; aa[m] = a;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) Nv[m][s] = Nv[k][s];
+          }
+        bmax = b > bmax ? b : bmax;
+        amin = a < amin ? a : amin;
+        ++h;
+      }
+    }
+    PROM_TS(o * 16 + 5);
+    if (window) {
+      // ---- 3d. envelopes B (suffix max of b), A (prefix min of a) over records, into LDS
+      double* sB = reinterpret_cast<double*>(skey);
+      double* sA = sF;
+      const double bcarry = wg_excl_suffix<double>(bmax, OpMax(), 0.0, wd);
+      const double acarry = wg_excl_prefix<double>(amin, OpMin(), 1.0e308, wd);   // barriers: LDS reuse ok
+      double run = bcarry;
+#pragma unroll
+      for (int m = kWPer - 1; m >= 0; --m)
+        if (m < nheads) { run = bb[m] > run ? bb[m] : run; sB[gb + m] = run; }
+      run = acarry;
+#pragma unroll
+      for (int m = 0; m < kWPer; ++m)
+        if (m < nheads) { run = aa[m] < run ? aa[m] : run; sA[gb + m] = run; }
+      PROM_TS(o * 16 + 6);
+      // ---- 3e. suffix tail moments  M_e(g) = c_e sum_{j >= g} F_j n_j^e
+      double part[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) part[k] = 0.0;
+#pragma unroll
+      for (int m = 0; m < kWPer; ++m)
+        if (m < nheads) {
+          double pw[NS][4];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const double v = Nv[m][s] * inv[s];
+            pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k) part[k] += gF[m] * mono_eval<NS>(M, k, pw);
+        }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        double inc = part[k];
+        for (int off = 1; off < 64; off <<= 1) {
+          const double u = __shfl_down(inc, off, 64);
+          if (lane + off < 64) inc += u;
+        }
+        double exc = __shfl_down(inc, 1, 64);
+        if (lane == 63) exc = 0.0;
+        if (lane == 0) rk[wid][k] = inc;
+        part[k] = exc;
+      }
+      __syncthreads();
+      double* mm = wmom + (int64_t)o * (n_pr + 1) * K;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        double c = part[k];
+        for (int w = NW - 1; w > wid; --w) c += rk[w][k];
+        part[k] = c;
+      }
+#pragma unroll
+      for (int m = kWPer - 1; m >= 0; --m)
+        if (m < nheads) {
+          double pw[NS][4];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const double v = Nv[m][s] * inv[s];
+            pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            part[k] += gF[m] * mono_eval<NS>(M, k, pw);
+            mm[(int64_t)(gb + m) * K + k] = M.c[k] * part[k];
+          }
+        }
+      if (tid < K) mm[(int64_t)G * K + tid] = 0.0;
+      PROM_TS(o * 16 + 7);
+      // ---- 3f. threshold tables (LDS searches)
+      int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
+      for (int32_t e = tid; e < kEnvN; e += kWBlock) {
+        const double X = __builtin_bit_cast(double, (unsigned long long)(kEnvVmin + e) << 49);
+        et[e] = count_ge(sB, G, X);
+        et[kEnvN + e] = count_ge(sA, G, X);
+      }
+    }
+  }
+  if (tid == 0) {
+    tfrac[o] = ts / fs;
+    fsum[o] = fs;
+    counts[o * kCnt + 0] = nact;
+    counts[o * kCnt + 1] = ntr;
+    counts[o * kCnt + 2] = nbl;
+    counts[o * kCnt + 3] = nnf;
+    counts[o * kCnt + 4] = G;
+    counts[o * kCnt + 5] = sorted ? 1 : 0;
+    counts[o * kCnt + 6] = (sorted && window) ? 1 : 0;
+    counts[o * kCnt + 7] = 0;
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (tid == s) nmax_out[o * NS + s] = nm[s];
+  PROM_TS(o * 16 + 8);
 }
 
 // ---- fast exp: acc + F * 2^(y/2048) with a 2048-entry table in LDS --------------------------------
@@ -743,6 +1256,14 @@ __device__ __forceinline__ void fill_exp_table(double* etab) {
   for (int i = threadIdx.x; i < PROM_EXP2_TABLE_N; i += kBlock) etab[i] = kExp2TableDev[i];
 }
 
+// Table index of a positive float threshold: the largest v with X_v = double(bits v << 49) <= x;
+// below the table for zero/denormal x, above it for +inf.
+__device__ __forceinline__ int env_floor(float x) {
+  if (!(x >= 1.17549435e-38f)) return -(1 << 28);
+  if (!(x <= 3.40282347e+38f)) return 1 << 28;
+  return (int)(__builtin_bit_cast(uint32_t, x) >> 20) + 7168;
+}
+
 // Fused sigma lookup -> tau -> exp(-tau) -> disk sum -> ratio.
 // Grid: (wavelength tiles of kBlock, phase groups).  A thread owns one wavelength and walks the
 // phases of its group: per phase it refreshes sigma_s = 10^interp(shift_o lambda) - offset (only
@@ -761,8 +1282,16 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
                                                 const double* __restrict__ tfrac,
                                                 const double* __restrict__ fsum, int32_t n_atoms_rt,
                                                 int32_t n_pr, int32_t n_orb, int32_t phases_per_group,
-                                                int64_t n_wav, double* __restrict__ R) {
-  extern __shared__ double lds[];   // [2048] exp table | NS == 0: [3][n_atoms][kBlock]
+                                                int64_t n_wav, const double* __restrict__ nmax,
+                                                const int32_t* __restrict__ wenv,
+                                                const double* __restrict__ wmom,
+                                                unsigned long long* __restrict__ evals,
+                                                double* __restrict__ R) {
+  PROM_CLK(tk0);
+#ifdef PROM_TRACE
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) { g_trace[4002] = wall_clock64(); g_trace[4003] = clock64(); }
+#endif
+  extern __shared__ double lds[];   // [2048] exp table | NS == 0: [2][n_atoms][kBlock]
   double* etab = lds;
   double* sgl = lds + (EXPK ? PROM_EXP2_TABLE_N : 0);
   if (EXPK) fill_exp_table(etab);
@@ -777,40 +1306,98 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
   constexpr int NR = NS > 0 ? NS : 1;
   double sg[NR];            // sigma_s at the current phase (NS > 0)
   double shv[NR];           // Doppler factor sg was computed for
-  int64_t hint[NR];
 #pragma unroll
-  for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); hint[s] = -1; }
+  for (int s = 0; s < NR; ++s) shv[s] = __builtin_nan("");
   double* sg_l = sgl;                                  // NS == 0: [ns][kBlock]
   double* sh_l = sgl + (int64_t)ns * kBlock;           // NS == 0: [ns][kBlock]
-  int64_t* hi_l = reinterpret_cast<int64_t*>(sgl + 2 * (int64_t)ns * kBlock);
   if constexpr (NS == 0) {
-    for (int32_t s = 0; s < ns; ++s) { sh_l[s * kBlock + threadIdx.x] = __builtin_nan(""); hi_l[s * kBlock + threadIdx.x] = -1; }
+    for (int32_t s = 0; s < ns; ++s) sh_l[s * kBlock + threadIdx.x] = __builtin_nan("");
   }
   for (int32_t o = o0; o < o1; ++o) {
-    const bool exact = !EXPK || counts[o * 6 + 3] != 0;
-    const bool merged = !exact && counts[o * 6 + 5] != 0;
-    const int32_t n_act = counts[o * 6 + (merged ? 4 : 0)];
-    const double* __restrict__ rec = (merged ? mrecs : recs) + (int64_t)o * n_pr * stride;
+    PROM_CLK(tc0);
+    const bool exact = !EXPK || counts[o * kCnt + 3] != 0;
+    const bool sorted = !exact && counts[o * kCnt + 5] != 0;
+    const bool win = sorted && counts[o * kCnt + 6] != 0;
+    const int32_t n_act = counts[o * kCnt + (sorted ? 4 : 0)];
+    const double* __restrict__ rec = (sorted ? mrecs : recs) + (int64_t)o * n_pr * stride;
     double acc = 0.0;
     if constexpr (NS > 0) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const double sh = tabs[s].shift[o];
         if (!(sh == shv[s])) {
-          sg[s] = exp10(np_interp_hint(sh * lam, tabs[s].x, tabs[s].y, tabs[s].n, hint[s])) - tabs[s].offset;
+          sg[s] = sigma_of(sh * lam, tabs[s]);
           shv[s] = sh;
         }
       }
+      PROM_CLK(tc1);
       if (!exact) {
         double sp[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) sp[s] = sg[s] * kMinus2048OverLn2;
-        for (int32_t i = 0; i < n_act; ++i) {
+        int32_t i_lo = 0, i_hi = n_act;
+        double q[NS];
+        if (win) {
+          // window [h, t) of this wavefront (see "windowed integration" above k_chords_w)
+          double Q = 0.0;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) { q[s] = sg[s] * nmax[o * NS + s]; Q += q[s]; }
+          const bool bad = !(Q <= 1.0e100);
+          const float qf = (float)Q;
+          float qh = qf * (1.0f + 0x1p-20f), ql = qf * (1.0f - 0x1p-20f);
+          for (int off = 32; off > 0; off >>= 1) {
+            qh = fmaxf(qh, __shfl_xor(qh, off, 64));
+            ql = fminf(ql, __shfl_xor(ql, off, 64));
+          }
+          if (__ballot(bad) == 0ull) {
+            const int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
+            const int vt = env_floor((float)kTailEps / qh * (1.0f - 0x1p-20f));
+            const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
+            int32_t t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? n_act : et[vt - kEnvVmin]);
+            int32_t h = vh >= kEnvVmax ? 0 : et[kEnvN + (vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin)];
+            h = h < t ? h : t;
+            i_lo = __builtin_amdgcn_readfirstlane(h);
+            i_hi = __builtin_amdgcn_readfirstlane(t);
+          }
+        }
+        PROM_CLK(tc2);
+        for (int32_t i = i_lo; i < i_hi; ++i) {
           const double* r = rec + (int64_t)i * stride;
           double y = r[1] * sp[0];
 #pragma unroll
           for (int s = 1; s < NS; ++s) y = __builtin_fma(r[1 + s], sp[s], y);
           acc = acc_exp2k(acc, r[0], y, etab);
+        }
+        PROM_CLK(tc3);
+        if (win && i_hi < n_act) {
+          // records [t, G): cubic Taylor polynomial in q from the suffix moments
+          constexpr Monos<NS> M{};
+          const double* mm = wmom + ((int64_t)o * (n_pr + 1) + i_hi) * Monos<NS>::K;
+          double p[NS][4];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) { p[s][0] = 1.0; p[s][1] = q[s]; p[s][2] = q[s] * q[s]; p[s][3] = p[s][2] * q[s]; }
+          double tl = 0.0;
+#pragma unroll
+          for (int k = 0; k < Monos<NS>::K; ++k) tl = __builtin_fma(mm[k], mono_eval<NS>(M, k, p), tl);
+          acc += tl;
+        }
+#ifdef PROM_TRACE
+        {
+          const long long tc4 = clock64();
+          const int64_t wv = 65536 + 8 * (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6));
+          PROM_ACC(wv + 0, tc1 - tc0);
+          PROM_ACC(wv + 1, tc2 - tc1);
+          PROM_ACC(wv + 2, tc3 - tc2);
+          PROM_ACC(wv + 3, tc4 - tc3);
+          PROM_ACC(wv + 4, 1);
+          PROM_ACC(wv + 5, i_hi - i_lo);
+        }
+#endif
+        if (evals) {
+          const int nl = __popcll(__ballot(live));
+          if ((threadIdx.x & 63) == 0)
+            atomicAdd(&evals[(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & 63],
+                      (unsigned long long)(i_hi - i_lo) * (unsigned long long)nl);
         }
       } else {
         const int32_t* ipl = act_ip + (int64_t)o * n_pr;
@@ -827,9 +1414,7 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
         const int64_t li = (int64_t)s * kBlock + threadIdx.x;
         const double sh = tabs[s].shift[o];
         if (!(sh == sh_l[li])) {
-          int64_t h = hi_l[li];
-          sg_l[li] = exp10(np_interp_hint(sh * lam, tabs[s].x, tabs[s].y, tabs[s].n, h)) - tabs[s].offset;
-          hi_l[li] = h;
+          sg_l[li] = sigma_of(sh * lam, tabs[s]);
           sh_l[li] = sh;
         }
       }
@@ -852,6 +1437,16 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
     }
     if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
   }
+#ifdef PROM_TRACE
+  {
+    const int64_t wv = 65536 + 8 * (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6));
+    PROM_ACC(wv + 6, clock64() - tk0);
+    PROM_ACC(wv + 7, 1);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+      g_trace[4000] = wall_clock64(); g_trace[4001] = clock64();
+    }
+  }
+#endif
 }
 
 // ---- molecular fused kernel -------------------------------------------------------------------
@@ -889,20 +1484,19 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabDev* __restrict_
   constexpr int ST = 1 + NSA;
   constexpr int NR = NSA > 0 ? NSA : 1;
   double sg[NR], shv[NR];
-  int64_t hint[NR];
 #pragma unroll
-  for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); hint[s] = -1; sg[s] = 0.0; }
+  for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); sg[s] = 0.0; }
   int64_t whint[4] = {-1, -1, -1, -1};
   const int64_t nc = (int64_t)n_orb * n_pr;
   for (int32_t o = o0; o < o1; ++o) {
-    const bool exact = !EXPK || counts[o * 6 + 3] != 0;
-    const int32_t n_act = counts[o * 6 + 0];
+    const bool exact = !EXPK || counts[o * kCnt + 3] != 0;
+    const int32_t n_act = counts[o * kCnt + 0];
     const double* __restrict__ rec = recs + (int64_t)o * n_pr * ST;
 #pragma unroll
     for (int s = 0; s < NSA; ++s) {
       const double sh = tabs[s].shift[o];
       if (!(sh == shv[s])) {
-        sg[s] = exp10(np_interp_hint(sh * lam, tabs[s].x, tabs[s].y, tabs[s].n, hint[s])) - tabs[s].offset;
+        sg[s] = sigma_of(sh * lam, tabs[s]);
         shv[s] = sh;
       }
     }
@@ -1027,11 +1621,28 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
                        tr.molcol.as<double>(), tr.flags.as<int32_t>());
     PROM_HIP(hipGetLastError());
   }
-  // 2. per-phase compaction (+ merging of equal-column chords)
-  hipLaunchKernelGGL(k_chords, dim3(tr.n_orb), dim3(kChordBlock), 0, s, tr.flags.as<int32_t>(),
-                     tr.cfout.as<double>(), tr.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
-                     (tr.merge && tr.exp_mode && tr.n_mol == 0) ? 1 : 0, tr.recs.as<double>(), tr.act_ip.as<int32_t>(),
-                     tr.mrecs.as<double>(), tr.counts.as<int32_t>(), tr.tsum.as<double>(), tr.fsum.as<double>());
+  // 2. per-phase compaction, ordering, merging of equal-column chords, window tables
+  const bool wpath = tr.exp_mode && tr.n_mol == 0 && tr.n_atoms >= 1 && tr.n_atoms <= kWinMaxSpecies;
+  if (wpath) {
+#define PROM_CHW(NSV)                                                                                   \
+  hipLaunchKernelGGL(k_chords_w<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, tr.flags.as<int32_t>(),      \
+                     tr.cfout.as<double>(), tr.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
+                     tr.window ? 1 : 0, tr.recs.as<double>(), tr.act_ip.as<int32_t>(), tr.mrecs.as<double>(), \
+                     tr.counts.as<int32_t>(), tr.tsum.as<double>(), tr.fsum.as<double>(), tr.nmax.as<double>(), \
+                     tr.wenv.as<int32_t>(), tr.wmom.as<double>())
+    switch (tr.n_atoms) {
+      case 1: PROM_CHW(1); break;
+      case 2: PROM_CHW(2); break;
+      case 3: PROM_CHW(3); break;
+      default: PROM_CHW(4); break;
+    }
+#undef PROM_CHW
+  } else {
+    hipLaunchKernelGGL(k_chords, dim3(tr.n_orb), dim3(kChordBlock), 0, s, tr.flags.as<int32_t>(),
+                       tr.cfout.as<double>(), tr.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
+                       (tr.merge && tr.exp_mode && tr.n_mol == 0) ? 1 : 0, tr.recs.as<double>(), tr.act_ip.as<int32_t>(),
+                       tr.mrecs.as<double>(), tr.counts.as<int32_t>(), tr.tsum.as<double>(), tr.fsum.as<double>());
+  }
   PROM_HIP(hipGetLastError());
   PROM_HIP(hipEventRecord(ev[1], s));
   // 2. (sigma is fused into the tau kernel; the event pair brackets nothing since round 1.2)
@@ -1058,8 +1669,10 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
 #define PROM_TAU(NSV, EK)                                                                              \
   hipLaunchKernelGGL((k_tau<NSV, EK>), g, dim3(kBlock),                                                \
                      ((EK) ? PROM_EXP2_TABLE_N * sizeof(double) : 0) +                                  \
-                         ((NSV) == 0 ? (size_t)3 * na * kBlock * sizeof(double) : 0),                  \
-                     s, tabs, wav, recs, mrecs, aip, fo, counts, tf, fs, na, tr.n_pr, tr.n_orb, ppg, tr.n_wav, R)
+                         ((NSV) == 0 ? (size_t)2 * na * kBlock * sizeof(double) : 0),                  \
+                     s, tabs, wav, recs, mrecs, aip, fo, counts, tf, fs, na, tr.n_pr, tr.n_orb, ppg, tr.n_wav, \
+                     tr.nmax.as<double>(), tr.wenv.as<int32_t>(), tr.wmom.as<double>(),                     \
+                     tr.count_evals ? tr.evals.as<unsigned long long>() : nullptr, R)
 #define PROM_TAU_NS(EK)                 \
   switch (na) {                         \
     case 1: PROM_TAU(1, EK); break;     \
@@ -1098,3 +1711,14 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
 }
 
 }  // namespace prom
+
+#ifdef PROM_TRACE
+extern "C" int32_t prom_trace_read(unsigned long long* out, int32_t n, int32_t reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(prom::g_trace), sizeof(unsigned long long) * n) != hipSuccess) return -2;
+  if (reset) {
+    static unsigned long long z[1 << 20] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(prom::g_trace), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

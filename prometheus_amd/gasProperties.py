@@ -490,8 +490,16 @@ class WavelengthGrid:
 
 
 # ============================================================================== transit
+# Shard and chunk boundaries are multiples of one wavefront (64 wavelengths): the tau kernel's
+# integration window is chosen per wavefront, so aligned boundaries keep every wavefront's set of
+# wavelengths -- and hence R, bit for bit -- independent of the number of shards and chunks.
+WAVE_ALIGN = 64
+
+
 def _split(n: int, parts: int) -> List[Tuple[int, int]]:
-    edges = np.linspace(0, n, parts + 1).round().astype(np.int64)
+    edges = (np.linspace(0, n / WAVE_ALIGN, parts + 1).round() * WAVE_ALIGN).astype(np.int64)
+    edges[-1] = n
+    edges = np.minimum(edges, n)
     return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:]) if b > a]
 
 
@@ -593,7 +601,7 @@ class Transit:
         n_atoms = sum(1 for d in self.atmosphere.densityDistributionList for c in d.constituents
                       if not c.isMolecule)
         per_wav = 8 * n_orb * (2 + max(1, n_atoms))
-        chunk = max(4096, int(max_memory_gb * 1e9) // per_wav)
+        chunk = max(4096, int(max_memory_gb * 1e9) // per_wav) // WAVE_ALIGN * WAVE_ALIGN
         R = np.empty((n_orb, n_wav))
         shards = _split(n_wav, len(devices))
         errors: List[BaseException] = []

@@ -148,7 +148,8 @@ def test_chord_merging(dev, name):
     st_m = tr.last_stats[-1]
     R_n = tr.sumOverChords(devices=[0], options=_native.OPT_NO_MERGE)
     st_n = tr.last_stats[-1]
-    assert np.max(np.abs(R_m - R_n)) <= 2.0 ** -40 / np.e + 1e-15
+    # merging moves R by <= 2^-40/e; both runs are windowed (<= 2^-40/24 + e^-40 each vs full evaluation)
+    assert np.max(np.abs(R_m - R_n)) <= 2.0 ** -40 / np.e + 2 * (2.0 ** -40 / 24 + np.exp(-40.0)) + 1e-15
     assert st_n["tau_records"] == st_n["active_chords"]
     assert st_m["tau_records"] <= st_m["active_chords"]
     print(name, "records merged %d -> %d" % (st_m["active_chords"], st_m["tau_records"]))
@@ -183,3 +184,33 @@ def test_transit_c2_full_grid_sampled(dev):
     print("C2 sampled max rel err %.3e" % err)
     assert err < R_TOL
     assert np.all(np.isfinite(R)) and np.all((R > 0) & (R <= 1.0 + 1e-12))
+
+
+@pytest.mark.parametrize("name", ["C1", "C2r", "C3r", "C4r", "exomoon"])
+def test_windowed_integration(dev, name):
+    """Windowed integration (saturated-head skip + cubic tail moments) against full
+    evaluation of every record: |dR| <= 2^-40/24 + e^-40 (+ rounding), and fewer exp evaluations."""
+    from prometheus_amd import _native
+    d = load("transit_" + name)
+    tr = _product_transit(json.loads(str(d["config"])))
+    R_w = tr.sumOverChords(devices=[0])
+    st_w = tr.last_stats[-1]
+    R_f = tr.sumOverChords(devices=[0], options=_native.OPT_NO_WINDOW)
+    st_f = tr.last_stats[-1]
+    bound = 2.0 ** -40 / 24 + np.exp(-40.0) + 1e-15
+    diff = float(np.max(np.abs(R_w - R_f)))
+    print(name, "window |dR| %.3e, exp evals %d -> %d" % (diff, st_f["exp_evals"], st_w["exp_evals"]))
+    assert diff <= bound
+    assert st_w["exp_evals"] <= st_f["exp_evals"]
+    assert st_f["exp_evals"] == st_f["tau_records"] * R_f.shape[1]
+    assert rel(R_w, d["R"]) < R_TOL
+
+
+def test_windowed_no_merge_no_window_matches_reference(dev):
+    """All four combinations of merging and windows agree with the reference on C2r."""
+    from prometheus_amd import _native
+    d = load("transit_C2r")
+    tr = _product_transit(json.loads(str(d["config"])))
+    for opt in (0, _native.OPT_NO_MERGE, _native.OPT_NO_WINDOW, _native.OPT_NO_MERGE | _native.OPT_NO_WINDOW):
+        R = tr.sumOverChords(devices=[0], options=opt)
+        assert rel(R, d["R"]) < R_TOL, opt
