@@ -71,7 +71,8 @@ int32_t prom_create(int32_t device, prom_ctx** out) {
   prom_ctx* ctx = new (std::nothrow) prom_ctx();
   if (!ctx) return PROM_E_NOMEM;
   ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream1, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return PROM_E_HIP;
   }
@@ -81,6 +82,7 @@ int32_t prom_create(int32_t device, prom_ctx** out) {
       return PROM_E_HIP;
     }
   }
+
   *out = ctx;
   return PROM_OK;
 }
@@ -92,6 +94,8 @@ void prom_destroy(prom_ctx* ctx) {
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->tev) (void)hipEventDestroy(e);
+  if (ctx->stream1) (void)hipStreamSynchronize(ctx->stream1);
+  if (ctx->stream1) (void)hipStreamDestroy(ctx->stream1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;  // DevBuf destructors free device memory
 }
@@ -99,15 +103,18 @@ void prom_destroy(prom_ctx* ctx) {
 const char* prom_last_error(const prom_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 int32_t prom_synchronize(prom_ctx* ctx) {
-  return guarded(ctx, [&] { PROM_HIP(hipStreamSynchronize(ctx->stream)); });
+  return guarded(ctx, [&] {
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+    PROM_HIP(hipStreamSynchronize(ctx->stream1));
+  });
 }
 
 // ------------------------------------------------------------------------------ tables
-// Bucket directory of a table's nodes: n_dir equal buckets over [x0, x[n-1]], dir[j] = number of
+// Bucket directory of a table's nodes: n_dir = 4 n equal buckets over [x0, x[n-1]], dir[j] = number of
 // nodes <= x0 + j h.  The tau kernel starts its np.interp bracket search from buckets j, j+1 of a
 // target and verifies the bracket, so rounding in j only costs steps, never correctness.
 static void build_directory(prom_ctx* ctx, prom::AtomTable& t, const double* x, int64_t n) {
-  const int64_t nd = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)1 << 24));
+  const int64_t nd = std::max<int64_t>(1, std::min<int64_t>(4 * n, (int64_t)1 << 26));
   const double x0 = x[0], span = x[n - 1] - x[0];
   std::vector<int32_t> d(nd + 1);
   const double h = span > 0.0 ? span / (double)nd : 1.0;
@@ -298,6 +305,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.delta_x = pb->delta_x;
     tr.planet_R = pb->planet_R;
     tr.cull_tau = pb->cull_tau > 0.0 ? pb->cull_tau : std::ldexp(1.0, -60);
+    PROM_HIP(hipStreamSynchronize(ctx->stream1));   // a pipelined run may still read the old problem
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
     tr.exp_mode = (pb->options & PROM_OPT_OCML_EXP) ? 0 : 1;
     tr.merge = (pb->options & PROM_OPT_NO_MERGE) == 0;
     tr.window = (pb->options & PROM_OPT_NO_WINDOW) == 0;
@@ -382,15 +391,45 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     }
     upload(tr.molslot, tr.mslots.data(), (int64_t)tr.mslots.size(), s);
     {
+      // per-scenario density bound n_ref (every built-in model peaks at p[0] = n_0 on its domain;
+      // tabulated: the largest finite value) -> column normalisation c_s = 1 / (chi_s n_ref n_x dx)
+      std::vector<double> nref(tr.n_sc, 0.0);
+      for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
+        const prom_scenario& S = pb->scenarios[sc];
+        if (S.density.kind == PROM_DENSITY_TABULATED) {
+          double m = 0.0;
+          const int64_t cnt = n_orb * tr.n_pr * tr.n_x;
+          for (int64_t i = 0; i < cnt; ++i) {
+            const double v = std::fabs(S.n_tabulated[i]);
+            if (std::isfinite(v) && v > m) m = v;
+          }
+          nref[sc] = m;
+        } else {
+          nref[sc] = std::fabs(S.density.p[0]);
+        }
+      }
       std::vector<prom::SigTabDev> st;
       for (const auto& t : tr.terms) {
         if (t.is_molecule) continue;
         const prom::AtomTable& tb = ctx->tables[t.table];
+        const double bound = std::fabs(t.chi) * nref[t.scenario] * (double)tr.n_x * tr.delta_x;
+        const double c = (bound > 0.0 && std::isfinite(bound)) ? 1.0 / bound : 0.0;
+        // an overflowing bound cannot normalise the columns: integrate without windows
+        if (!std::isfinite(bound) || (bound > 0.0 && !(c > 0.0))) tr.window = false;
+        const double inv = (c > 0.0 && std::isfinite(c)) ? bound : 0.0;
         st.push_back({tb.x.as<double>(), tb.y.as<double>(), tb.n, tb.offset,
                       tr.shift.as<double>() + (int64_t)t.scenario * n_orb, tb.dir.as<int32_t>(), tb.n_dir, 0,
-                      tb.dir_x0, tb.dir_inv_h});
+                      tb.dir_x0, tb.dir_inv_h, std::isfinite(c) ? c : 0.0, inv});
       }
       upload(tr.sigtab, st.data(), (int64_t)st.size(), s);
+      tr.uniform_shift = true;
+      for (const auto& t : tr.terms) {
+        if (t.is_molecule) continue;
+        for (int64_t o = 1; o < n_orb; ++o)
+          if (!(sh[t.scenario * n_orb + o] == sh[t.scenario * n_orb])) tr.uniform_shift = false;
+      }
+      tr.sigtab_v = prom::SigTabs4{};
+      for (size_t i = 0; i < st.size() && i < 4; ++i) tr.sigtab_v.t[i] = st[i];
     }
     tr.tab.ensure(sizeof(double) * std::max<int64_t>(tab_total, 1));
     {
@@ -400,6 +439,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         sd[sc].tab = tr.tab_off[sc] >= 0 ? tr.tab.as<double>() + tr.tab_off[sc] : nullptr;
       }
       upload(tr.scdev, sd.data(), (int64_t)sd.size(), s);
+      tr.colargs = prom::ColArgs{};
+      for (int32_t i = 0; i < tr.n_sc && i < 4; ++i) tr.colargs.sc[i] = sd[i];
+      for (int32_t i = 0; i < tr.n_terms && i < 8; ++i) tr.colargs.t[i] = tr.terms[i];
     }
     for (int32_t sc = 0; sc < tr.n_sc; ++sc)
       if (tr.tab_off[sc] >= 0)
@@ -408,27 +450,32 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     // work buffers
     const int64_t nc = n_orb * tr.n_pr;
     tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
-    tr.ncol.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * nc);
-    tr.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
-    if (n_mol > 0) {
-      tr.mol_ip.ensure(sizeof(int32_t) * n_mol * nc * tr.n_x);
-      tr.mol_wp.ensure(sizeof(double) * n_mol * nc * tr.n_x);
-      tr.mol_na.ensure(sizeof(double) * n_mol * nc * tr.n_x);
+    tr.pipelined = tr.exp_mode && n_mol == 0 && n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && tr.window;
+    for (int si = 0; si < (tr.pipelined ? 2 : 1); ++si) {
+    prom::RunSlot& rs = tr.slot[si];
+      rs.ncol.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * nc);
+      tr.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
+      if (n_mol > 0) {
+        tr.mol_ip.ensure(sizeof(int32_t) * n_mol * nc * tr.n_x);
+        tr.mol_wp.ensure(sizeof(double) * n_mol * nc * tr.n_x);
+        tr.mol_na.ensure(sizeof(double) * n_mol * nc * tr.n_x);
+      }
+      rs.flags.ensure(sizeof(int32_t) * nc);
+      rs.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
+      rs.act_ip.ensure(sizeof(int32_t) * nc);
+      rs.counts.ensure(sizeof(int32_t) * n_orb * prom::kCnt);
+      rs.mrecs.ensure(sizeof(double) * nc * (1 + n_atoms));
+      if (n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && n_mol == 0) {
+        rs.wenv.ensure(sizeof(int32_t) * n_orb * 2 * prom::kEnvN);
+        rs.wmom.ensure(sizeof(double) * n_orb * (tr.n_pr + 1) * prom::n_tail_moments(n_atoms));
+      }
+      rs.evals.ensure(sizeof(unsigned long long) * 64);
+      rs.sig.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * tr.n_wav);
+      rs.tsum.ensure(sizeof(double) * n_orb);
+      rs.fsum.ensure(sizeof(double) * n_orb);
+      rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);
     }
-    tr.flags.ensure(sizeof(int32_t) * nc);
-    tr.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
-    tr.act_ip.ensure(sizeof(int32_t) * nc);
-    tr.counts.ensure(sizeof(int32_t) * n_orb * prom::kCnt);
-    tr.mrecs.ensure(sizeof(double) * nc * (1 + n_atoms));
-    tr.nmax.ensure(sizeof(double) * n_orb * std::max<int64_t>(n_atoms, 1));
-    if (n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && n_mol == 0) {
-      tr.wenv.ensure(sizeof(int32_t) * n_orb * 2 * prom::kEnvN);
-      tr.wmom.ensure(sizeof(double) * n_orb * (tr.n_pr + 1) * prom::n_tail_moments(n_atoms));
-    }
-    tr.evals.ensure(sizeof(unsigned long long) * 64);
-    tr.tsum.ensure(sizeof(double) * n_orb);
-    tr.fsum.ensure(sizeof(double) * n_orb);
-    tr.R.ensure(sizeof(double) * n_orb * tr.n_wav);
+    tr.last = 0;
     PROM_HIP(hipStreamSynchronize(s));
     tr.ready = true;
   });
@@ -451,8 +498,14 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
       ++ctx->timed_runs;
     }
     tr.count_evals = stats != nullptr;
-    if (tr.count_evals) PROM_HIP(hipMemsetAsync(tr.evals.p, 0, sizeof(unsigned long long) * 64, ctx->stream));
-    prom::launch_transit(ctx->stream, tr, ctx->tables, ctx->mtables, ev, &variant);
+    // pipelined problems alternate slots and streams: this run's column / ordering kernels overlap the
+    // previous run's tau kernel; a slot is reused two runs later, after its stream's previous run
+    const int si = tr.pipelined ? (tr.last ^ 1) : 0;
+    const hipStream_t st = si ? ctx->stream1 : ctx->stream;
+    prom::RunSlot& rs = tr.slot[si];
+    if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
+    prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, (stats || ctx->timing) ? ev : nullptr, &variant);
+    tr.last = si;
     tr.count_evals = false;
 
     tr.ran = true;
@@ -470,10 +523,10 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
       stats->ms_total = t;
       const int K = prom::kCnt;
       std::vector<int32_t> cnt(tr.n_orb * K);
-      download(cnt.data(), tr.counts, (int64_t)cnt.size(), ctx->stream);
+      download(cnt.data(), rs.counts, (int64_t)cnt.size(), st);
       unsigned long long ev64[64];
-      download(ev64, tr.evals, 64, ctx->stream);
-      PROM_HIP(hipStreamSynchronize(ctx->stream));
+      download(ev64, rs.evals, 64, st);
+      PROM_HIP(hipStreamSynchronize(st));
       int64_t unwindowed = 0, counted = 0;
       for (int32_t o = 0; o < tr.n_orb; ++o) {
         const bool sorted = cnt[o * K + 5] != 0;
@@ -500,7 +553,8 @@ int32_t prom_transit_result(prom_ctx* ctx, double* R_out) {
     prom::TransitDev& tr = ctx->tr;
     if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_result: no completed run");
     PROM_REQUIRE(R_out, "prom_transit_result: null output");
-    download(R_out, tr.R, (int64_t)tr.n_orb * tr.n_wav, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream1));
+    download(R_out, tr.slot[tr.last].R, (int64_t)tr.n_orb * tr.n_wav, ctx->stream);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
   });
 }
@@ -510,7 +564,8 @@ int32_t prom_transit_columns(prom_ctx* ctx, double* N_out) {
     prom::TransitDev& tr = ctx->tr;
     if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_columns: no completed run");
     PROM_REQUIRE(N_out, "prom_transit_columns: null output");
-    download(N_out, tr.ncol, (int64_t)tr.n_atoms * tr.n_orb * tr.n_pr, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream1));
+    download(N_out, tr.slot[tr.last].ncol, (int64_t)tr.n_atoms * tr.n_orb * tr.n_pr, ctx->stream);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
   });
 }
@@ -528,6 +583,7 @@ int32_t prom_timing_end(prom_ctx* ctx, int32_t max_runs, double* ms, int32_t* n_
     ctx->timing = false;
     const int32_t n = std::min(ctx->timed_runs, std::max(max_runs, 0));
     PROM_HIP(hipStreamSynchronize(ctx->stream));
+    PROM_HIP(hipStreamSynchronize(ctx->stream1));
     for (int32_t r = 0; r < n; ++r) {
       hipEvent_t* e = &ctx->tev[4 * (size_t)r];
       float v[4];

@@ -100,6 +100,8 @@ struct SigTabDev {
   int32_t n_dir;
   int32_t pad;
   double dir_x0, dir_inv_h;
+  double ncoef;          // c_s: column normalisation of the windowed integration (n = c_s N <= 1)
+  double nscale;         // 1 / c_s (0 when c_s == 0)
 };
 
 // Per molecular slot of a transit problem.
@@ -118,6 +120,17 @@ struct MolSlotDev {
   const double* shift;   // [n_orb] Doppler factors of its scenario
   int32_t scenario;
   int32_t pad;
+};
+
+// Terms and scenarios of small problems passed by value to the column kernel.
+struct ColArgs {
+  TermDev t[8];
+  ScDevHost sc[4];
+};
+
+// Tables of up to kWinMaxSpecies atomic slots passed by value (kernel arguments: no dependent load).
+struct SigTabs4 {
+  SigTabDev t[4];
 };
 
 struct AtomTable {
@@ -140,6 +153,25 @@ struct MolTable {
   double vmax = 0.0;
 };
 
+// Work and output buffers of one run.  Two slots: consecutive runs alternate between them (and between
+// the context's two streams) so that a run's column / ordering kernels overlap the previous run's tau
+// kernel.
+struct RunSlot {
+  DevBuf ncol;                              // [n_atoms][n_orb][n_pr]
+  DevBuf flags;                             // [n_orb][n_pr] int32: 0 active, 1 transparent, 2 blocked
+  DevBuf recs;                              // [n_orb][n_pr][1 + n_atoms] chord-order records {F/Fsum, N_s}
+  DevBuf act_ip;                            // [n_orb][n_pr] int32 chord positions of the records
+  DevBuf counts;                            // [n_orb][kCnt] int32 (k_order / k_chords)
+  DevBuf tsum;                              // [n_orb] transparent flux sum / F_out sum
+  DevBuf fsum;                              // [n_orb] F_out sum
+  DevBuf mrecs;                             // sorted (+ merged) records [n_orb][n_pr][1 + n_atoms]
+  DevBuf wenv;                              // [n_orb][2][kEnvN] int32 threshold -> record tables
+  DevBuf wmom;                              // [n_orb][n_pr + 1][K] suffix tail moments
+  DevBuf evals;                             // [64] uint64 exp-evaluation counters (stats runs)
+  DevBuf sig;                               // no orbital Doppler shift: sigma_s(lambda_w) [n_atoms][n_wav]
+  DevBuf R;                                 // [n_orb][n_wav]
+};
+
 // Everything the transit kernels need, as device pointers.
 struct TransitDev {
   int64_t n_wav = 0;
@@ -160,41 +192,34 @@ struct TransitDev {
   DevBuf terms_dev;                         // [n_terms] TermDev
   DevBuf tab;                               // tabulated densities, raw host order, concatenated
   DevBuf ntot;                              // [n_sc][n_orb][n_pr][n_x]
-  DevBuf ncol;                              // [n_atoms][n_orb][n_pr]
   DevBuf molcol;                            // [n_mol][n_orb][n_pr] sum_x n_abs*dx (for the bound)
-  DevBuf flags;                             // [n_orb][n_pr] int32: 0 active, 1 transparent, 2 blocked
-  DevBuf recs;                              // [n_orb][n_pr][1 + n_atoms] {log2(F/Fsum)*2048, N_s}
-  DevBuf act_ip;                            // [n_orb][n_pr] int32 chord positions of active chords
-  DevBuf counts;                            // [n_orb][6] int32: active, transparent, blocked, nonfinite,
-                                            //   records, merged
-  DevBuf tsum;                              // [n_orb] transparent flux sum / F_out sum
-  DevBuf fsum;                              // [n_orb] F_out sum
   DevBuf sigma;                             // [n_atoms][n_orb][n_wav]
   DevBuf sigma_max_dev;                     // [n_atoms]
   DevBuf sigtab;                            // [n_atoms] SigTabDev
+  SigTabs4 sigtab_v{};                      // the first (up to) 4 slots, for kernel arguments
+  ColArgs colargs{};                        // terms / scenarios by value (n_terms <= 8, n_sc <= 4)
   int32_t exp_mode = 1;                     // 1: table-driven exp in k_tau, 0: ocml exp
   bool merge = true;                        // merge chords with equal (2^-40) column densities
-  DevBuf mrecs;                             // sorted (+ merged) records [n_orb][n_pr][1 + n_atoms]
   bool window = true;                       // windowed integration with tail moments
-  DevBuf nmax;                              // [n_orb][n_atoms] max column density over active chords
-  DevBuf wenv;                              // [n_orb][2][kEnvN] int32 threshold -> record tables
-  DevBuf wmom;                              // [n_orb][n_pr + 1][K] suffix tail moments
-  DevBuf evals;                             // [64] uint64 exp-evaluation counters (stats runs)
+  bool uniform_shift = false;               // every atomic species' Doppler factor equal at all phases
   bool count_evals = false;
-  DevBuf R;                                 // [n_orb][n_wav]
   DevBuf molslot;                           // [n_mol] MolSlotDev
   DevBuf mol_ip;                            // [n_mol][n_orb][n_pr][n_x] int32 P bracket (-1: out of table)
   DevBuf mol_wp;                            // [n_mol][n_orb][n_pr][n_x] P weight
   DevBuf mol_na;                            // [n_mol][n_orb][n_pr][n_x] n_abs = n chi
   std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
+  RunSlot slot[2];
+  bool pipelined = false;                   // fast path: runs alternate slots / streams
+  int last = 0;                             // slot of the most recent run
 };
 
 }  // namespace prom
 
 struct prom_ctx {
   int32_t device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // slot-0 stream (and the stream of every non-run call)
+  hipStream_t stream1 = nullptr; // slot-1 stream
   hipEvent_t ev[8] = {};
   std::string err;
   std::vector<prom::AtomTable> tables;
@@ -218,7 +243,8 @@ void launch_density(hipStream_t s, const DensityDev& m, const double* x, int32_t
                     const double* z, const double* bx, const double* by, int64_t n_chords, double* out);
 void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, int32_t n_x,
                             const double* P, double T, int64_t n_wav, const double* wav, double* out);
-void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>& tables,
+// ev (may be null): stage events {start, columns+ordering done, (same), tau done}
+void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
 

@@ -16,6 +16,8 @@
 //                 order, merging of chords with equal (2^-40) column densities
 //     k_tau<NS>   per (phase, wavelength): sigma_s = 10^interp(shift_o * lambda_w) - offset for each
 //                 species, then tau over the active chords, exp(-tau), disk sum, ratio
+#include <hip/hip_ext.h>
+
 #include "exp2_table.h"
 #include "faddeeva.h"
 #include "prom_internal.h"
@@ -82,8 +84,10 @@ __device__ __forceinline__ double np_interp(double t, const double* __restrict__
   return r;
 }
 
-// np_interp for one table of a transit problem, bracket from the bucket directory (same unique
-// bracket as numpy's search: the largest j <= n-2 with xp[j] <= t), then 10^v - offset.
+// np_interp for one table of a transit problem, then 10^v - offset.  The bracket (numpy's: the largest
+// j <= n-2 with xp[j] <= t) comes from the bucket directory: dir[j] - 1 is the last node at or before
+// the bucket's start, and a window of 4 nodes (x and f fetched together) holds the bracket unless the
+// bucket is crowded or rounding moved j, in which case a gallop + bisection finds it.
 __device__ __forceinline__ double sigma_of(double t, const SigTabDev& tb) {
   const double* __restrict__ xp = tb.x;
   const double* __restrict__ fp = tb.y;
@@ -93,26 +97,38 @@ __device__ __forceinline__ double sigma_of(double t, const SigTabDev& tb) {
   else if (n == 1 || !(t >= xp[0])) v = fp[0];
   else if (t >= xp[n - 1]) v = fp[n - 1];
   else {
-    double fj = (t - tb.dir_x0) * tb.dir_inv_h;
-    int32_t j = fj < 0.0 ? 0 : (fj >= (double)(tb.n_dir - 1) ? tb.n_dir - 1 : (int32_t)fj);
-    int64_t lo = tb.dir[j] - 1, hi = tb.dir[j + 1];
+    const double fj = (t - tb.dir_x0) * tb.dir_inv_h;
+    const int32_t j = fj < 0.0 ? 0 : (fj >= (double)(tb.n_dir - 1) ? tb.n_dir - 1 : (int32_t)fj);
+    int64_t lo = tb.dir[j] - 1;
     lo = lo < 0 ? 0 : (lo > n - 2 ? n - 2 : lo);
-    hi = hi > n - 1 ? n - 1 : hi;
-    hi = hi <= lo ? lo + 1 : hi;
-    // verify the bracket xp[lo] <= t < xp[hi]; widen by galloping if rounding moved j
-    for (int64_t step = 1; lo > 0 && xp[lo] > t; step <<= 1) { hi = lo; lo = lo - step > 0 ? lo - step : 0; }
-    for (int64_t step = 1; hi < n - 1 && xp[hi] <= t; step <<= 1) { lo = hi; hi = hi + step < n - 1 ? hi + step : n - 1; }
-    while (hi - lo > 1) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (xp[mid] <= t) lo = mid; else hi = mid;
+    const int64_t l1 = lo + 1, l2 = lo + 2 < n ? lo + 2 : n - 1, l3 = lo + 3 < n ? lo + 3 : n - 1;
+    const double x0 = xp[lo], x1 = xp[l1], x2 = xp[l2], x3 = xp[l3];
+    const double f0 = fp[lo], f1 = fp[l1], f2 = fp[l2], f3 = fp[l3];
+    double xa, xb, fa, fb;
+    int64_t k = -1;
+    if (x0 <= t) {
+      if (t < x1) { k = lo; xa = x0; xb = x1; fa = f0; fb = f1; }
+      else if (t < x2) { k = l1; xa = x1; xb = x2; fa = f1; fb = f2; }
+      else if (t < x3) { k = l2; xa = x2; xb = x3; fa = f2; fb = f3; }
     }
-    if (xp[lo] == t) v = fp[lo];
+    if (k < 0) {
+      int64_t a = lo, b = l3;   // invariant after the gallop: xp[a] <= t < xp[b]
+      for (int64_t st = 1; a > 0 && xp[a] > t; st <<= 1) { b = a; a = a - st > 0 ? a - st : 0; }
+      for (int64_t st = 1; b < n - 1 && xp[b] <= t; st <<= 1) { a = b; b = b + st < n - 1 ? b + st : n - 1; }
+      while (b - a > 1) {
+        const int64_t mid = (a + b) >> 1;
+        if (xp[mid] <= t) a = mid; else b = mid;
+      }
+      k = a;
+      xa = xp[a]; xb = xp[a + 1]; fa = fp[a]; fb = fp[a + 1];
+    }
+    if (xa == t) v = fa;
     else {
-      const double slope = (fp[lo + 1] - fp[lo]) / (xp[lo + 1] - xp[lo]);
-      v = slope * (t - xp[lo]) + fp[lo];
+      const double slope = (fb - fa) / (xb - xa);
+      v = slope * (t - xa) + fa;
       if (v != v) {
-        v = slope * (t - xp[lo + 1]) + fp[lo + 1];
-        if (v != v && fp[lo] == fp[lo + 1]) v = fp[lo];
+        v = slope * (t - xb) + fb;
+        if (v != v && fa == fb) v = fa;
       }
     }
   }
@@ -468,27 +484,43 @@ using ScDev = ScDevHost;
 // lanes 0..7 form numpy's eight pairwise partial sums, lane 0 combines them (loops_utils.h.src order)
 // -> N = (0.0 + pairwise_x(n chi)) * delta_x exactly as gasProperties.py:940.  The k_ntot + k_columns
 // pair handles molecular terms and n_x > 64.
-template <int L>
-__global__ void __launch_bounds__(kBlock) k_columns_lanes(const TermDev* __restrict__ terms, int32_t n_terms,
-                                 const ScDev* __restrict__ scs, const double* __restrict__ x, int32_t n_x,
+template <int L, int NSIG>
+__global__ void __launch_bounds__(kBlock) k_columns_lanes(const ColArgs ca, int32_t n_terms,
+                                 const double* __restrict__ x, int32_t n_x,
                                  int32_t n_pr, int32_t n_orb, double delta_x, const double* __restrict__ cy,
                                  const double* __restrict__ cz, const double* __restrict__ bx,
                                  const double* __restrict__ by, const double* __restrict__ planet_y,
                                  double planet_R, int32_t n_moons, const double* __restrict__ moon_y,
                                  const double* __restrict__ moon_R, const double* __restrict__ sig_max,
-                                 double cull, double* __restrict__ ncol, int32_t* __restrict__ flags) {
+                                 double cull, double* __restrict__ ncol, int32_t* __restrict__ flags,
+                                 const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
+                                 double* __restrict__ sig) {
   // a chord's L lanes sit inside one wavefront: the pairwise partial sums move by cross-lane
   // shuffles, no LDS and no workgroup barrier
   PROM_CLK(tk0);
   constexpr int G = kBlock / L;         // chords per workgroup
+  if constexpr (NSIG > 0) {
+    // trailing workgroups: sigma_s(shift_s lambda_w) for problems without orbital Doppler shift
+    const unsigned cb = (unsigned)(((int64_t)n_orb * n_pr + G - 1) / G);
+    if (blockIdx.x >= cb) {
+      const int64_t w = (int64_t)(blockIdx.x - cb) * kBlock + threadIdx.x;
+      if (w < n_wav) {
+        const double lam = wav[w];
+#pragma unroll
+        for (int s = 0; s < NSIG; ++s)
+          sig[(int64_t)s * n_wav + w] = sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
+      }
+      return;
+    }
+  }
   const int lane = threadIdx.x & 63;
   const int gl = lane & (L - 1);        // lane within the chord's group
   const int gbase = lane & ~(L - 1);    // the group's first lane in the wavefront
-  const int64_t nc = (int64_t)n_orb * n_pr;
-  const int64_t c = (int64_t)blockIdx.x * G + threadIdx.x / L;
+  const int32_t nc = n_orb * n_pr;
+  const int32_t c = (int32_t)blockIdx.x * G + (int32_t)threadIdx.x / L;
   const bool valid = c < nc;
-  const int32_t ip = valid ? (int32_t)(c % n_pr) : 0;
-  const int32_t o = valid ? (int32_t)(c / n_pr) : 0;
+  const int32_t o = valid ? c / n_pr : 0;
+  const int32_t ip = valid ? c - o * n_pr : 0;
   const double y = cy[ip], z = cz[ip];
   const double dyp = y - planet_y[o];
   bool blocked = sqrt(dyp * dyp + z * z) < planet_R;
@@ -500,11 +532,13 @@ __global__ void __launch_bounds__(kBlock) k_columns_lanes(const TermDev* __restr
   const int32_t lim = n_x - (n_x % 8);
   double bound = 0.0, nv = 0.0;
   int32_t cur_sc = -1;
-  for (int32_t t = 0; t < n_terms; ++t) {
-    const TermDev td = terms[t];
+#pragma unroll
+  for (int32_t t = 0; t < 8; ++t) {
+    if (t >= n_terms) break;
+    const TermDev td = ca.t[t];
     if (td.scenario != cur_sc) {   // one density evaluation per scenario, shared by its constituents
       cur_sc = td.scenario;
-      const ScDev sc = scs[cur_sc];
+      const ScDev sc = ca.sc[cur_sc & 3];
       nv = 0.0;
       if (live)
         nv = sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + gl]
@@ -749,9 +783,11 @@ __global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restric
 }
 
 // ---- windowed integration: per-phase record order, envelopes, threshold tables, tail moments ----
-// For one phase and one wavelength, tau_i = sum_s N_si sigma_s.  With n_si = N_si / Nmax_s (Nmax_s:
-// max over the phase's active chords) and q_s = sigma_s Nmax_s, every record i satisfies
-//     a_i Q <= tau_i <= b_i Q,   a_i = min_s n_si,  b_i = max_s n_si,  Q = sum_s q_s.
+// For one phase and one wavelength, tau_i = sum_s N_si sigma_s.  With n_si = c_s N_si (c_s = 1 /
+// (chi_s n_ref L): n_ref bounds the scenario's density, L = n_x dx, so n <= 1; SigTabDev::ncoef) and
+// q_s = sigma_s / c_s, every record i satisfies
+//     a_i Q <= tau_i <= b_i Q,   a_i = min_s n_si,  b_i = max_s n_si,  Q = sum_s q_s
+// (sigma_s >= 0 up to the 1e-50 table offset's rounding, which the bounds absorb).
 // Records are ordered by b descending (ties: chord index), equal-column chords merged, and two
 // envelopes kept: B_i = max_{j >= i} b_j and A_i = min_{j <= i} a_j (both non-increasing in i).
 // For a wavefront whose wavelengths have Q in [Q_lo, Q_hi]:
@@ -767,7 +803,7 @@ __global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restric
 constexpr int kWBlock = 512;
 constexpr int kWPer = kWinMax / kWBlock;           // sorted positions per thread
 constexpr int kEnvVmax = 8184;                     // bits(1.0) >> 49
-constexpr int kEnvVmin = kEnvVmax - kEnvN + 1;     // X_vmin = 2^-256
+constexpr int kEnvVmin = kEnvVmax - kEnvN + 1;     // X_vmin = 2^-(kEnvN / 8)
 constexpr double kTailEps = 0x1p-10;
 constexpr double kTauSat = 40.0;
 
@@ -855,6 +891,65 @@ __device__ __forceinline__ T wg_excl_suffix(T v, Op op, T id, T* wsum) {
   return op(carry, exc);
 }
 
+// ---- wavefront scans on DPP row shifts + cross-row readlanes (no LDS traffic, no bpermute) ----
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int32_t dpp_mov(int32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double lane_read(double v, int l) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ int32_t lane_read(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// inclusive prefix over lanes 0..63 (op applied as op(earlier, later))
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_prefix(T v, Op op) {
+  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
+  T t = dpp_mov<0x111>(v);
+  if (rl >= 1) v = op(t, v);
+  t = dpp_mov<0x112>(v);
+  if (rl >= 2) v = op(t, v);
+  t = dpp_mov<0x114>(v);
+  if (rl >= 4) v = op(t, v);
+  t = dpp_mov<0x118>(v);
+  if (rl >= 8) v = op(t, v);
+  const T r0 = lane_read(v, 15), r1 = lane_read(v, 31), r2 = lane_read(v, 47);
+  const T c01 = op(r0, r1), c012 = op(c01, r2);
+  if (row == 1) v = op(r0, v);
+  else if (row == 2) v = op(c01, v);
+  else if (row == 3) v = op(c012, v);
+  return v;
+}
+// inclusive suffix over lanes 63..0 (op applied as op(earlier, later))
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_suffix(T v, Op op) {
+  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
+  T t = dpp_mov<0x101>(v);
+  if (rl <= 14) v = op(v, t);
+  t = dpp_mov<0x102>(v);
+  if (rl <= 13) v = op(v, t);
+  t = dpp_mov<0x104>(v);
+  if (rl <= 11) v = op(v, t);
+  t = dpp_mov<0x108>(v);
+  if (rl <= 7) v = op(v, t);
+  const T r1 = lane_read(v, 16), r2 = lane_read(v, 32), r3 = lane_read(v, 48);
+  const T c23 = op(r2, r3), c123 = op(r1, c23);
+  if (row == 2) v = op(v, r3);
+  else if (row == 1) v = op(v, c23);
+  else if (row == 0) v = op(v, c123);
+  return v;
+}
+
 // #{i in [0, n) : v[i] >= x} for a non-increasing v
 __device__ __forceinline__ int32_t count_ge(const double* v, int32_t n, double x) {
   int32_t lo = 0, hi = n;
@@ -865,200 +960,219 @@ __device__ __forceinline__ int32_t count_ge(const double* v, int32_t n, double x
   return lo;
 }
 
-// One workgroup per phase, designed around few dependent memory round trips:
-//  1. each thread loads kCPT consecutive chords (flags, F_out, N_s) per sweep, all loads issued
-//     before use; F_out and transparent sums, counts and Nmax_s are reduced over the workgroup;
-//  2. either the chord-order compaction of k_chords (phases with non-finite columns -> exact path;
-//     more than kWinMax active chords; neither merging nor windows requested), or
-//  3. the sorted path: keys (b descending, chord index) bitonic-sorted in LDS; each thread then owns
-//     kWPer consecutive sorted positions, fetches their columns (one round trip), marks group heads
-//     (equal 2^-40 keys of every species when merge != 0) and keeps its groups -- a contiguous range
-//     of record indices -- in registers: summed weights, envelopes, suffix tail moments and the
-//     sorted records are produced from there; threshold tables are searched in LDS.
+// One workgroup per phase, few dependent steps (2 global round trips, ~8 workgroup barriers for
+// phases with <= 1024 active chords):
+//  1. every thread loads its strided chords (flags, F_out, N_s) -- one round trip per 4096 chords --
+//     classifies them, writes the sort key (b descending, chord index) of each active chord at its
+//     thread-major compaction position; one combined workgroup scan/reduction gives positions,
+//     counts, the F_out sum and the transparent sum;
+//  2. phases with non-finite columns (exact path) or more than kWinMax active chords, or with neither
+//     merging nor windows requested: chord-order-free compaction into recs/act_ip instead;
+//  3. keys sorted in LDS: rank sort (<= 1024 keys: each key's rank = number of smaller keys, counted
+//     against LDS broadcasts) or bitonic;
+//  4. each thread fetches the columns of its ceil(n / kWBlock) consecutive sorted positions (one trip),
+//     forms b, a, F and group heads (equal 2^-40 keys of every species when merge != 0);
+//  5. one combined workgroup scan: group ids (prefix sum of heads), A (prefix min of a), B (suffix max
+//     of b) and the K suffix moments;
+//  6. each group head writes its record (summed weight, head's columns), moments and envelopes;
+//     threshold tables are searched in LDS.
 // counts[o * kCnt] = {active, transparent, blocked, nonfinite, records, sorted, windowed, 0}.
-constexpr int kCPT = kWinMax / kWBlock;            // chords per thread and sweep
+constexpr int kLD = kWinMax / kWBlock;              // strided chords per thread and sweep
+constexpr int kRankMax = 2 * kWBlock;               // rank sort up to this many keys
 
 template <int NS>
-__global__ void __launch_bounds__(kWBlock) k_chords_w(const int32_t* __restrict__ flags,
-                                                      const double* __restrict__ fout,
-                                                      const double* __restrict__ ncol, int32_t n_pr,
-                                                      int32_t n_orb, int32_t merge, int32_t window,
-                                                      double* __restrict__ recs,
-                                                      int32_t* __restrict__ act_ip,
-                                                      double* __restrict__ mrecs,
-                                                      int32_t* __restrict__ counts,
-                                                      double* __restrict__ tfrac,
-                                                      double* __restrict__ fsum,
-                                                      double* __restrict__ nmax_out,
-                                                      int32_t* __restrict__ wenv,
-                                                      double* __restrict__ wmom) {
+__global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ flags,
+                                                   const double* __restrict__ fout,
+                                                   const double* __restrict__ ncol, int32_t n_pr,
+                                                   int32_t n_orb, int32_t merge, int32_t window,
+                                                   const SigTabs4 tabv,
+                                                   double* __restrict__ recs,
+                                                   int32_t* __restrict__ act_ip,
+                                                   double* __restrict__ mrecs,
+                                                   int32_t* __restrict__ counts,
+                                                   double* __restrict__ tfrac,
+                                                   double* __restrict__ fsum,
+                                                   int32_t* __restrict__ wenv,
+                                                   double* __restrict__ wmom) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
   constexpr int ST = 1 + NS;
-  __shared__ unsigned long long skey[kWinMax];   // sort keys; later the B envelope (as double)
-  __shared__ double sF[kWinMax];                 // member weights; later the A envelope
-  __shared__ int32_t sgid[kWinMax];
-  __shared__ double rd[NW][2 + NS];
-  __shared__ int32_t ri[NW][4];
-  __shared__ int32_t wi[NW];
-  __shared__ double wd[NW];
-  __shared__ double rk[NW][K];
+  __shared__ unsigned long long skey[kWinMax];   // sort keys; after step 4 the B envelope (doubles)
+  __shared__ double sF[kWinMax];                 // weights of the sorted chords
+  __shared__ double sA[kWinMax];                 // A envelope per record
+  __shared__ unsigned char sHead[kWinMax];
+  __shared__ int32_t pi_[NW][5];
+  __shared__ double pd_[NW][2];
+  __shared__ double pm_[NW][K + 2];
+  __shared__ int32_t pg_[NW];
   const int32_t o = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int32_t* fl = flags + (int64_t)o * n_pr;
   const int64_t nstride = (int64_t)n_orb * n_pr;
   const double* nc0 = ncol + (int64_t)o * n_pr;
+  double cs[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) cs[s] = tabv.t[s].ncoef;
 
   PROM_TS(o * 16 + 0);
-  // ---- 1. sums, counts, Nmax
-  double fpart = 0.0, tpart = 0.0;
-  double nm[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) nm[s] = 0.0;
-  int32_t ntr = 0, nbl = 0, nact = 0, nnf = 0;
+  // ---- 1. load, classify, keys, combined scan/reduction
+  double fs = 0.0, ts = 0.0;
+  int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0;
   for (int32_t sw = 0; sw < n_pr; sw += kWinMax) {
-    const int32_t c0 = sw + tid * kCPT;
-    int32_t f[kCPT];
-    double fo[kCPT], nv[kCPT][NS];
+    int32_t f[kLD];
+    double fo[kLD], nv[kLD][NS];
 #pragma unroll
-    for (int k = 0; k < kCPT; ++k) {
-      const int32_t ip = c0 + k;
+    for (int k = 0; k < kLD; ++k) {
+      const int32_t ip = sw + tid + k * kWBlock;
       const bool in = ip < n_pr;
       f[k] = in ? fl[ip] : 3;
       fo[k] = in ? fout[ip] : 0.0;
 #pragma unroll
       for (int s = 0; s < NS; ++s) nv[k][s] = in ? nc0[s * nstride + ip] : 0.0;
     }
+    double fp = 0.0, tp = 0.0;
+    int32_t c[5] = {0, 0, 0, 0, 0};   // active, transparent, blocked, nonfinite
 #pragma unroll
-    for (int k = 0; k < kCPT; ++k) {
+    for (int k = 0; k < kLD; ++k) {
       if (f[k] == 3) continue;
-      fpart += fo[k];
-      if (f[k] == 1) { tpart += fo[k]; ++ntr; }
-      else if (f[k] == 2) ++nbl;
+      fp += fo[k];
+      if (f[k] == 1) { tp += fo[k]; ++c[1]; }
+      else if (f[k] == 2) ++c[2];
       else {
-        ++nact;
-        bool fin = true;
+        ++c[0];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          if (!__builtin_isfinite(nv[k][s])) fin = false;
-          else nm[s] = nv[k][s] > nm[s] ? nv[k][s] : nm[s];
-        }
-        if (!fin) ++nnf;
+        for (int s = 0; s < NS; ++s)
+          if (!__builtin_isfinite(nv[k][s])) { ++c[3]; break; }
       }
     }
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    fpart += __shfl_down(fpart, off, 64);
-    tpart += __shfl_down(tpart, off, 64);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const double u = __shfl_down(nm[s], off, 64);
-      nm[s] = u > nm[s] ? u : nm[s];
+    // combined: prefix of the active count, wavefront totals of everything (DPP scans)
+    const int32_t inc = wave_prefix<int32_t>(c[0], OpAdd());
+    const double fpw = lane_read(wave_prefix<double>(fp, OpAdd()), 63);
+    const double tpw = lane_read(wave_prefix<double>(tp, OpAdd()), 63);
+    const int32_t c1w = lane_read(wave_prefix<int32_t>(c[1], OpAdd()), 63);
+    const int32_t c2w = lane_read(wave_prefix<int32_t>(c[2], OpAdd()), 63);
+    const int32_t c3w = lane_read(wave_prefix<int32_t>(c[3], OpAdd()), 63);
+    __syncthreads();
+    if (lane == 63) pi_[wid][0] = inc;
+    if (lane == 0) {
+      pi_[wid][1] = c1w; pi_[wid][2] = c2w; pi_[wid][3] = c3w;
+      pd_[wid][0] = fpw; pd_[wid][1] = tpw;
     }
-    ntr += __shfl_down(ntr, off, 64);
-    nbl += __shfl_down(nbl, off, 64);
-    nact += __shfl_down(nact, off, 64);
-    nnf += __shfl_down(nnf, off, 64);
+    __syncthreads();
+    int32_t pos = nact + inc - c[0];
+    for (int w = 0; w < NW; ++w) {
+      if (w < wid) pos += pi_[w][0];
+      nact += pi_[w][0]; ntr += pi_[w][1]; nbl += pi_[w][2]; nnf += pi_[w][3];
+      fs += pd_[w][0]; ts += pd_[w][1];
+    }
+#pragma unroll
+    for (int k = 0; k < kLD; ++k) {
+      if (f[k] != 0) continue;
+      if (pos < kWinMax) {
+        double b = 0.0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const double v = nv[k][s] * cs[s];
+          b = v > b ? v : b;
+        }
+        b = b < 1.0 ? b : 1.0;   // NaN -> 1.0 (such phases take the unsorted path anyway)
+        const unsigned long long d =
+            (__builtin_bit_cast(unsigned long long, 1.0) - __builtin_bit_cast(unsigned long long, b)) >> 22;
+        skey[pos] = (d << 24) | (unsigned long long)(sw + tid + k * kWBlock);
+      }
+      ++pos;
+    }
   }
-  if (lane == 0) {
-    rd[wid][0] = fpart;
-    rd[wid][1] = tpart;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) rd[wid][2 + s] = nm[s];
-    ri[wid][0] = ntr; ri[wid][1] = nbl; ri[wid][2] = nact; ri[wid][3] = nnf;
-  }
-  __syncthreads();
-  double fs = 0.0, ts = 0.0;
-  ntr = nbl = nact = nnf = 0;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) nm[s] = 0.0;
-  for (int w = 0; w < NW; ++w) {
-    fs += rd[w][0];
-    ts += rd[w][1];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) nm[s] = rd[w][2 + s] > nm[s] ? rd[w][2 + s] : nm[s];
-    ntr += ri[w][0]; nbl += ri[w][1]; nact += ri[w][2]; nnf += ri[w][3];
-  }
-  double inv[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) inv[s] = nm[s] > 0.0 ? 1.0 / nm[s] : 0.0;
-
+  __syncthreads();   // keys visible to the sort
   PROM_TS(o * 16 + 1);
   const bool sorted = nnf == 0 && nact <= kWinMax && (merge || window);
   int32_t G = nact;
-  // ---- 2. compaction in chord order (records or sort keys)
-  {
+  if (!sorted) {
+    // ---- 2. compaction into recs / act_ip (thread-major order, deterministic)
     int32_t base = 0;
     for (int32_t sw = 0; sw < n_pr; sw += kWinMax) {
-      const int32_t c0 = sw + tid * kCPT;
-      int32_t f[kCPT];
+      int32_t f[kLD];
       int32_t mine = 0;
 #pragma unroll
-      for (int k = 0; k < kCPT; ++k) {
-        const int32_t ip = c0 + k;
+      for (int k = 0; k < kLD; ++k) {
+        const int32_t ip = sw + tid + k * kWBlock;
         f[k] = ip < n_pr ? fl[ip] : 3;
         mine += f[k] == 0 ? 1 : 0;
       }
       int32_t tot;
-      int32_t pos = base + wg_excl_prefix<int32_t>(mine, OpAdd(), 0, wi, &tot);
+      int32_t pos = base + wg_excl_prefix<int32_t>(mine, OpAdd(), 0, pg_, &tot);
 #pragma unroll
-      for (int k = 0; k < kCPT; ++k) {
+      for (int k = 0; k < kLD; ++k) {
         if (f[k] != 0) continue;
-        const int32_t ip = c0 + k;
-        if (sorted) {
-          double b = 0.0;
+        const int32_t ip = sw + tid + k * kWBlock;
+        act_ip[(int64_t)o * n_pr + pos] = ip;
+        double* r = recs + ((int64_t)o * n_pr + pos) * ST;
+        r[0] = fout[ip] / fs;
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const double v = nc0[s * nstride + ip] * inv[s];
-            b = v > b ? v : b;
-          }
-          b = b < 1.0 ? b : 1.0;
-          const unsigned long long d =
-              (__builtin_bit_cast(unsigned long long, 1.0) - __builtin_bit_cast(unsigned long long, b)) >> 22;
-          skey[pos] = (d << 24) | (unsigned long long)ip;
-        } else {
-          act_ip[(int64_t)o * n_pr + pos] = ip;
-          double* r = recs + ((int64_t)o * n_pr + pos) * ST;
-          r[0] = fout[ip] / fs;
-#pragma unroll
-          for (int s = 0; s < NS; ++s) r[1 + s] = nc0[s * nstride + ip];
-        }
+        for (int s = 0; s < NS; ++s) r[1 + s] = nc0[s * nstride + ip];
         ++pos;
       }
       base += tot;
     }
-  }
-  PROM_TS(o * 16 + 2);
-  if (sorted) {
-    // ---- 3a. bitonic sort of the keys
+  } else {
     const int32_t n = nact;
-    int32_t P = 1;
-    while (P < n) P <<= 1;
-    for (int32_t i = n + tid; i < P; i += kWBlock) skey[i] = ~0ull;
-    __syncthreads();
-    for (int32_t size = 2; size <= P; size <<= 1) {
-      for (int32_t st = size >> 1; st > 0; st >>= 1) {
-        for (int32_t t = tid; t < P / 2; t += kWBlock) {
-          const int32_t i = 2 * t - (t & (st - 1));
-          const int32_t j = i + st;
-          const bool up = (i & size) == 0;
-          const unsigned long long a = skey[i], b = skey[j];
-          if ((a > b) == up) { skey[i] = b; skey[j] = a; }
+    // ---- 3. sort
+    if (n <= kRankMax) {
+      // rank = number of smaller keys (keys are unique: they carry the chord index); only the
+      // wavefronts holding keys count, against LDS broadcasts
+      const int32_t i0 = tid, i1 = tid + kWBlock;
+      const bool has0 = i0 < n, has1 = i1 < n;
+      const unsigned long long k0 = has0 ? skey[i0] : ~0ull;
+      const unsigned long long k1 = has1 ? skey[i1] : ~0ull;
+      int32_t r0 = 0, r1 = 0;
+      if (n > kWBlock) {
+        for (int32_t j = 0; j < n; ++j) {
+          const unsigned long long a0 = skey[j];
+          r0 += a0 < k0;
+          r1 += a0 < k1;
         }
-        __syncthreads();
+      } else if (__builtin_amdgcn_readfirstlane(tid) < n) {
+        int32_t j = 0;
+        for (; j + 4 <= n; j += 4) {
+          const unsigned long long a0 = skey[j], a1 = skey[j + 1], a2 = skey[j + 2], a3 = skey[j + 3];
+          r0 += (a0 < k0) + (a1 < k0) + (a2 < k0) + (a3 < k0);
+        }
+        for (; j < n; ++j) r0 += skey[j] < k0;
+      }
+      __syncthreads();
+      if (has0) skey[r0] = k0;
+      if (has1) skey[r1] = k1;
+      __syncthreads();
+    } else {
+      int32_t P = 1;
+      while (P < n) P <<= 1;
+      for (int32_t i = n + tid; i < P; i += kWBlock) skey[i] = ~0ull;
+      __syncthreads();
+      for (int32_t size = 2; size <= P; size <<= 1) {
+        for (int32_t st = size >> 1; st > 0; st >>= 1) {
+          for (int32_t t = tid; t < P / 2; t += kWBlock) {
+            const int32_t i = 2 * t - (t & (st - 1));
+            const int32_t jj = i + st;
+            const bool up = (i & size) == 0;
+            const unsigned long long a = skey[i], b = skey[jj];
+            if ((a > b) == up) { skey[i] = b; skey[jj] = a; }
+          }
+          __syncthreads();
+        }
       }
     }
-    PROM_TS(o * 16 + 3);
-    // ---- 3b. this thread's sorted positions [i0, i0 + cnt): columns, group heads
-    const int32_t i0 = min(n, tid * kWPer);
-    const int32_t cnt = min(n, i0 + kWPer) - i0;
-    double Nv[kWPer][NS], Fv[kWPer];
-    unsigned long long pk[NS];
+    PROM_TS(o * 16 + 2);
+    // ---- 4. this thread's sorted positions [i0, i0 + cnt)
+    const int32_t per = (n + kWBlock - 1) / kWBlock;   // <= kWPer
+    const int32_t i0 = min(n, tid * per);
+    const int32_t cnt = min(n, i0 + per) - i0;
+    double Nv[kWPer][NS], Fv[kWPer], bv[kWPer], av[kWPer];
+    double Np[NS];
     {
       const int32_t ipp = i0 > 0 ? (int32_t)(skey[i0 - 1] & 0xffffffull) : 0;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) pk[s] = (i0 > 0 && cnt > 0) ? mkey(nc0[s * nstride + ipp]) : 0ull;
+      for (int s = 0; s < NS; ++s) Np[s] = (i0 > 0 && cnt > 0) ? nc0[s * nstride + ipp] : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < kWPer; ++k) {
@@ -1069,141 +1183,126 @@ __global__ void __launch_bounds__(kWBlock) k_chords_w(const int32_t* __restrict_
     }
     uint32_t headbits = 0;
     int32_t nheads = 0;
+    double bmax = 0.0, amin = 1.0e308;
+    double msum[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) msum[k] = 0.0;
 #pragma unroll
     for (int k = 0; k < kWPer; ++k) {
-      if (k >= cnt) break;
+      bv[k] = 0.0; av[k] = 1.0e308;
+      if (k >= cnt) continue;
       bool head = !merge || (i0 + k) == 0;
+      double pw[NS][4];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const unsigned long long kk = mkey(Nv[k][s]);
-        if ((i0 + k) > 0 && kk != pk[s]) head = true;
-        pk[s] = kk;
+        const double prev = k == 0 ? Np[s] : Nv[k > 0 ? k - 1 : 0][s];
+        if ((i0 + k) > 0 && mkey(Nv[k][s]) != mkey(prev)) head = true;
+        const double v = Nv[k][s] * cs[s];
+        bv[k] = v > bv[k] ? v : bv[k];
+        av[k] = v < av[k] ? v : av[k];
+        pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
       }
       Fv[k] = Fv[k] / fs;
       sF[i0 + k] = Fv[k];
+      sHead[i0 + k] = head ? 1 : 0;
       if (head) { headbits |= 1u << k; ++nheads; }
-    }
-    int32_t gtot;
-    const int32_t gb = wg_excl_prefix<int32_t>(nheads, OpAdd(), 0, wi, &gtot);
-    {
-      int32_t g = gb - 1;
-      for (int k = 0; k < cnt; ++k) {
-        if ((headbits >> k) & 1u) ++g;
-        sgid[i0 + k] = g;
+      bmax = bv[k] > bmax ? bv[k] : bmax;
+      amin = av[k] < amin ? av[k] : amin;
+      if (window) {
+#pragma unroll
+        for (int m = 0; m < K; ++m) msum[m] += Fv[k] * mono_eval<NS>(M, m, pw);
       }
+    }
+    // ---- 5. combined workgroup scan (DPP): group ids (prefix sum of heads), A (prefix min of a),
+    //         suffix moments; the B envelope needs no scan: records are sorted by 2^-30 buckets of
+    //         b, so every later record has b_j <= b_i (1 + 2^-29) (b >= 1 only ahead of b < 1)
+    const int32_t hinc = wave_prefix<int32_t>(nheads, OpAdd());
+    const double ainc = wave_prefix<double>(amin, OpMin());
+    double aexc = dpp_mov<0x138>(ainc);   // wave_shr:1
+    if (lane == 0) aexc = 1.0e308;
+    const double bw = lane_read(wave_prefix<double>(bmax, OpMax()), 63);
+    if (window) {
+#pragma unroll
+      for (int m = 0; m < K; ++m) {
+        const double inc = wave_suffix<double>(msum[m], OpAdd());
+        if (lane == 0) pm_[wid][m] = inc;
+        const double exc = dpp_mov<0x130>(inc);   // wave_shl:1: suffix of the later lanes
+        msum[m] = lane == 63 ? 0.0 : exc;
+      }
+    }
+    if (lane == 63) { pg_[wid] = hinc; pm_[wid][K] = ainc; }
+    if (lane == 0) pm_[wid][K + 1] = bw;
+    __syncthreads();
+    int32_t gb = hinc - nheads, gtot = 0;
+    double ball = 0.0;
+    for (int w = 0; w < NW; ++w) {
+      if (w < wid) {
+        gb += pg_[w];
+        aexc = pm_[w][K] < aexc ? pm_[w][K] : aexc;
+      }
+      if (w > wid && window) {
+#pragma unroll
+        for (int m = 0; m < K; ++m) msum[m] += pm_[w][m];
+      }
+      ball = pm_[w][K + 1] > ball ? pm_[w][K + 1] : ball;
+      gtot += pg_[w];
     }
     G = gtot;
-    __syncthreads();
-    PROM_TS(o * 16 + 4);
-    // ---- 3c. this thread's groups gb .. gb + nheads - 1: summed weight, head's columns, b, a
+    PROM_TS(o * 16 + 3);
+    // ---- 6. records, envelopes, moments (group heads), in the sorted order
     double* mo = mrecs + (int64_t)o * n_pr * ST;
-    double gF[kWPer], bb[kWPer], aa[kWPer];
-    double bmax = 0.0, amin = 1.0e308;
+    double* sB = reinterpret_cast<double*>(skey);   // all key reads are before the barrier above
+    double* mm = wmom + (int64_t)o * (n_pr + 1) * K;
     {
-      int h = 0;
+      // forward: group ids and A
+      int32_t g = gb - 1;
+      double arun = aexc;
+      int32_t gk[kWPer];
+      double ak[kWPer];
 #pragma unroll
       for (int k = 0; k < kWPer; ++k) {
-        gF[k] = 0.0; bb[k] = 0.0; aa[k] = 0.0;
+        gk[k] = -1;
+        ak[k] = 0.0;
+        if (k >= cnt) continue;
+        arun = av[k] < arun ? av[k] : arun;
+        if ((headbits >> k) & 1u) { ++g; gk[k] = g; ak[k] = arun; }
       }
+      // backward: moments
 #pragma unroll
-      for (int k = 0; k < kWPer; ++k) {
-        if (!((headbits >> k) & 1u)) continue;
-        const int32_t i = i0 + k, gi = gb + h;
+      for (int k = kWPer - 1; k >= 0; --k) {
+        if (k >= cnt) continue;
+        if (window) {
+          double pw[NS][4];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const double v = Nv[k][s] * cs[s];
+            pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
+          }
+#pragma unroll
+          for (int m = 0; m < K; ++m) msum[m] += Fv[k] * mono_eval<NS>(M, m, pw);
+        }
+        if (gk[k] < 0) continue;
+        const int32_t gi = gk[k];
+        const int32_t i = i0 + k;
         double F = Fv[k];
-        for (int32_t j = i + 1; j < n && sgid[j] == gi; ++j) F += sF[j];
+        for (int32_t j = i + 1; j < n && !sHead[j]; ++j) F += sF[j];
         double* r = mo + (int64_t)gi * ST;
         r[0] = F;
-        double b = 0.0, a = 1.0e308;
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          r[1 + s] = Nv[k][s];
-          const double v = Nv[k][s] * inv[s];
-          b = v > b ? v : b;
-          a = v < a ? v : a;
+        for (int s = 0; s < NS; ++s) r[1 + s] = Nv[k][s];
+        if (window) {
+          // later members' a are within 2^-40 of the head's: A is widened by 2^-38 to cover them
+          sB[gi] = bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28);
+          sA[gi] = ak[k] * (1.0 - 0x1p-38);
+#pragma unroll
+          for (int m = 0; m < K; ++m) mm[(int64_t)gi * K + m] = M.c[m] * msum[m];
         }
-        // compact the thread's groups to slots 0 .. nheads-1 (k >= h always)
-#pragma unroll
-        for (int m = 0; m < kWPer; ++m)
-          if (m == h) {
-            gF[m] = F; bb[m] = b; aa[m] = a;
-#pragma unroll
-            for (int s = 0; s < NS; ++s) Nv[m][s] = Nv[k][s];
-          }
-        bmax = b > bmax ? b : bmax;
-        amin = a < amin ? a : amin;
-        ++h;
       }
     }
-    PROM_TS(o * 16 + 5);
     if (window) {
-      // ---- 3d. envelopes B (suffix max of b), A (prefix min of a) over records, into LDS
-      double* sB = reinterpret_cast<double*>(skey);
-      double* sA = sF;
-      const double bcarry = wg_excl_suffix<double>(bmax, OpMax(), 0.0, wd);
-      const double acarry = wg_excl_prefix<double>(amin, OpMin(), 1.0e308, wd);   // barriers: LDS reuse ok
-      double run = bcarry;
-#pragma unroll
-      for (int m = kWPer - 1; m >= 0; --m)
-        if (m < nheads) { run = bb[m] > run ? bb[m] : run; sB[gb + m] = run; }
-      run = acarry;
-#pragma unroll
-      for (int m = 0; m < kWPer; ++m)
-        if (m < nheads) { run = aa[m] < run ? aa[m] : run; sA[gb + m] = run; }
-      PROM_TS(o * 16 + 6);
-      // ---- 3e. suffix tail moments  M_e(g) = c_e sum_{j >= g} F_j n_j^e
-      double part[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) part[k] = 0.0;
-#pragma unroll
-      for (int m = 0; m < kWPer; ++m)
-        if (m < nheads) {
-          double pw[NS][4];
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const double v = Nv[m][s] * inv[s];
-            pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
-          }
-#pragma unroll
-          for (int k = 0; k < K; ++k) part[k] += gF[m] * mono_eval<NS>(M, k, pw);
-        }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        double inc = part[k];
-        for (int off = 1; off < 64; off <<= 1) {
-          const double u = __shfl_down(inc, off, 64);
-          if (lane + off < 64) inc += u;
-        }
-        double exc = __shfl_down(inc, 1, 64);
-        if (lane == 63) exc = 0.0;
-        if (lane == 0) rk[wid][k] = inc;
-        part[k] = exc;
-      }
-      __syncthreads();
-      double* mm = wmom + (int64_t)o * (n_pr + 1) * K;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        double c = part[k];
-        for (int w = NW - 1; w > wid; --w) c += rk[w][k];
-        part[k] = c;
-      }
-#pragma unroll
-      for (int m = kWPer - 1; m >= 0; --m)
-        if (m < nheads) {
-          double pw[NS][4];
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const double v = Nv[m][s] * inv[s];
-            pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
-          }
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            part[k] += gF[m] * mono_eval<NS>(M, k, pw);
-            mm[(int64_t)(gb + m) * K + k] = M.c[k] * part[k];
-          }
-        }
       if (tid < K) mm[(int64_t)G * K + tid] = 0.0;
-      PROM_TS(o * 16 + 7);
-      // ---- 3f. threshold tables (LDS searches)
+      __syncthreads();
+      PROM_TS(o * 16 + 4);
       int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
       for (int32_t e = tid; e < kEnvN; e += kWBlock) {
         const double X = __builtin_bit_cast(double, (unsigned long long)(kEnvVmin + e) << 49);
@@ -1224,9 +1323,6 @@ __global__ void __launch_bounds__(kWBlock) k_chords_w(const int32_t* __restrict_
     counts[o * kCnt + 6] = (sorted && window) ? 1 : 0;
     counts[o * kCnt + 7] = 0;
   }
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-    if (tid == s) nmax_out[o * NS + s] = nm[s];
   PROM_TS(o * 16 + 8);
 }
 
@@ -1252,6 +1348,30 @@ __device__ __forceinline__ double acc_exp2k(double acc, double F, double y, cons
   return __builtin_fma(F * S, e, acc);
 }
 
+// acc + F * exp(-tau) with y = -tau * 256 / ln2 given: 2^(y/256) = 2^(k >> 8) T[k & 255] exp(d ln2/256),
+// k = rint(y), d = y - k in [-1/2, 1/2], degree-5 Taylor polynomial (truncation (ln2/512)^6/720 = 9e-21
+// relative), T[i] = 2^(i/256) = the 2048-entry table at 8i (LDS, 2 KB).  y below -2^31 saturates the
+// integer conversion and ldexp returns 0, exp's own answer there.  About 12 FP64 operations.
+constexpr double kE256C1 = 0x1.62e42fefa39efp-9;   // (ln2/256)^1 / 1!
+constexpr double kE256C2 = 0x1.ebfbdff82c58fp-19;  // (ln2/256)^2 / 2!
+constexpr double kE256C3 = 0x1.c6b08d704a0c0p-29;  // (ln2/256)^3 / 3!
+constexpr double kE256C4 = 0x1.3b2ab6fba4e77p-39;  // (ln2/256)^4 / 4!
+constexpr double kE256C5 = 0x1.5d87fe78a6731p-50;  // (ln2/256)^5 / 5!
+constexpr double kM256Ln2 = -0x1.71547652b82fep+8; // -256 / ln2
+
+__device__ __forceinline__ double acc_exp256(double acc, double F, double y, const double* __restrict__ tab) {
+  const double k = __builtin_rint(y);
+  const int ki = (int)k;
+  const double d = y - k;
+  double p = __builtin_fma(d, kE256C5, kE256C4);
+  p = __builtin_fma(d, p, kE256C3);
+  p = __builtin_fma(d, p, kE256C2);
+  p = __builtin_fma(d, p, kE256C1);
+  p = __builtin_fma(d, p, 1.0);
+  const double S = __builtin_amdgcn_ldexp(tab[ki & 255], ki >> 8);
+  return __builtin_fma(F * S, p, acc);
+}
+
 __device__ __forceinline__ void fill_exp_table(double* etab) {
   for (int i = threadIdx.x; i < PROM_EXP2_TABLE_N; i += kBlock) etab[i] = kExp2TableDev[i];
 }
@@ -1272,7 +1392,7 @@ __device__ __forceinline__ int env_floor(float x) {
 // R[o][w].  NS: atomic slots (0 = runtime count, sigma in LDS).  EXPK 1: table exp (the exact ocml
 // path for phases flagged non-finite); 0: ocml exp everywhere (validation).
 template <int NS, int EXPK>
-__global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ tabs,
+__global__ void __launch_bounds__(kBlock) k_tau(const SigTabs4 tabv, const SigTabDev* __restrict__ tabs,
                                                 const double* __restrict__ wav,
                                                 const double* __restrict__ recs,
                                                 const double* __restrict__ mrecs,
@@ -1282,8 +1402,7 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
                                                 const double* __restrict__ tfrac,
                                                 const double* __restrict__ fsum, int32_t n_atoms_rt,
                                                 int32_t n_pr, int32_t n_orb, int32_t phases_per_group,
-                                                int64_t n_wav, const double* __restrict__ nmax,
-                                                const int32_t* __restrict__ wenv,
+                                                int64_t n_wav, const int32_t* __restrict__ wenv,
                                                 const double* __restrict__ wmom,
                                                 unsigned long long* __restrict__ evals,
                                                 double* __restrict__ R) {
@@ -1291,11 +1410,13 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
 #ifdef PROM_TRACE
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) { g_trace[4002] = wall_clock64(); g_trace[4003] = clock64(); }
 #endif
-  extern __shared__ double lds[];   // [2048] exp table | NS == 0: [2][n_atoms][kBlock]
+  extern __shared__ double lds[];   // EXPK 1: [2048] exp table | NS == 0: [2][n_atoms][kBlock]
   double* etab = lds;
-  double* sgl = lds + (EXPK ? PROM_EXP2_TABLE_N : 0);
-  if (EXPK) fill_exp_table(etab);
-  __syncthreads();
+  double* sgl = lds + (EXPK == 1 ? PROM_EXP2_TABLE_N : 0);
+  if constexpr (EXPK == 1) {
+    fill_exp_table(etab);
+    __syncthreads();
+  }
   const int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
@@ -1324,9 +1445,9 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
     if constexpr (NS > 0) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const double sh = tabs[s].shift[o];
+        const double sh = tabv.t[s].shift[o];
         if (!(sh == shv[s])) {
-          sg[s] = sigma_of(sh * lam, tabs[s]);
+          sg[s] = sigma_of(sh * lam, tabv.t[s]);
           shv[s] = sh;
         }
       }
@@ -1341,7 +1462,7 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
           // window [h, t) of this wavefront (see "windowed integration" above k_chords_w)
           double Q = 0.0;
 #pragma unroll
-          for (int s = 0; s < NS; ++s) { q[s] = sg[s] * nmax[o * NS + s]; Q += q[s]; }
+          for (int s = 0; s < NS; ++s) { q[s] = sg[s] * tabv.t[s].nscale; Q += q[s] > 0.0 ? q[s] : 0.0; }
           const bool bad = !(Q <= 1.0e100);
           const float qf = (float)Q;
           float qh = qf * (1.0f + 0x1p-20f), ql = qf * (1.0f - 0x1p-20f);
@@ -1361,12 +1482,22 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
           }
         }
         PROM_CLK(tc2);
-        for (int32_t i = i_lo; i < i_hi; ++i) {
-          const double* r = rec + (int64_t)i * stride;
-          double y = r[1] * sp[0];
+        if constexpr (EXPK == 2) {
+          for (int32_t i = i_lo; i < i_hi; ++i) {
+            const double* r = rec + (int64_t)i * stride;
+            double tau = r[1] * sg[0];
 #pragma unroll
-          for (int s = 1; s < NS; ++s) y = __builtin_fma(r[1 + s], sp[s], y);
-          acc = acc_exp2k(acc, r[0], y, etab);
+            for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[s];
+            acc = __builtin_fma(r[0], exp(-tau), acc);
+          }
+        } else {
+          for (int32_t i = i_lo; i < i_hi; ++i) {
+            const double* r = rec + (int64_t)i * stride;
+            double y = r[1] * sp[0];
+#pragma unroll
+            for (int s = 1; s < NS; ++s) y = __builtin_fma(r[1 + s], sp[s], y);
+            acc = acc_exp2k(acc, r[0], y, etab);
+          }
         }
         PROM_CLK(tc3);
         if (win && i_hi < n_act) {
@@ -1418,12 +1549,19 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
           sh_l[li] = sh;
         }
       }
-      if (!exact) {
+      if (!exact && EXPK == 1) {
         for (int32_t i = 0; i < n_act; ++i) {
           const double* r = rec + (int64_t)i * stride;
           double y = r[1] * (sg_l[threadIdx.x] * kMinus2048OverLn2);
           for (int32_t s = 1; s < ns; ++s) y = __builtin_fma(r[1 + s], sg_l[s * kBlock + threadIdx.x] * kMinus2048OverLn2, y);
           acc = acc_exp2k(acc, r[0], y, etab);
+        }
+      } else if (!exact) {
+        for (int32_t i = 0; i < n_act; ++i) {
+          const double* r = rec + (int64_t)i * stride;
+          double tau = r[1] * sg_l[threadIdx.x];
+          for (int32_t s = 1; s < ns; ++s) tau = tau + r[1 + s] * sg_l[s * kBlock + threadIdx.x];
+          acc = __builtin_fma(r[0], exp(-tau), acc);
         }
       } else {
         const int32_t* ipl = act_ip + (int64_t)o * n_pr;
@@ -1449,6 +1587,230 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
 #endif
 }
 
+// ---- windowed fused kernel: sigma -> window -> exp(-tau) over [h, t) + tail polynomial -> R ------------
+// A workgroup covers kTW = 256 consecutive wavelengths x kTP = 4 phases: wavefront p of the workgroup
+// integrates phase o0 + p for all 256 wavelengths (4 per lane: w = tile + 64 j + lane).  Everything is
+// arranged around few dependent memory round trips (about 2 us each on a busy MI355X):
+//   1. wavelengths (vector loads), phase counters and Doppler factors (scalar loads);
+//   2.-3. sigma_s at the shifted wavelengths: bucket directory, then a 4-node window.  UNI (no orbital
+//      Doppler shift): sigma was resampled once per wavelength by the column kernel, one load;
+//   4. the wavefront's window [h, t): threshold tables at its Q range (DPP max/min);
+//   5. records [h, t) and the tail moments at t (scalar loads, shared by the 4 wavelengths of a lane).
+constexpr int kTW = 256;   // wavelengths per workgroup
+constexpr int kTP = 4;     // phases per workgroup (one per wavefront)
+constexpr int kLPT = kTW / 64;
+
+template <int NS, bool UNI>
+__global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs4 tabv, const double* __restrict__ wav,
+                                                  const double* __restrict__ recs,
+                                                  const double* __restrict__ mrecs,
+                                                  const int32_t* __restrict__ act_ip,
+                                                  const double* __restrict__ fout,
+                                                  const int32_t* __restrict__ counts,
+                                                  const double* __restrict__ tfrac,
+                                                  const double* __restrict__ fsum, int32_t n_pr,
+                                                  int32_t n_orb, int64_t n_wav,
+                                                  const int32_t* __restrict__ wenv,
+                                                  const double* __restrict__ wmom,
+                                                  const double* __restrict__ sig,
+                                                  unsigned long long* __restrict__ evals,
+                                                  double* __restrict__ R) {
+  constexpr Monos<NS> M{};
+  constexpr int K = Monos<NS>::K;
+  constexpr int ST = 1 + NS;
+  __shared__ double srec[kTP][2 * 64 * ST];   // per wavefront: two chunks of 64 records
+  __shared__ double sexp[256];                 // 2^(i/256)
+  sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
+  PROM_CLK(tk0);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kTW;
+  const int32_t o = blockIdx.y * kTP + wid;
+  const bool ph = o < n_orb;             // this wavefront has a phase
+  const int32_t oo = ph ? o : n_orb - 1;
+  // ---- 1.
+  double lam[kLPT];
+  bool live[kLPT];
+#pragma unroll
+  for (int j = 0; j < kLPT; ++j) {
+    const int64_t w = tile + 64 * j + lane;
+    live[j] = w < n_wav;
+    lam[j] = wav[live[j] ? w : n_wav - 1];
+  }
+  const int32_t* cp = counts + oo * kCnt;
+  const int32_t cA = cp[0], cG = cp[4];
+  const int32_t cF = (cp[5] ? 1 : 0) | (cp[6] ? 2 : 0) | (cp[3] ? 4 : 0);
+  const double tf = tfrac[oo];
+  // ---- 2.-3. sigma
+  double sg[kLPT][NS];
+  if constexpr (UNI) {
+    // resampled by the trailing workgroups of k_columns_lanes
+#pragma unroll
+    for (int j = 0; j < kLPT; ++j) {
+      const int64_t w = tile + 64 * j + lane;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sg[j][s] = sig[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double sh = tabv.t[s].shift[oo];
+#pragma unroll
+      for (int j = 0; j < kLPT; ++j) sg[j][s] = sigma_of(sh * lam[j], tabv.t[s]);
+    }
+  }
+  __syncthreads();   // sexp
+  if (!ph) return;
+  PROM_CLK(tk1);
+  // ---- 4. window (q_s = sigma_s / c_s, Q = sum_s max(q_s, 0))
+  bool bad = false;
+  float qh = 0.0f, ql = 3.4e38f;
+#pragma unroll
+  for (int j = 0; j < kLPT; ++j) {
+    double Qj = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double qs = sg[j][s] * tabv.t[s].nscale;
+      Qj += qs > 0.0 ? qs : 0.0;
+    }
+    bad = bad || !(Qj <= 1.0e100);
+    const float qf = (float)Qj;
+    qh = fmaxf(qh, qf * (1.0f + 0x1p-20f));
+    ql = fminf(ql, qf * (1.0f - 0x1p-20f));
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    qh = fmaxf(qh, __shfl_xor(qh, off, 64));
+    ql = fminf(ql, __shfl_xor(ql, off, 64));
+  }
+  bad = __ballot(bad) != 0ull;
+  const int32_t G = cG;
+  int32_t h = 0, t = (cF & 1) ? G : cA;
+  if ((cF & 2) && !bad) {
+    const int vt = env_floor((float)kTailEps / qh * (1.0f - 0x1p-20f));
+    const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
+    const int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
+    t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : et[vt - kEnvVmin]);
+    h = vh >= kEnvVmax ? 0 : et[kEnvN + (vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin)];
+  }
+  h = __builtin_amdgcn_readfirstlane(h < t ? h : t);
+  t = __builtin_amdgcn_readfirstlane(t);
+  PROM_CLK(tk2);
+  // ---- 5. integrate
+  double acc[kLPT];
+#pragma unroll
+  for (int j = 0; j < kLPT; ++j) acc[j] = 0.0;
+  if (cF & 4) {
+    // non-finite column densities: exact reference order over the chord-order records
+    const double* rb = recs + (int64_t)o * n_pr * ST;
+    const int32_t* ipl = act_ip + (int64_t)o * n_pr;
+    for (int32_t i = 0; i < cA; ++i) {
+      const double* r = rb + (int64_t)i * ST;
+      const double F = fout[ipl[i]];
+#pragma unroll
+      for (int j = 0; j < kLPT; ++j) {
+        double tau = r[1] * sg[j][0];
+#pragma unroll
+        for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[j][s];
+        acc[j] = acc[j] + F * exp(-tau);
+      }
+    }
+    const double fs = fsum[o];
+#pragma unroll
+    for (int j = 0; j < kLPT; ++j) acc[j] = (acc[j] + tf * fs) / fs;
+  } else {
+    const double* rb = ((cF & 1) ? mrecs : recs) + (int64_t)o * n_pr * ST;
+    const bool tail = (cF & 2) && t < G;
+    const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
+    // records staged through this wavefront's LDS slice in chunks of 64: one coalesced vector load per
+    // chunk (the next chunk's load is in flight while this one is integrated), broadcast LDS reads
+    if (h < t) {
+      double sy[kLPT][NS];   // -sigma 256/ln2: y = -tau 256/ln2 = sum_s N_s sy_s
+#pragma unroll
+      for (int j = 0; j < kLPT; ++j)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) sy[j][s] = sg[j][s] * kM256Ln2;
+      double* sr = srec[wid];
+      const double* src = rb + (int64_t)h * ST;
+      const int32_t nel = (t - h) * ST;
+      double nx[ST];
+#pragma unroll
+      for (int c = 0; c < ST; ++c) {
+        const int32_t e = 64 * c + lane;
+        nx[c] = e < nel ? src[e] : 0.0;
+      }
+      for (int32_t c0 = 0; c0 < t - h; c0 += 64) {
+        const int32_t nr = (t - h - c0) < 64 ? (t - h - c0) : 64;
+        double* buf = sr + ((c0 >> 6) & 1) * 64 * ST;
+#pragma unroll
+        for (int c = 0; c < ST; ++c) buf[64 * c + lane] = nx[c];
+        if (c0 + 64 < t - h) {
+#pragma unroll
+          for (int c = 0; c < ST; ++c) {
+            const int32_t e = (c0 + 64) * ST + 64 * c + lane;
+            nx[c] = e < nel ? src[e] : 0.0;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int32_t r = 0; r < nr; ++r) {
+          const double F = buf[r * ST];
+          double Nr[NS];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) Nr[s] = buf[r * ST + 1 + s];
+#pragma unroll
+          for (int j = 0; j < kLPT; ++j) {
+            double y = Nr[0] * sy[j][0];
+#pragma unroll
+            for (int s = 1; s < NS; ++s) y = __builtin_fma(Nr[s], sy[j][s], y);
+            acc[j] = acc_exp256(acc[j], F, y, sexp);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (tail) {
+#pragma unroll
+      for (int j = 0; j < kLPT; ++j) {
+        double pw[NS][4];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const double v = sg[j][s] * tabv.t[s].nscale;
+          pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = pw[s][2] * v;
+        }
+        double tl = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) tl = __builtin_fma(mp[k], mono_eval<NS>(M, k, pw), tl);
+        acc[j] += tl;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kLPT; ++j) acc[j] += tf;
+  }
+#pragma unroll
+  for (int j = 0; j < kLPT; ++j)
+    if (live[j]) R[(int64_t)o * n_wav + tile + 64 * j + lane] = acc[j];
+  if (evals && !(cF & 4)) {
+    int nl = 0;
+#pragma unroll
+    for (int j = 0; j < kLPT; ++j) nl += __popcll(__ballot(live[j]));
+    if (lane == 0)
+      atomicAdd(&evals[(blockIdx.x * kTP + wid) & 63], (unsigned long long)(t - h) * (unsigned long long)nl);
+  }
+#ifdef PROM_TRACE
+  {
+    const int64_t wv = 65536 + 8 * (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kTP + wid);
+    const long long tk3 = clock64();
+    PROM_ACC(wv + 0, tk1 - tk0);
+    PROM_ACC(wv + 1, tk2 - tk1);
+    PROM_ACC(wv + 2, tk3 - tk2);
+    PROM_ACC(wv + 4, 1);
+    PROM_ACC(wv + 5, t - h);
+    PROM_ACC(wv + 6, tk3 - tk0);
+    PROM_ACC(wv + 7, 1);
+  }
+#endif
+}
+
 // ---- molecular fused kernel -------------------------------------------------------------------
 // tau(c, w) = sum_atomic N_s sigma_s(w) + sum_mol dx * sum_x n_abs(c,x) sigma_m(P(c,x), T, lambda'_w)
 // (gasProperties.py:924-954).  Per thread (phase o, wavelength w) and molecular slot, the (T, lambda)
@@ -1457,7 +1819,7 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabDev* __restrict__ ta
 // (uniform bracket from k_mol_prep), 10^v and an FMA.  Out-of-table samples (P, T or lambda) take the
 // fill value, i.e. sigma = 0, as in the reference.
 template <int NSA, int EXPK>
-__global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabDev* __restrict__ tabs,
+__global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const SigTabDev* __restrict__ tabs,
                                                     const MolSlotDev* __restrict__ ms, int32_t n_mol,
                                                     int32_t max_np, const double* __restrict__ wav,
                                                     const double* __restrict__ recs,
@@ -1494,9 +1856,9 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabDev* __restrict_
     const double* __restrict__ rec = recs + (int64_t)o * n_pr * ST;
 #pragma unroll
     for (int s = 0; s < NSA; ++s) {
-      const double sh = tabs[s].shift[o];
+      const double sh = tabv.t[s].shift[o];
       if (!(sh == shv[s])) {
-        sg[s] = sigma_of(sh * lam, tabs[s]);
+        sg[s] = sigma_of(sh * lam, tabv.t[s]);
         shv[s] = sh;
       }
     }
@@ -1572,28 +1934,46 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabDev* __restrict_
   }
 }
 
-void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>& tables,
+void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;
-  PROM_HIP(hipEventRecord(ev[0], s));
+  const bool wpath = tr.exp_mode && tr.n_mol == 0 && tr.n_atoms >= 1 && tr.n_atoms <= kWinMaxSpecies;
+  // no orbital Doppler shift: sigma_s(lambda_w) is resampled once per wavelength by extra workgroups
+  // of the column kernel (they run beside the chord work) instead of once per phase group
+  const bool pre_sigma = wpath && tr.window && tr.uniform_shift;
+  const int32_t na = tr.n_atoms;
+  *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? (wpath && tr.window ? 20 : 10) : 0);
+  // stage events ride on the fast path's dispatch packets (hipExtLaunchKernelGGL start/stop events):
+  // no separate event packets between the kernels
+  hipEvent_t ev0 = ev ? ev[0] : nullptr;
   // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
-  if (tr.n_mol == 0 && tr.n_x <= 64) {
-#define PROM_COLS(LV)                                                                                    \
-  hipLaunchKernelGGL(k_columns_lanes<LV>, dim3((unsigned)((nc + kBlock / (LV) - 1) / (kBlock / (LV)))),  \
-                     dim3(kBlock), 0, s, tr.terms_dev.as<TermDev>(), tr.n_terms, tr.scdev.as<ScDev>(),    \
+  if (tr.n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4) {
+    const unsigned sig_blocks = pre_sigma ? grid_for(tr.n_wav) : 0u;
+#define PROM_COLS(LV, NSV)                                                                               \
+  hipExtLaunchKernelGGL((k_columns_lanes<LV, NSV>),                                                      \
+                     dim3((unsigned)((nc + kBlock / (LV) - 1) / (kBlock / (LV))) + sig_blocks),          \
+                     dim3(kBlock), 0, s, ev0, nullptr, 0, tr.colargs, tr.n_terms,                         \
                      tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
                      tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
                      tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
-                     tr.moon_R.as<double>(), tr.sigma_max_dev.as<double>(), tr.cull_tau, tr.ncol.as<double>(), \
-                     tr.flags.as<int32_t>())
-    if (tr.n_x <= 8) PROM_COLS(8);
-    else if (tr.n_x <= 16) PROM_COLS(16);
-    else if (tr.n_x <= 32) PROM_COLS(32);
-    else PROM_COLS(64);
+                     tr.moon_R.as<double>(), tr.sigma_max_dev.as<double>(), tr.cull_tau, rs.ncol.as<double>(), \
+                     rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>())
+#define PROM_COLS_L(NSV)                       \
+  if (tr.n_x <= 8) PROM_COLS(8, NSV);          \
+  else if (tr.n_x <= 16) PROM_COLS(16, NSV);   \
+  else if (tr.n_x <= 32) PROM_COLS(32, NSV);   \
+  else PROM_COLS(64, NSV);
+    if (!pre_sigma) { PROM_COLS_L(0) }
+    else if (na == 1) { PROM_COLS_L(1) }
+    else if (na == 2) { PROM_COLS_L(2) }
+    else if (na == 3) { PROM_COLS_L(3) }
+    else { PROM_COLS_L(4) }
+#undef PROM_COLS_L
 #undef PROM_COLS
     PROM_HIP(hipGetLastError());
   } else {
+    if (ev0) PROM_HIP(hipEventRecord(ev0, s));
     for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
       const DensityDev& m = tr.dens[sc];
       const double* tab = nullptr;
@@ -1617,19 +1997,19 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
                        tr.n_terms, tr.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
                        tr.cy.as<double>(), tr.cz.as<double>(), tr.planet_y.as<double>(), tr.planet_R,
                        tr.n_moons, tr.moon_y.as<double>(), tr.moon_R.as<double>(),
-                       tr.sigma_max_dev.as<double>(), mol_max, tr.cull_tau, tr.ncol.as<double>(),
-                       tr.molcol.as<double>(), tr.flags.as<int32_t>());
+                       tr.sigma_max_dev.as<double>(), mol_max, tr.cull_tau, rs.ncol.as<double>(),
+                       tr.molcol.as<double>(), rs.flags.as<int32_t>());
     PROM_HIP(hipGetLastError());
   }
   // 2. per-phase compaction, ordering, merging of equal-column chords, window tables
-  const bool wpath = tr.exp_mode && tr.n_mol == 0 && tr.n_atoms >= 1 && tr.n_atoms <= kWinMaxSpecies;
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
-  hipLaunchKernelGGL(k_chords_w<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, tr.flags.as<int32_t>(),      \
-                     tr.cfout.as<double>(), tr.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
-                     tr.window ? 1 : 0, tr.recs.as<double>(), tr.act_ip.as<int32_t>(), tr.mrecs.as<double>(), \
-                     tr.counts.as<int32_t>(), tr.tsum.as<double>(), tr.fsum.as<double>(), tr.nmax.as<double>(), \
-                     tr.wenv.as<int32_t>(), tr.wmom.as<double>())
+  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev ? ev[1] : nullptr, 0, \
+                     rs.flags.as<int32_t>(),                                                              \
+                     tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
+                     tr.window ? 1 : 0, tr.sigtab_v, rs.recs.as<double>(),                               \
+                     rs.act_ip.as<int32_t>(), rs.mrecs.as<double>(), rs.counts.as<int32_t>(),            \
+                     rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>())
     switch (tr.n_atoms) {
       case 1: PROM_CHW(1); break;
       case 2: PROM_CHW(2); break;
@@ -1638,15 +2018,13 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
     }
 #undef PROM_CHW
   } else {
-    hipLaunchKernelGGL(k_chords, dim3(tr.n_orb), dim3(kChordBlock), 0, s, tr.flags.as<int32_t>(),
-                       tr.cfout.as<double>(), tr.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
-                       (tr.merge && tr.exp_mode && tr.n_mol == 0) ? 1 : 0, tr.recs.as<double>(), tr.act_ip.as<int32_t>(),
-                       tr.mrecs.as<double>(), tr.counts.as<int32_t>(), tr.tsum.as<double>(), tr.fsum.as<double>());
+    hipLaunchKernelGGL(k_chords, dim3(tr.n_orb), dim3(kChordBlock), 0, s, rs.flags.as<int32_t>(),
+                       tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
+                       (tr.merge && tr.exp_mode && tr.n_mol == 0) ? 1 : 0, rs.recs.as<double>(), rs.act_ip.as<int32_t>(),
+                       rs.mrecs.as<double>(), rs.counts.as<int32_t>(), rs.tsum.as<double>(), rs.fsum.as<double>());
+    if (ev) PROM_HIP(hipEventRecord(ev[1], s));
   }
   PROM_HIP(hipGetLastError());
-  PROM_HIP(hipEventRecord(ev[1], s));
-  // 2. (sigma is fused into the tau kernel; the event pair brackets nothing since round 1.2)
-  PROM_HIP(hipEventRecord(ev[2], s));
   // 3. fused sigma -> tau -> exp -> disk-sum kernel
   // phase groups: enough waves for latency hiding (~8 per SIMD over 1024 SIMDs), few enough that
   // each thread reuses its sigma bracket across several phases
@@ -1657,22 +2035,22 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
   dim3 g((unsigned)n_tiles, (unsigned)groups);
   const SigTabDev* tabs = tr.sigtab.as<SigTabDev>();
   const double* wav = tr.wav.as<double>();
-  const double* recs = tr.recs.as<double>();
-  const double* mrecs = tr.mrecs.as<double>();
-  const int32_t* aip = tr.act_ip.as<int32_t>();
+  const double* recs = rs.recs.as<double>();
+  const double* mrecs = rs.mrecs.as<double>();
+  const int32_t* aip = rs.act_ip.as<int32_t>();
   const double* fo = tr.cfout.as<double>();
-  const int32_t* counts = tr.counts.as<int32_t>();
-  const double* tf = tr.tsum.as<double>();
-  const double* fs = tr.fsum.as<double>();
-  double* R = tr.R.as<double>();
-  const int na = tr.n_atoms;
+  const int32_t* counts = rs.counts.as<int32_t>();
+  const double* tf = rs.tsum.as<double>();
+  const double* fs = rs.fsum.as<double>();
+  double* R = rs.R.as<double>();
 #define PROM_TAU(NSV, EK)                                                                              \
   hipLaunchKernelGGL((k_tau<NSV, EK>), g, dim3(kBlock),                                                \
-                     ((EK) ? PROM_EXP2_TABLE_N * sizeof(double) : 0) +                                  \
+                     ((EK) == 1 ? PROM_EXP2_TABLE_N * sizeof(double) : 0) +                             \
                          ((NSV) == 0 ? (size_t)2 * na * kBlock * sizeof(double) : 0),                  \
-                     s, tabs, wav, recs, mrecs, aip, fo, counts, tf, fs, na, tr.n_pr, tr.n_orb, ppg, tr.n_wav, \
-                     tr.nmax.as<double>(), tr.wenv.as<int32_t>(), tr.wmom.as<double>(),                     \
-                     tr.count_evals ? tr.evals.as<unsigned long long>() : nullptr, R)
+                     s, tr.sigtab_v, tabs, wav, recs, mrecs, aip, fo, counts, tf, fs, na, tr.n_pr, tr.n_orb, ppg, \
+                     tr.n_wav, \
+                     rs.wenv.as<int32_t>(), rs.wmom.as<double>(),                                            \
+                     tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
 #define PROM_TAU_NS(EK)                 \
   switch (na) {                         \
     case 1: PROM_TAU(1, EK); break;     \
@@ -1681,6 +2059,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
     case 4: PROM_TAU(4, EK); break;     \
     default: PROM_TAU(0, EK);           \
   }
+  const bool tau_w = !(tr.n_mol > 0) && tr.exp_mode && wpath && tr.window;
+  if (ev && !tau_w) PROM_HIP(hipEventRecord(ev[2], s));
   if (tr.n_mol > 0) {
     PROM_REQUIRE(na <= 4, "transit: at most 4 atomic constituents next to molecular ones");
     int32_t max_np = 0;
@@ -1688,7 +2068,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
     const size_t lds = PROM_EXP2_TABLE_N * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
     PROM_REQUIRE(lds <= 160 * 1024, "transit: molecular tables too large for the LDS staging (n_mol * n_p)");
 #define PROM_TAUM(NSV, EK)                                                                                  \
-  hipLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
+  hipLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
                      max_np, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x,         \
                      tr.delta_x, tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(), R)
 #define PROM_TAUM_NS(EK)                \
@@ -1702,12 +2082,31 @@ void launch_transit(hipStream_t s, TransitDev& tr, const std::vector<AtomTable>&
     if (tr.exp_mode) { PROM_TAUM_NS(1) } else { PROM_TAUM_NS(0) }
 #undef PROM_TAUM_NS
 #undef PROM_TAUM
-  } else if (tr.exp_mode) { PROM_TAU_NS(1) } else { PROM_TAU_NS(0) }
+  } else if (tr.exp_mode && wpath && tr.window) {
+#define PROM_TAUW(NSV, PMV, UV)                                                                         \
+  hipExtLaunchKernelGGL((k_tau_w<NSV, UV>), dim3((unsigned)((tr.n_wav + kTW - 1) / kTW), (unsigned)((tr.n_orb + kTP - 1) / kTP)), \
+                     dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0,                  \
+                     tr.sigtab_v, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                     \
+                     tr.n_orb, tr.n_wav, rs.wenv.as<int32_t>(), rs.wmom.as<double>(), rs.sig.as<double>(),  \
+                     tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
+#define PROM_TAUW_NS(PMV, UV)            \
+  switch (na) {                          \
+    case 1: PROM_TAUW(1, PMV, UV); break; \
+    case 2: PROM_TAUW(2, PMV, UV); break; \
+    case 3: PROM_TAUW(3, PMV, UV); break; \
+    default: PROM_TAUW(4, PMV, UV); break; \
+  }
+    if (pre_sigma) { PROM_TAUW_NS(8, true) } else { PROM_TAUW_NS(2, false) }
+#undef PROM_TAUW_NS
+#undef PROM_TAUW
+    PROM_HIP(hipGetLastError());
+  }
+  else if (tr.exp_mode) { PROM_TAU_NS(1) }
+  else { PROM_TAU_NS(0) }
 #undef PROM_TAU_NS
 #undef PROM_TAU
   PROM_HIP(hipGetLastError());
-  *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? 10 : 0);
-  PROM_HIP(hipEventRecord(ev[3], s));
+  if (ev && !tau_w) PROM_HIP(hipEventRecord(ev[3], s));
 }
 
 }  // namespace prom

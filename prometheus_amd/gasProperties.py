@@ -490,10 +490,10 @@ class WavelengthGrid:
 
 
 # ============================================================================== transit
-# Shard and chunk boundaries are multiples of one wavefront (64 wavelengths): the tau kernel's
-# integration window is chosen per wavefront, so aligned boundaries keep every wavefront's set of
-# wavelengths -- and hence R, bit for bit -- independent of the number of shards and chunks.
-WAVE_ALIGN = 64
+# Shard and chunk boundaries are multiples of the tau kernel's wavelength tile (256 wavelengths, one
+# wavefront's integration window): aligned boundaries keep every tile's set of wavelengths -- and
+# hence R, bit for bit -- independent of the number of shards and chunks.
+WAVE_ALIGN = 256
 
 
 def _split(n: int, parts: int) -> List[Tuple[int, int]]:

@@ -42,8 +42,8 @@ for it in range(3):
     lib.prom_trace_read(buf, N, 1)
 a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
 n_orb = len(host["orb"])
-print("k_chords_w step times (us, workgroup of each phase): 1 pass1 | 2 compaction | 3 sort | 4 heads | "
-      "5 groups | 6 envelopes | 7 moments | 8 tables+end")
+print("k_order step times (us, workgroup of each phase): 1 load+scan | 2 sort | 3 fetch+scan | 4 records | "
+      "5-7 - | 8 tables+end")
 for o in range(n_orb):
     t = a[o * 16: o * 16 + 9]
     if t[0] == 0:
@@ -56,9 +56,15 @@ wall = (a[4000] - a[4002]) * 10.0  # ns, block 0 wave 0 lifetime
 clk = a[4001] - a[4003]
 print("clock64 ticks per ns (block 0 wave 0): %.3f" % (clk / max(wall, 1)))
 pairs = kt[:, 4].sum()
-print("k_tau per (wave, phase) mean ticks: sigma %.0f, window setup %.0f, exp loop %.0f, tail %.0f; "
-      "records/phase %.1f; pairs %d" % tuple([kt[:, i].sum() / pairs for i in range(4)] + [kt[:, 5].sum() / pairs, pairs]))
+print("k_tau_w per (wave, phase) mean ticks: sigma+windows %.0f, -, phases %.0f, -; records/phase %.1f; pairs %d"
+      % tuple([kt[:, i].sum() / pairs for i in range(4) if i in (0, 2)] + [kt[:, 5].sum() / pairs, pairs]))
 tot = kt[:, 6]
+win = kt[:, 5]
+print("window records per wave: p50 %.0f p90 %.0f p99 %.0f max %.0f" % tuple(np.percentile(win, [50, 90, 99, 100])))
+for lo, hi in [(0, 4), (4, 16), (16, 64), (64, 256), (256, 10**9)]:
+    m = (win >= lo) & (win < hi)
+    if m.any():
+        print("  window [%d,%d): %5d waves, lifetime mean %.0f max %.0f ticks" % (lo, hi, m.sum(), tot[m].mean(), tot[m].max()))
 print("k_tau per wave lifetime ticks: mean %.0f  p10 %.0f  p50 %.0f  p90 %.0f  max %.0f  (%d waves)"
       % (tot.mean(), *np.percentile(tot, [10, 50, 90, 100]), len(tot)))
 kc = a[600000:600000 + 2 * 100000].reshape(-1, 2)
