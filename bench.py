@@ -64,22 +64,32 @@ def global_config(name: str, world: int) -> dict:
 
 
 def flops_per_eval(n_atoms: int) -> int:
-    """FP64 flops (FMA = 2, as the 78.6 TFLOP/s peak counts them) of one chord-wavelength evaluation
-    in k_tau ("Roofline"): y = -tau*2048/ln2 = N_0 s_0 (+ fma per further species) ->
-    2S - 1;  2^(y/2048): rint, d = y - k, 3 FMA polynomial, ldexp -> 9;  F * S -> 1;  acc fma -> 2."""
-    return 2 * n_atoms - 1 + 12
+    """FP64 flops (FMA = 2) of one exact chord-wavelength evaluation in k_tau_w's window:
+    y = -tau 256/ln2 = sum_s N_s sy_s -> 2S - 1;  2^(y/256): rint, d = y - k, 5-FMA polynomial, ldexp -> 13;
+    F * S -> 1;  acc fma -> 2."""
+    return 2 * n_atoms - 1 + 16
 
 
-def latest_profile_traffic():
-    """HBM bytes per k_tau launch from the committed rocprofv3 PMC summary, if present."""
-    hits = sorted(glob.glob(os.path.join(REPO, "profiles", "*k_tau_traffic*.json")))
-    if not hits:
-        return None
-    try:
-        with open(hits[-1]) as fh:
-            return json.load(fh).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+def tau_bytes_per_launch(n_wav: int, n_orb: int, n_atoms: int) -> int:
+    """Algorithmic HBM bytes of one k_tau_w launch (DESIGN.md "Roofline"): R[n_orb][n_wav] written,
+    lambda and sigma_s (resampled by the column kernel) read once per wavelength; window records and
+    tail moments (<= 1 %) are not counted."""
+    return 8 * n_orb * n_wav + 8 * n_wav * (1 + n_atoms)
+
+
+def latest_profile_traffic(kernel: str = "prom::k_tau_w"):
+    """Measured HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC summary
+    (profiles/*traffic_all_kernels.json, tools/bench_traffic.sh), or None."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*traffic_all_kernels.json")), reverse=True):
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+        except Exception:
+            continue
+        for name, v in d.items():
+            if name.startswith(kernel):
+                return v.get("hbm_bytes_per_launch")
+    return None
 
 
 def describe(cfg: dict) -> str:
@@ -172,13 +182,15 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_pts * args.steps / elapsed
 
-    # dominant kernel: k_tau (fused tau/exp/disk-sum), average launch duration from live hipEvents
+    # dominant kernel: k_tau_w (windowed tau/exp/disk-sum); mean launch duration from the start/stop
+    # events carried on its own dispatch packets over the timed runs
     tau_ms = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
     n_atoms = prob.n_atoms
     cle = st["chord_lambda_evals"]
     evals = st["exp_evals"]
+    tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, n_atoms)
+    achieved_gbs = tau_bytes / (tau_ms * 1e-3) / 1e9
     flops = evals * flops_per_eval(n_atoms)
-    achieved_tflops = flops / (tau_ms * 1e-3) / 1e12
     traffic = latest_profile_traffic()
     # end-to-end (host prep + H2D + run + D2H) for reference, one call
     t_e2e = time.perf_counter()
@@ -202,13 +214,13 @@ def main():
                    "global_wavelengths": n_wav_global, "orbital_phases": n_orb,
                    "chords_per_phase": len(host["y"]), "los_samples": len(host["x"]),
                    "parallelism": "wavelength shards x%d (no collective)" % world},
-        "roofline": {"bound": "valu", "kernel": "k_tau", "achieved": achieved_tflops,
-                     "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tflops / FP64_VALU_PEAK_TFLOPS, "traffic": traffic,
-                     "tau_ms": tau_ms, "chord_lambda_evals": cle, "exp_evals": evals,
-                     "flops_per_eval": flops_per_eval(n_atoms),
-                     "exp_per_s": evals / (tau_ms * 1e-3),
-                     "chord_lambda_per_s": cle / (tau_ms * 1e-3)},
+        "roofline": {"bound": "hbm", "kernel": "k_tau_w", "achieved": achieved_gbs,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
+                     "traffic": traffic, "algorithmic_bytes": tau_bytes, "tau_ms": tau_ms,
+                     "exp_evals": evals, "chord_lambda_evals": cle,
+                     "valu": {"flops": flops, "flops_per_exp_eval": flops_per_eval(n_atoms),
+                              "achieved_tflops": flops / (tau_ms * 1e-3) / 1e12,
+                              "peak_tflops": FP64_VALU_PEAK_TFLOPS}},
         "stage_ms": {"density": float(np.mean(ms_runs[:, 0])) if len(ms_runs) else None,
                      "sigma": float(np.mean(ms_runs[:, 1])) if len(ms_runs) else None,
                      "tau": tau_ms,
