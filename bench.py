@@ -125,7 +125,7 @@ def main():
     if world > 1:
         import torch.distributed as dist  # noqa: F811  (gloo: barrier + max-reduce of times only)
         dist.init_process_group("gloo")
-    from prometheus_amd import _native, setupfile, gasProperties  # noqa: F401
+    from prometheus_amd import _native, setupfile, gasProperties, sharding  # noqa: F401
     _native.set_default_device(local_rank)
 
     cfg = global_config(args.config, world)
@@ -137,8 +137,7 @@ def main():
     tr = setupfile.build_transit(cfg)   # lambda grid + device Voigt tables on this rank's GPU
     dev = _native.get_device(local_rank)
     n_wav_global = len(tr.wavelength)
-    shards = gasProperties._split(n_wav_global, world)   # wavefront-aligned contiguous shards
-    w0, w1 = shards[rank] if rank < len(shards) else (n_wav_global, n_wav_global)
+    w0, w1 = sharding.shard_for_rank(n_wav_global, world, rank)   # tile-aligned contiguous shards
     host = tr._host_inputs()
     prob = tr._problem(dev, host, w0, w1, 0.0)
     dev.transit_set(prob)
@@ -169,16 +168,7 @@ def main():
     ms_runs = dev.timing_end(max_runs=args.steps)
     if dist:
         dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        pts = torch.tensor([float(n_pts_rank)], dtype=torch.float64)
-        dist.all_reduce(pts, op=dist.ReduceOp.SUM)
-        total_pts = float(pts.item())
-    else:
-        total_pts = float(n_pts_rank)
+    elapsed, total_pts = sharding.reduce_timing(dist, t1 - t0, n_pts_rank)
     ms_step = elapsed / args.steps * 1e3
     value = total_pts * args.steps / elapsed
 

@@ -31,6 +31,7 @@ import numpy as np
 from . import _native
 from . import constants as const
 from . import geometryHandler as geom
+from .sharding import WAVE_ALIGN, split as _split   # shard / chunk edges
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 lineListPath: str = os.path.join(_HERE, "resources", "LineList.txt")
@@ -490,19 +491,6 @@ class WavelengthGrid:
 
 
 # ============================================================================== transit
-# Shard and chunk boundaries are multiples of the tau kernel's wavelength tile (256 wavelengths, one
-# wavefront's integration window): aligned boundaries keep every tile's set of wavelengths -- and
-# hence R, bit for bit -- independent of the number of shards and chunks.
-WAVE_ALIGN = 256
-
-
-def _split(n: int, parts: int) -> List[Tuple[int, int]]:
-    edges = (np.linspace(0, n / WAVE_ALIGN, parts + 1).round() * WAVE_ALIGN).astype(np.int64)
-    edges[-1] = n
-    edges = np.minimum(edges, n)
-    return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:]) if b > a]
-
-
 class Transit:
     """Transit depth R(orbital phase, wavelength) (gasProperties.py:1074-1258)."""
 
