@@ -211,10 +211,7 @@ def main():
                      "valu": {"flops": flops, "flops_per_exp_eval": flops_per_eval(n_atoms),
                               "achieved_tflops": flops / (tau_ms * 1e-3) / 1e12,
                               "peak_tflops": FP64_VALU_PEAK_TFLOPS}},
-        "stage_ms": {"density": float(np.mean(ms_runs[:, 0])) if len(ms_runs) else None,
-                     "sigma": float(np.mean(ms_runs[:, 1])) if len(ms_runs) else None,
-                     "tau": tau_ms,
-                     "total": float(np.mean(ms_runs[:, 3])) if len(ms_runs) else None},
+        "stage_ms_single_run": {"columns_order": st["ms_density"], "tau": st["ms_tau"], "total": st["ms_total"]},
         "chords": {"active": st["active_chords"], "transparent": st["transparent_chords"],
                    "blocked": st["blocked_chords"], "integrated_records": st["tau_records"]},
         "setup_s": setup_s,

@@ -183,17 +183,21 @@ typedef struct prom_transit_stats {
 
 /* Copy a problem to the device (all host arrays are read during the call). */
 int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* problem);
-/* Run the integrator on the device; R stays in device memory.  stats may be NULL. */
+/* Run the integrator on the device; R stays in device memory.  stats may be NULL (with stats the
+ * call waits for the run).  Runs are asynchronous: consecutive runs of a problem on the fast path
+ * (1-4 atomic species, windows on) rotate over PROM_PIPELINE (default 4) internal streams and
+ * work-buffer slots, so one run's column / ordering kernels overlap earlier runs' tau kernels;
+ * prom_transit_result, prom_synchronize and prom_transit_set wait for all of them. */
 int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats);
 /* Copy R[n_orb][n_wav] (row-major) of the last run to a host buffer. */
 int32_t prom_transit_result(prom_ctx* ctx, double* R_out);
 /* Column densities N[s][o][ip] of the last run (atomic constituents in scenario order); testing aid. */
 int32_t prom_transit_columns(prom_ctx* ctx, double* N_out);
 
-/* Live per-run stage timing without per-run synchronisation: between prom_timing_begin and
- * prom_timing_end every prom_transit_run records its own hipEvents on the context's stream;
- * prom_timing_end waits for them and returns ms[run][4] = {density, sigma, tau, total} for up to
- * max_runs runs (n_runs receives the count). */
+/* Live per-run timing of the tau kernel without per-run synchronisation: between prom_timing_begin
+ * and prom_timing_end every prom_transit_run carries start/stop events on its tau kernel's dispatch;
+ * prom_timing_end waits for them and returns ms[run][4] = {NaN, NaN, tau, NaN} for up to max_runs
+ * runs (n_runs receives the count).  Stage times of a single run come from prom_transit_run's stats. */
 int32_t prom_timing_begin(prom_ctx* ctx);
 int32_t prom_timing_end(prom_ctx* ctx, int32_t max_runs, double* ms, int32_t* n_runs);
 

@@ -1,6 +1,7 @@
 // C-ABI layer of libprom_hip.so (declared in include/prom_hip.h).  Host code only: argument checks,
 // device memory owned by the context, H2D/D2H copies and kernel launches on the context's stream.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <exception>
@@ -71,8 +72,12 @@ int32_t prom_create(int32_t device, prom_ctx** out) {
   prom_ctx* ctx = new (std::nothrow) prom_ctx();
   if (!ctx) return PROM_E_NOMEM;
   ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream1, hipStreamNonBlocking) != hipSuccess) {
+  bool ok = hipSetDevice(device) == hipSuccess;
+  for (int i = 0; ok && i < prom::kMaxSlots; ++i)
+    ok = hipStreamCreateWithFlags(&ctx->streams[i], hipStreamNonBlocking) == hipSuccess;
+  ctx->stream = ctx->streams[0];
+  if (const char* e = std::getenv("PROM_PIPELINE")) ctx->pipeline = std::max(1, std::min(prom::kMaxSlots, std::atoi(e)));
+  if (!ok) {
     delete ctx;
     return PROM_E_HIP;
   }
@@ -94,9 +99,11 @@ void prom_destroy(prom_ctx* ctx) {
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->tev) (void)hipEventDestroy(e);
-  if (ctx->stream1) (void)hipStreamSynchronize(ctx->stream1);
-  if (ctx->stream1) (void)hipStreamDestroy(ctx->stream1);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  for (auto& st : ctx->streams)
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
   delete ctx;  // DevBuf destructors free device memory
 }
 
@@ -104,8 +111,7 @@ const char* prom_last_error(const prom_ctx* ctx) { return ctx ? ctx->err.c_str()
 
 int32_t prom_synchronize(prom_ctx* ctx) {
   return guarded(ctx, [&] {
-    PROM_HIP(hipStreamSynchronize(ctx->stream));
-    PROM_HIP(hipStreamSynchronize(ctx->stream1));
+    for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
   });
 }
 
@@ -305,8 +311,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.delta_x = pb->delta_x;
     tr.planet_R = pb->planet_R;
     tr.cull_tau = pb->cull_tau > 0.0 ? pb->cull_tau : std::ldexp(1.0, -60);
-    PROM_HIP(hipStreamSynchronize(ctx->stream1));   // a pipelined run may still read the old problem
-    PROM_HIP(hipStreamSynchronize(ctx->stream));
+    for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));   // pipelined runs may still read the old problem
     tr.exp_mode = (pb->options & PROM_OPT_OCML_EXP) ? 0 : 1;
     tr.merge = (pb->options & PROM_OPT_NO_MERGE) == 0;
     tr.window = (pb->options & PROM_OPT_NO_WINDOW) == 0;
@@ -450,8 +455,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     // work buffers
     const int64_t nc = n_orb * tr.n_pr;
     tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
-    tr.pipelined = tr.exp_mode && n_mol == 0 && n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && tr.window;
-    for (int si = 0; si < (tr.pipelined ? 2 : 1); ++si) {
+    const bool fast = tr.exp_mode && n_mol == 0 && n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && tr.window;
+    tr.depth = fast ? ctx->pipeline : 1;
+    for (int si = 0; si < tr.depth; ++si) {
     prom::RunSlot& rs = tr.slot[si];
       rs.ncol.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * nc);
       tr.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
@@ -500,11 +506,12 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     tr.count_evals = stats != nullptr;
     // pipelined problems alternate slots and streams: this run's column / ordering kernels overlap the
     // previous run's tau kernel; a slot is reused two runs later, after its stream's previous run
-    const int si = tr.pipelined ? (tr.last ^ 1) : 0;
-    const hipStream_t st = si ? ctx->stream1 : ctx->stream;
+    const int si = (tr.last + 1) % tr.depth;
+    const hipStream_t st = ctx->streams[si];
     prom::RunSlot& rs = tr.slot[si];
     if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
-    prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, (stats || ctx->timing) ? ev : nullptr, &variant);
+    prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, (stats || ctx->timing) ? ev : nullptr, &variant,
+                         stats != nullptr);
     tr.last = si;
     tr.count_evals = false;
 
@@ -553,7 +560,7 @@ int32_t prom_transit_result(prom_ctx* ctx, double* R_out) {
     prom::TransitDev& tr = ctx->tr;
     if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_result: no completed run");
     PROM_REQUIRE(R_out, "prom_transit_result: null output");
-    PROM_HIP(hipStreamSynchronize(ctx->stream1));
+    for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
     download(R_out, tr.slot[tr.last].R, (int64_t)tr.n_orb * tr.n_wav, ctx->stream);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
   });
@@ -564,7 +571,7 @@ int32_t prom_transit_columns(prom_ctx* ctx, double* N_out) {
     prom::TransitDev& tr = ctx->tr;
     if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_columns: no completed run");
     PROM_REQUIRE(N_out, "prom_transit_columns: null output");
-    PROM_HIP(hipStreamSynchronize(ctx->stream1));
+    for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
     download(N_out, tr.slot[tr.last].ncol, (int64_t)tr.n_atoms * tr.n_orb * tr.n_pr, ctx->stream);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
   });
@@ -582,16 +589,14 @@ int32_t prom_timing_end(prom_ctx* ctx, int32_t max_runs, double* ms, int32_t* n_
     PROM_REQUIRE(n_runs && (max_runs <= 0 || ms), "prom_timing_end: bad arguments");
     ctx->timing = false;
     const int32_t n = std::min(ctx->timed_runs, std::max(max_runs, 0));
-    PROM_HIP(hipStreamSynchronize(ctx->stream));
-    PROM_HIP(hipStreamSynchronize(ctx->stream1));
+    for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
     for (int32_t r = 0; r < n; ++r) {
       hipEvent_t* e = &ctx->tev[4 * (size_t)r];
       float v[4];
-      PROM_HIP(hipEventElapsedTime(&v[0], e[0], e[1]));
-      PROM_HIP(hipEventElapsedTime(&v[1], e[1], e[2]));
+      // timed runs carry only the tau kernel's start/stop pair (no extra packets between kernels)
       PROM_HIP(hipEventElapsedTime(&v[2], e[2], e[3]));
-      PROM_HIP(hipEventElapsedTime(&v[3], e[0], e[3]));
-      for (int i = 0; i < 4; ++i) ms[4 * r + i] = v[i];
+      ms[4 * r + 0] = ms[4 * r + 1] = ms[4 * r + 3] = std::nan("");
+      ms[4 * r + 2] = v[2];
     }
     *n_runs = ctx->timed_runs;
     ctx->timed_runs = 0;

@@ -153,9 +153,10 @@ struct MolTable {
   double vmax = 0.0;
 };
 
-// Work and output buffers of one run.  Two slots: consecutive runs alternate between them (and between
-// the context's two streams) so that a run's column / ordering kernels overlap the previous run's tau
-// kernel.
+// Work and output buffers of one run.  Fast-path problems rotate consecutive runs over `depth` slots
+// and as many streams (PROM_PIPELINE, default 4), so that a run's column / ordering kernels overlap
+// the previous runs' tau kernels; every run is complete and independent.
+constexpr int kMaxSlots = 4;
 struct RunSlot {
   DevBuf ncol;                              // [n_atoms][n_orb][n_pr]
   DevBuf flags;                             // [n_orb][n_pr] int32: 0 active, 1 transparent, 2 blocked
@@ -209,8 +210,8 @@ struct TransitDev {
   DevBuf mol_na;                            // [n_mol][n_orb][n_pr][n_x] n_abs = n chi
   std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
-  RunSlot slot[2];
-  bool pipelined = false;                   // fast path: runs alternate slots / streams
+  RunSlot slot[kMaxSlots];
+  int depth = 1;                            // slots in use: fast path = pipeline depth, else 1
   int last = 0;                             // slot of the most recent run
 };
 
@@ -219,7 +220,8 @@ struct TransitDev {
 struct prom_ctx {
   int32_t device = 0;
   hipStream_t stream = nullptr;  // slot-0 stream (and the stream of every non-run call)
-  hipStream_t stream1 = nullptr; // slot-1 stream
+  hipStream_t streams[prom::kMaxSlots] = {};   // streams[0] == stream
+  int pipeline = 4;              // PROM_PIPELINE (1 .. kMaxSlots)
   hipEvent_t ev[8] = {};
   std::string err;
   std::vector<prom::AtomTable> tables;
@@ -243,9 +245,10 @@ void launch_density(hipStream_t s, const DensityDev& m, const double* x, int32_t
                     const double* z, const double* bx, const double* by, int64_t n_chords, double* out);
 void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, int32_t n_x,
                             const double* P, double T, int64_t n_wav, const double* wav, double* out);
-// ev (may be null): stage events {start, columns+ordering done, (same), tau done}
+// ev (may be null): {start, columns+ordering done, tau start, tau done}; stage_events false: only the
+// tau pair (the fast path carries them on the tau kernel's dispatch packet)
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
-                    const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant);
+                    const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
 
 }  // namespace prom

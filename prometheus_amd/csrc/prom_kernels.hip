@@ -1935,7 +1935,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
 }
 
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
-                    const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant) {
+                    const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;
   const bool wpath = tr.exp_mode && tr.n_mol == 0 && tr.n_atoms >= 1 && tr.n_atoms <= kWinMaxSpecies;
   // no orbital Doppler shift: sigma_s(lambda_w) is resampled once per wavelength by extra workgroups
@@ -1945,7 +1945,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? (wpath && tr.window ? 20 : 10) : 0);
   // stage events ride on the fast path's dispatch packets (hipExtLaunchKernelGGL start/stop events):
   // no separate event packets between the kernels
-  hipEvent_t ev0 = ev ? ev[0] : nullptr;
+  hipEvent_t ev0 = (ev && stage_events) ? ev[0] : nullptr;
+  hipEvent_t ev1 = (ev && stage_events) ? ev[1] : nullptr;
   // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
   if (tr.n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4) {
@@ -2004,7 +2005,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // 2. per-phase compaction, ordering, merging of equal-column chords, window tables
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
-  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev ? ev[1] : nullptr, 0, \
+  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev1, 0,                \
                      rs.flags.as<int32_t>(),                                                              \
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
                      tr.window ? 1 : 0, tr.sigtab_v, rs.recs.as<double>(),                               \
@@ -2022,7 +2023,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                        tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
                        (tr.merge && tr.exp_mode && tr.n_mol == 0) ? 1 : 0, rs.recs.as<double>(), rs.act_ip.as<int32_t>(),
                        rs.mrecs.as<double>(), rs.counts.as<int32_t>(), rs.tsum.as<double>(), rs.fsum.as<double>());
-    if (ev) PROM_HIP(hipEventRecord(ev[1], s));
+    if (ev1) PROM_HIP(hipEventRecord(ev1, s));
   }
   PROM_HIP(hipGetLastError());
   // 3. fused sigma -> tau -> exp -> disk-sum kernel

@@ -19,6 +19,7 @@ for _ in range(5):
     dev.transit_run()
 dev.synchronize()
 N = 200
+print("PROM_PIPELINE", os.environ.get("PROM_PIPELINE", "2"))
 for timing in (False, True):
     if timing:
         dev.timing_begin()
