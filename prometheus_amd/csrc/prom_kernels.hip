@@ -1588,15 +1588,16 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabs4 tabv, const SigTa
 }
 
 // ---- windowed fused kernel: sigma -> window -> exp(-tau) over [h, t) + tail polynomial -> R ------------
-// A workgroup covers kTW = 256 consecutive wavelengths x kTP = 4 phases: wavefront p of the workgroup
-// integrates phase o0 + p for all 256 wavelengths (4 per lane: w = tile + 64 j + lane).  Everything is
+// A workgroup covers kTW = 128 consecutive wavelengths x kTP = 4 phases: wavefront p of the workgroup
+// integrates phase o0 + p for all 128 wavelengths (2 per lane: w = tile + 64 j + lane; 128 measured
+// faster than 64 or 256: wider tiles widen the union window at line cores).  Everything is
 // arranged around few dependent memory round trips (about 2 us each on a busy MI355X):
 //   1. wavelengths (vector loads), phase counters and Doppler factors (scalar loads);
 //   2.-3. sigma_s at the shifted wavelengths: bucket directory, then a 4-node window.  UNI (no orbital
 //      Doppler shift): sigma was resampled once per wavelength by the column kernel, one load;
 //   4. the wavefront's window [h, t): threshold tables at its Q range (DPP max/min);
 //   5. records [h, t) and the tail moments at t (scalar loads, shared by the 4 wavelengths of a lane).
-constexpr int kTW = 256;   // wavelengths per workgroup
+constexpr int kTW = 128;   // wavelengths per workgroup
 constexpr int kTP = 4;     // phases per workgroup (one per wavefront)
 constexpr int kLPT = kTW / 64;
 

@@ -4,7 +4,8 @@ reference memoryHandler.py:13-66, for the multi-device case).
 R at one wavelength does not depend on any other wavelength, so the spectrum splits into contiguous
 wavelength shards with no exchange step: one process (bench.py under torch.distributed.run) or one
 host thread (Transit.sumOverChords(devices=...)) per GPU, and a host-side gather.  Shard edges are
-multiples of the tau kernel's 256-wavelength tile, which keeps R bitwise identical
+multiples of 256 wavelengths, a multiple of the tau kernel's wavelength tile, which
+keeps R bitwise identical
 for any number of shards.
 """
 from __future__ import annotations
