@@ -9,7 +9,7 @@
 //   k_mol_sigma      MolecularConstituent.getSigmaAbs        gasProperties.py:789-818
 //   transit pipeline Transit.sumOverChords + getLOSopticalDepth_Batch (gasProperties.py:885-956,
 //                    :1160-1258):
-//     k_columns_lanes   blocking masks, densities evaluated on the fly, column densities
+//     k_columns8  blocking masks, densities evaluated on the fly, column densities
 //                 N = sum_x(n chi) dx (numpy pairwise order), tau upper bound -> active /
 //                 transparent / blocked  (k_ntot + k_columns when densities must be stored)
 //     k_chords    per phase: F_out and transparent sums, compaction of the active chords in chord
@@ -133,6 +133,65 @@ __device__ __forceinline__ double sigma_of(double t, const SigTabDev& tb) {
     }
   }
   return exp10(v) - tb.offset;
+}
+
+// ---- wavefront scans on DPP row shifts + cross-row readlanes (no LDS traffic, no bpermute) ----
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int32_t dpp_mov(int32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double lane_read(double v, int l) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ int32_t lane_read(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// inclusive prefix over lanes 0..63 (op applied as op(earlier, later))
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_prefix(T v, Op op) {
+  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
+  T t = dpp_mov<0x111>(v);
+  if (rl >= 1) v = op(t, v);
+  t = dpp_mov<0x112>(v);
+  if (rl >= 2) v = op(t, v);
+  t = dpp_mov<0x114>(v);
+  if (rl >= 4) v = op(t, v);
+  t = dpp_mov<0x118>(v);
+  if (rl >= 8) v = op(t, v);
+  const T r0 = lane_read(v, 15), r1 = lane_read(v, 31), r2 = lane_read(v, 47);
+  const T c01 = op(r0, r1), c012 = op(c01, r2);
+  if (row == 1) v = op(r0, v);
+  else if (row == 2) v = op(c01, v);
+  else if (row == 3) v = op(c012, v);
+  return v;
+}
+// inclusive suffix over lanes 63..0 (op applied as op(earlier, later))
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_suffix(T v, Op op) {
+  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
+  T t = dpp_mov<0x101>(v);
+  if (rl <= 14) v = op(v, t);
+  t = dpp_mov<0x102>(v);
+  if (rl <= 13) v = op(v, t);
+  t = dpp_mov<0x104>(v);
+  if (rl <= 11) v = op(v, t);
+  t = dpp_mov<0x108>(v);
+  if (rl <= 7) v = op(v, t);
+  const T r1 = lane_read(v, 16), r2 = lane_read(v, 32), r3 = lane_read(v, 48);
+  const T c23 = op(r2, r3), c123 = op(r1, c23);
+  if (row == 2) v = op(v, r3);
+  else if (row == 1) v = op(v, c23);
+  else if (row == 0) v = op(v, c123);
+  return v;
 }
 
 // numpy.heaviside(d, 1.0)
@@ -484,8 +543,8 @@ using ScDev = ScDevHost;
 // lanes 0..7 form numpy's eight pairwise partial sums, lane 0 combines them (loops_utils.h.src order)
 // -> N = (0.0 + pairwise_x(n chi)) * delta_x exactly as gasProperties.py:940.  The k_ntot + k_columns
 // pair handles molecular terms and n_x > 64.
-template <int L, int NSIG>
-__global__ void __launch_bounds__(kBlock) k_columns_lanes(const ColArgs ca, int32_t n_terms,
+template <int SPL, int NSIG>
+__global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n_terms,
                                  const double* __restrict__ x, int32_t n_x,
                                  int32_t n_pr, int32_t n_orb, double delta_x, const double* __restrict__ cy,
                                  const double* __restrict__ cz, const double* __restrict__ bx,
@@ -495,10 +554,12 @@ __global__ void __launch_bounds__(kBlock) k_columns_lanes(const ColArgs ca, int3
                                  double cull, double* __restrict__ ncol, int32_t* __restrict__ flags,
                                  const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
                                  double* __restrict__ sig) {
-  // a chord's L lanes sit inside one wavefront: the pairwise partial sums move by cross-lane
-  // shuffles, no LDS and no workgroup barrier
+  // Eight lanes per chord; lane j holds samples j, j + 8, ..., j + 8 (SPL - 1).  That is numpy's
+  // pairwise_sum layout (loops_utils.h.src) for 8 <= n_x < 128: lane j accumulates r[j] = a[j] +
+  // a[j+8] + ... sequentially, the eight partial sums combine as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+  // through DPP quad permutes and a row shift, and lane 0 adds the n_x % 8 remainder in order.
   PROM_CLK(tk0);
-  constexpr int G = kBlock / L;         // chords per workgroup
+  constexpr int G = kBlock / 8;         // chords per workgroup
   if constexpr (NSIG > 0) {
     // trailing workgroups: sigma_s(shift_s lambda_w) for problems without orbital Doppler shift
     const unsigned cb = (unsigned)(((int64_t)n_orb * n_pr + G - 1) / G);
@@ -514,10 +575,10 @@ __global__ void __launch_bounds__(kBlock) k_columns_lanes(const ColArgs ca, int3
     }
   }
   const int lane = threadIdx.x & 63;
-  const int gl = lane & (L - 1);        // lane within the chord's group
-  const int gbase = lane & ~(L - 1);    // the group's first lane in the wavefront
+  const int gl = lane & 7;              // lane within the chord's group
+  const int gbase = lane & ~7;
   const int32_t nc = n_orb * n_pr;
-  const int32_t c = (int32_t)blockIdx.x * G + (int32_t)threadIdx.x / L;
+  const int32_t c = (int32_t)blockIdx.x * G + (int32_t)threadIdx.x / 8;
   const bool valid = c < nc;
   const int32_t o = valid ? c / n_pr : 0;
   const int32_t ip = valid ? c - o * n_pr : 0;
@@ -528,9 +589,16 @@ __global__ void __launch_bounds__(kBlock) k_columns_lanes(const ColArgs ca, int3
     const double dym = y - moon_y[m * n_orb + o];
     blocked = blocked || ((dym * dym + z * z) < moon_R[m] * moon_R[m]);
   }
-  const bool live = valid && !blocked && gl < n_x;
   const int32_t lim = n_x - (n_x % 8);
-  double bound = 0.0, nv = 0.0;
+  const int32_t krem = lim >> 3;        // slot of the remainder samples (lanes 0 .. n_x % 8 - 1)
+  double xs[SPL];
+#pragma unroll
+  for (int k = 0; k < SPL; ++k) {
+    const int32_t i = gl + 8 * k;
+    xs[k] = i < n_x ? x[i] : 0.0;
+  }
+  double bound = 0.0;
+  double nv[SPL];
   int32_t cur_sc = -1;
 #pragma unroll
   for (int32_t t = 0; t < 8; ++t) {
@@ -539,25 +607,46 @@ __global__ void __launch_bounds__(kBlock) k_columns_lanes(const ColArgs ca, int3
     if (td.scenario != cur_sc) {   // one density evaluation per scenario, shared by its constituents
       cur_sc = td.scenario;
       const ScDev sc = ca.sc[cur_sc & 3];
-      nv = 0.0;
-      if (live)
-        nv = sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + gl]
-                    : density_at(sc.m, x[gl], y, z, bx[cur_sc * n_orb + o], by[cur_sc * n_orb + o]);
+      const double bxo = bx[cur_sc * n_orb + o], byo = by[cur_sc * n_orb + o];
+#pragma unroll
+      for (int k = 0; k < SPL; ++k) {
+        const int32_t i = gl + 8 * k;
+        nv[k] = 0.0;
+        if (valid && !blocked && i < n_x)
+          nv[k] = sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + i] : density_at(sc.m, xs[k], y, z, bxo, byo);
+      }
     }
-    const double a = live ? nv * td.chi : 0.0;
+    double av[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) av[k] = (gl + 8 * k < n_x) ? nv[k] * td.chi : 0.0;
     double res;
     if (n_x < 8) {
       res = 0.0;
-      for (int32_t i = 0; i < n_x; ++i) res += __shfl(a, gbase + i, 64);
+      for (int32_t i = 0; i < n_x; ++i) res += __shfl(av[0], gbase + i, 64);
     } else {
-      double r = a;   // lanes gl < 8: numpy's r[gl] = a[gl] + a[gl + 8] + ... (i < lim)
-      for (int32_t i = 8; i < lim; i += 8) r += __shfl(a, (gbase + gl + i) & 63, 64);
-      const double r0 = __shfl(r, gbase + 0, 64), r1 = __shfl(r, gbase + 1, 64);
-      const double r2 = __shfl(r, gbase + 2, 64), r3 = __shfl(r, gbase + 3, 64);
-      const double r4 = __shfl(r, gbase + 4, 64), r5 = __shfl(r, gbase + 5, 64);
-      const double r6 = __shfl(r, gbase + 6, 64), r7 = __shfl(r, gbase + 7, 64);
-      res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-      for (int32_t i = lim; i < n_x; ++i) res += __shfl(a, gbase + i, 64);
+      double r = av[0];
+#pragma unroll
+      for (int k = 1; k < SPL; ++k)
+        if (8 * k < lim) r += av[k];
+      double t1 = dpp_mov<0xB1>(r);        // quad_perm [1,0,3,2]: partner lane ^ 1
+      r = r + t1;
+      t1 = dpp_mov<0x4E>(r);               // quad_perm [2,3,0,1]: partner lane ^ 2
+      r = r + t1;
+      t1 = dpp_mov<0x104>(r);              // row_shl:4: lanes 0-3 (8-11) read 4-7 (12-15)
+      res = r + t1;
+      double rem = 0.0;
+#pragma unroll
+      for (int k = 0; k < SPL; ++k)
+        if (k == krem) rem = av[k];
+      // lane 0 of the group adds the remainder samples lim .. n_x-1 (lanes 0 .. n_x-lim-1) in order
+      const int32_t nrem = n_x - lim;
+      if (nrem > 0) res += rem;
+      if (nrem > 1) res += dpp_mov<0x101>(rem);
+      if (nrem > 2) res += dpp_mov<0x102>(rem);
+      if (nrem > 3) res += dpp_mov<0x103>(rem);
+      if (nrem > 4) res += dpp_mov<0x104>(rem);
+      if (nrem > 5) res += dpp_mov<0x105>(rem);
+      if (nrem > 6) res += dpp_mov<0x106>(rem);
     }
     const double N = blocked ? 0.0 : (0.0 + res) * delta_x;
     if (gl == 0 && valid) ncol[((int64_t)td.slot * n_orb + o) * n_pr + ip] = N;
@@ -805,6 +894,13 @@ constexpr int kWPer = kWinMax / kWBlock;           // sorted positions per threa
 constexpr int kEnvVmax = 8184;                     // bits(1.0) >> 49
 constexpr int kEnvVmin = kEnvVmax - kEnvN + 1;     // X_vmin = 2^-(kEnvN / 8)
 constexpr double kTailEps = 0x1p-10;
+
+// histogram slot of a non-negative envelope value: 1 + (table index of its 1/8-octave bucket), 0 below
+// the table, kEnvN + 1 above it.  v >= X_e  <=>  (bits(v) >> 49) >= kEnvVmin + e.
+__device__ __forceinline__ int32_t env_slot(double v) {
+  const int64_t b = (int64_t)(__builtin_bit_cast(unsigned long long, v) >> 49) - kEnvVmin;
+  return b < 0 ? 0 : (b >= kEnvN ? kEnvN + 1 : (int32_t)b + 1);
+}
 constexpr double kTauSat = 40.0;
 
 template <int NS>
@@ -891,75 +987,6 @@ __device__ __forceinline__ T wg_excl_suffix(T v, Op op, T id, T* wsum) {
   return op(carry, exc);
 }
 
-// ---- wavefront scans on DPP row shifts + cross-row readlanes (no LDS traffic, no bpermute) ----
-template <int CTRL>
-__device__ __forceinline__ double dpp_mov(double v) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
-  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-template <int CTRL>
-__device__ __forceinline__ int32_t dpp_mov(int32_t v) {
-  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
-}
-__device__ __forceinline__ double lane_read(double v, int l) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ int32_t lane_read(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
-
-// inclusive prefix over lanes 0..63 (op applied as op(earlier, later))
-template <typename T, typename Op>
-__device__ __forceinline__ T wave_prefix(T v, Op op) {
-  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
-  T t = dpp_mov<0x111>(v);
-  if (rl >= 1) v = op(t, v);
-  t = dpp_mov<0x112>(v);
-  if (rl >= 2) v = op(t, v);
-  t = dpp_mov<0x114>(v);
-  if (rl >= 4) v = op(t, v);
-  t = dpp_mov<0x118>(v);
-  if (rl >= 8) v = op(t, v);
-  const T r0 = lane_read(v, 15), r1 = lane_read(v, 31), r2 = lane_read(v, 47);
-  const T c01 = op(r0, r1), c012 = op(c01, r2);
-  if (row == 1) v = op(r0, v);
-  else if (row == 2) v = op(c01, v);
-  else if (row == 3) v = op(c012, v);
-  return v;
-}
-// inclusive suffix over lanes 63..0 (op applied as op(earlier, later))
-template <typename T, typename Op>
-__device__ __forceinline__ T wave_suffix(T v, Op op) {
-  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
-  T t = dpp_mov<0x101>(v);
-  if (rl <= 14) v = op(v, t);
-  t = dpp_mov<0x102>(v);
-  if (rl <= 13) v = op(v, t);
-  t = dpp_mov<0x104>(v);
-  if (rl <= 11) v = op(v, t);
-  t = dpp_mov<0x108>(v);
-  if (rl <= 7) v = op(v, t);
-  const T r1 = lane_read(v, 16), r2 = lane_read(v, 32), r3 = lane_read(v, 48);
-  const T c23 = op(r2, r3), c123 = op(r1, c23);
-  if (row == 2) v = op(v, r3);
-  else if (row == 1) v = op(v, c23);
-  else if (row == 0) v = op(v, c123);
-  return v;
-}
-
-// #{i in [0, n) : v[i] >= x} for a non-increasing v
-__device__ __forceinline__ int32_t count_ge(const double* v, int32_t n, double x) {
-  int32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (v[mid] >= x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
 // One workgroup per phase, few dependent steps (2 global round trips, ~8 workgroup barriers for
 // phases with <= 1024 active chords):
 //  1. every thread loads its strided chords (flags, F_out, N_s) -- one round trip per 4096 chords --
@@ -998,10 +1025,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
   constexpr int ST = 1 + NS;
-  __shared__ unsigned long long skey[kWinMax];   // sort keys; after step 4 the B envelope (doubles)
+  __shared__ unsigned long long skey[kWinMax];   // sort keys
   __shared__ double sF[kWinMax];                 // weights of the sorted chords
-  __shared__ double sA[kWinMax];                 // A envelope per record
   __shared__ unsigned char sHead[kWinMax];
+  __shared__ int32_t hB[kEnvN + 2], hA[kEnvN + 2];   // envelope histograms (threshold tables)
   __shared__ int32_t pi_[NW][5];
   __shared__ double pd_[NW][2];
   __shared__ double pm_[NW][K + 2];
@@ -1016,6 +1043,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   for (int s = 0; s < NS; ++s) cs[s] = tabv.t[s].ncoef;
 
   PROM_TS(o * 16 + 0);
+  for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }
   // ---- 1. load, classify, keys, combined scan/reduction
   double fs = 0.0, ts = 0.0;
   int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0;
@@ -1251,7 +1279,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     PROM_TS(o * 16 + 3);
     // ---- 6. records, envelopes, moments (group heads), in the sorted order
     double* mo = mrecs + (int64_t)o * n_pr * ST;
-    double* sB = reinterpret_cast<double*>(skey);   // all key reads are before the barrier above
     double* mm = wmom + (int64_t)o * (n_pr + 1) * K;
     {
       // forward: group ids and A
@@ -1292,8 +1319,12 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         for (int s = 0; s < NS; ++s) r[1 + s] = Nv[k][s];
         if (window) {
           // later members' a are within 2^-40 of the head's: A is widened by 2^-38 to cover them
-          sB[gi] = bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28);
-          sA[gi] = ak[k] * (1.0 - 0x1p-38);
+          // envelopes -> histograms over the threshold-table index (1/8 octave): slot 0 below the
+          // table, slot kEnvN + 1 above it
+          const double Bg = bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28);
+          const double Ag = ak[k] * (1.0 - 0x1p-38);
+          atomicAdd(&hB[env_slot(Bg)], 1);
+          atomicAdd(&hA[env_slot(Ag)], 1);
 #pragma unroll
           for (int m = 0; m < K; ++m) mm[(int64_t)gi * K + m] = M.c[m] * msum[m];
         }
@@ -1303,11 +1334,28 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       if (tid < K) mm[(int64_t)G * K + tid] = 0.0;
       __syncthreads();
       PROM_TS(o * 16 + 4);
+      // tab_t[v] = #{g : B_g >= X_v} = sum of hB over slots >= v + 1 (and likewise tab_h from hA):
+      // one workgroup suffix scan over kEnvN + 2 slots, kEnvN / kWBlock per thread
+      constexpr int PT = kEnvN / kWBlock;
+      int32_t cb[PT], ca_[PT], sb = 0, sa = 0;
+#pragma unroll
+      for (int k = PT - 1; k >= 0; --k) {
+        const int32_t slot = 1 + tid * PT + k;
+        sb += hB[slot]; sa += hA[slot];
+        cb[k] = sb; ca_[k] = sa;
+      }
+      const int32_t bin = wave_suffix<int32_t>(sb, OpAdd()), ain = wave_suffix<int32_t>(sa, OpAdd());
+      int32_t bex = dpp_mov<0x130>(bin), aex = dpp_mov<0x130>(ain);   // wave_shl:1
+      if (lane == 63) { bex = 0; aex = 0; }
+      if (lane == 0) { pi_[wid][0] = bin; pi_[wid][1] = ain; }
+      __syncthreads();
+      int32_t bc = bex + hB[kEnvN + 1], ac = aex + hA[kEnvN + 1];
+      for (int w = NW - 1; w > wid; --w) { bc += pi_[w][0]; ac += pi_[w][1]; }
       int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
-      for (int32_t e = tid; e < kEnvN; e += kWBlock) {
-        const double X = __builtin_bit_cast(double, (unsigned long long)(kEnvVmin + e) << 49);
-        et[e] = count_ge(sB, G, X);
-        et[kEnvN + e] = count_ge(sA, G, X);
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        et[tid * PT + k] = cb[k] + bc;
+        et[kEnvN + tid * PT + k] = ca_[k] + ac;
       }
     }
   }
@@ -1644,7 +1692,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
   // ---- 2.-3. sigma
   double sg[kLPT][NS];
   if constexpr (UNI) {
-    // resampled by the trailing workgroups of k_columns_lanes
+    // resampled by the trailing workgroups of k_columns8
 #pragma unroll
     for (int j = 0; j < kLPT; ++j) {
       const int64_t w = tile + 64 * j + lane;
@@ -1952,9 +2000,9 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
   if (tr.n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4) {
     const unsigned sig_blocks = pre_sigma ? grid_for(tr.n_wav) : 0u;
-#define PROM_COLS(LV, NSV)                                                                               \
-  hipExtLaunchKernelGGL((k_columns_lanes<LV, NSV>),                                                      \
-                     dim3((unsigned)((nc + kBlock / (LV) - 1) / (kBlock / (LV))) + sig_blocks),          \
+#define PROM_COLS(SV, NSV)                                                                               \
+  hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
+                     dim3((unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8)) + sig_blocks),                \
                      dim3(kBlock), 0, s, ev0, nullptr, 0, tr.colargs, tr.n_terms,                         \
                      tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
                      tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
@@ -1962,10 +2010,10 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      tr.moon_R.as<double>(), tr.sigma_max_dev.as<double>(), tr.cull_tau, rs.ncol.as<double>(), \
                      rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>())
 #define PROM_COLS_L(NSV)                       \
-  if (tr.n_x <= 8) PROM_COLS(8, NSV);          \
-  else if (tr.n_x <= 16) PROM_COLS(16, NSV);   \
-  else if (tr.n_x <= 32) PROM_COLS(32, NSV);   \
-  else PROM_COLS(64, NSV);
+  if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
+  else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
+  else if (tr.n_x <= 32) PROM_COLS(4, NSV);    \
+  else PROM_COLS(8, NSV);
     if (!pre_sigma) { PROM_COLS_L(0) }
     else if (na == 1) { PROM_COLS_L(1) }
     else if (na == 2) { PROM_COLS_L(2) }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """In-kernel timing of the transit pipeline (GPU box): builds libprom_hip_trace.so with -DPROM_TRACE,
 runs one configuration and prints workgroup-0 step times of k_chords_w (wall clock, 10 ns ticks)
-and per-wavefront cycle breakdowns of k_tau / k_columns_lanes.
+and per-wavefront cycle breakdowns of k_tau / k_columns8.
 
     python tools/trace_kernels.py [C2]
 """
@@ -69,5 +69,5 @@ print("k_tau per wave lifetime ticks: mean %.0f  p10 %.0f  p50 %.0f  p90 %.0f  m
       % (tot.mean(), *np.percentile(tot, [10, 50, 90, 100]), len(tot)))
 kc = a[600000:600000 + 2 * 100000].reshape(-1, 2)
 kc = kc[kc[:, 1] > 0]
-print("k_columns_lanes per wave lifetime ticks: mean %.0f p50 %.0f p90 %.0f (%d waves)"
+print("k_columns8 per wave lifetime ticks: mean %.0f p50 %.0f p90 %.0f (%d waves)"
       % (kc[:, 0].mean(), np.percentile(kc[:, 0], 50), np.percentile(kc[:, 0], 90), len(kc)))
