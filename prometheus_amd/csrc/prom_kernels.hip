@@ -1006,6 +1006,7 @@ __device__ __forceinline__ T wg_excl_suffix(T v, Op op, T id, T* wsum) {
 // counts[o * kCnt] = {active, transparent, blocked, nonfinite, records, sorted, windowed, 0}.
 constexpr int kLD = kWinMax / kWBlock;              // strided chords per thread and sweep
 constexpr int kRankMax = 2 * kWBlock;               // rank sort up to this many keys
+constexpr int kPayMax = 2048;                       // stage columns in LDS up to this many chords
 
 template <int NS>
 __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ flags,
@@ -1025,8 +1026,12 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
   constexpr int ST = 1 + NS;
-  __shared__ unsigned long long skey[kWinMax];   // sort keys
-  __shared__ double sF[kWinMax];                 // weights of the sorted chords
+  __shared__ unsigned long long skey[kWinMax];   // sort keys: 2^-30 buckets of b, compaction position
+  __shared__ double sF[kWinMax];                 // F_out: by compaction position (payload in LDS) or by
+                                                 // sorted position (columns fetched from HBM)
+  constexpr int PAY = NS >= 4 ? kPayMax / 2 : kPayMax;   // LDS budget (160 KiB)
+  __shared__ double sN[NS][PAY];                 // columns by compaction position (n <= PAY)
+  __shared__ int32_t sIp[kWinMax];               // chord index by compaction position
   __shared__ unsigned char sHead[kWinMax];
   __shared__ int32_t hB[kEnvN + 2], hA[kEnvN + 2];   // envelope histograms (threshold tables)
   __shared__ int32_t pi_[NW][5];
@@ -1107,7 +1112,13 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         b = b < 1.0 ? b : 1.0;   // NaN -> 1.0 (such phases take the unsorted path anyway)
         const unsigned long long d =
             (__builtin_bit_cast(unsigned long long, 1.0) - __builtin_bit_cast(unsigned long long, b)) >> 22;
-        skey[pos] = (d << 24) | (unsigned long long)(sw + tid + k * kWBlock);
+        skey[pos] = (d << 24) | (unsigned long long)pos;
+        sIp[pos] = sw + tid + k * kWBlock;
+        if (pos < PAY) {
+          sF[pos] = fo[k];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) sN[s][pos] = nv[k][s];
+        }
       }
       ++pos;
     }
@@ -1154,19 +1165,26 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       const unsigned long long k0 = has0 ? skey[i0] : ~0ull;
       const unsigned long long k1 = has1 ? skey[i1] : ~0ull;
       int32_t r0 = 0, r1 = 0;
+      // keys past n read as ~0 (never smaller); 16 broadcast loads in flight per step
+      for (int32_t i = n + tid; i < ((n + 15) & ~15); i += kWBlock) skey[i] = ~0ull;
+      __syncthreads();
+      const int32_t n16 = (n + 15) & ~15;
       if (n > kWBlock) {
-        for (int32_t j = 0; j < n; ++j) {
-          const unsigned long long a0 = skey[j];
-          r0 += a0 < k0;
-          r1 += a0 < k1;
+        for (int32_t j = 0; j < n16; j += 16) {
+          unsigned long long a[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) a[q] = skey[j + q];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) { r0 += a[q] < k0; r1 += a[q] < k1; }
         }
       } else if (__builtin_amdgcn_readfirstlane(tid) < n) {
-        int32_t j = 0;
-        for (; j + 4 <= n; j += 4) {
-          const unsigned long long a0 = skey[j], a1 = skey[j + 1], a2 = skey[j + 2], a3 = skey[j + 3];
-          r0 += (a0 < k0) + (a1 < k0) + (a2 < k0) + (a3 < k0);
+        for (int32_t j = 0; j < n16; j += 16) {
+          unsigned long long a[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) a[q] = skey[j + q];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) r0 += a[q] < k0;
         }
-        for (; j < n; ++j) r0 += skey[j] < k0;
       }
       __syncthreads();
       if (has0) skey[r0] = k0;
@@ -1197,17 +1215,34 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     const int32_t cnt = min(n, i0 + per) - i0;
     double Nv[kWPer][NS], Fv[kWPer], bv[kWPer], av[kWPer];
     double Np[NS];
+    const bool lds_pay = n <= PAY;   // columns and F_out staged in LDS at compaction
     {
-      const int32_t ipp = i0 > 0 ? (int32_t)(skey[i0 - 1] & 0xffffffull) : 0;
+      const int32_t pp = i0 > 0 ? (int32_t)(skey[i0 - 1] & 0xffffffull) : 0;
+      if (lds_pay) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) Np[s] = (i0 > 0 && cnt > 0) ? nc0[s * nstride + ipp] : 0.0;
+        for (int s = 0; s < NS; ++s) Np[s] = (i0 > 0 && cnt > 0) ? sN[s][pp] : 0.0;
+      } else {
+        const int32_t ipp = sIp[pp];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) Np[s] = (i0 > 0 && cnt > 0) ? nc0[s * nstride + ipp] : 0.0;
+      }
     }
+    if (lds_pay) {
 #pragma unroll
-    for (int k = 0; k < kWPer; ++k) {
-      const int32_t ip = k < cnt ? (int32_t)(skey[i0 + k] & 0xffffffull) : 0;
-      Fv[k] = k < cnt ? fout[ip] : 0.0;
+      for (int k = 0; k < kWPer; ++k) {
+        const int32_t pk = k < cnt ? (int32_t)(skey[i0 + k] & 0xffffffull) : 0;
+        Fv[k] = k < cnt ? sF[pk] : 0.0;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) Nv[k][s] = k < cnt ? nc0[s * nstride + ip] : 0.0;
+        for (int s = 0; s < NS; ++s) Nv[k][s] = k < cnt ? sN[s][pk] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kWPer; ++k) {
+        const int32_t ip = k < cnt ? sIp[(int32_t)(skey[i0 + k] & 0xffffffull)] : 0;
+        Fv[k] = k < cnt ? fout[ip] : 0.0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) Nv[k][s] = k < cnt ? nc0[s * nstride + ip] : 0.0;
+      }
     }
     uint32_t headbits = 0;
     int32_t nheads = 0;
@@ -1231,7 +1266,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
       }
       Fv[k] = Fv[k] / fs;
-      sF[i0 + k] = Fv[k];
+      if (!lds_pay) sF[i0 + k] = Fv[k];   // (payload path: sF already holds F_out by position)
       sHead[i0 + k] = head ? 1 : 0;
       if (head) { headbits |= 1u << k; ++nheads; }
       bmax = bv[k] > bmax ? bv[k] : bmax;
@@ -1312,7 +1347,11 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         const int32_t gi = gk[k];
         const int32_t i = i0 + k;
         double F = Fv[k];
-        for (int32_t j = i + 1; j < n && !sHead[j]; ++j) F += sF[j];
+        if (lds_pay) {
+          for (int32_t j = i + 1; j < n && !sHead[j]; ++j) F += sF[(int32_t)(skey[j] & 0xffffffull)] / fs;
+        } else {
+          for (int32_t j = i + 1; j < n && !sHead[j]; ++j) F += sF[j];
+        }
         double* r = mo + (int64_t)gi * ST;
         r[0] = F;
 #pragma unroll
