@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PROM_ABI_VERSION 1
+#define PROM_ABI_VERSION 2
 
 typedef struct prom_ctx prom_ctx;
 
@@ -155,6 +155,16 @@ typedef struct prom_transit_problem {
   int32_t reserved2;
   double k_B;                  /* Boltzmann constant for P = n k_B T of molecular lookups
                                   (<= 0: the reference's 1.381e-16, constants.py:17)          */
+  /* Stellar spectrum (gasProperties.py:1180-1219): with has_star != 0 the flux of chord c at
+   * wavelength w is F = rho_c * (F_star(lambda_w / s_c) * clv_c), F_star(t) = 10^interp(t, star
+   * table) (n_interp_log with offset 0, :34-51) and s_c = calculateDopplerShift(vsini rho_c / R_star
+   * cos(phi_c - phi_rot)) (the Rossiter-McLaughlin shift, :1183-1184); chord_fout is then unused.
+   * has_star == 0 keeps the flat star (F_star = 1, :1210-1211).  Atomic constituents only. */
+  int32_t has_star;
+  int32_t star_table;          /* table id (prom_table_upload of Fstar_function.x, .y; offset 0) */
+  const double* chord_rho;     /* [n_pr] rho                                                  */
+  const double* chord_clv;     /* [n_pr] 1 - u1 (1 - mu) - u2 (1 - mu)^2                       */
+  const double* chord_star_shift;  /* [n_pr] s_c                                              */
 } prom_transit_problem;
 
 /* prom_transit_problem.options */

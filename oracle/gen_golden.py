@@ -156,6 +156,32 @@ def gen_transits():
               orbphase=sgrid.constructOrbphaseAxis(), config=np.array(json.dumps(cfg)), **tables)
 
 
+def gen_stars():
+    """Stellar-spectrum fixtures (gasProperties.py:1180-1219): CLV + RM rotation + a synthetic
+    spectrum installed as the reference's interp1d Fstar_function (celestialBodies.py:223-235)."""
+    from scipy.interpolate import interp1d
+    from oracle.prom_oracle import synthetic_star_spectrum
+    cfgs = configs.star_fixture_configs()
+    for name, (cname, star) in configs.STAR_FIXTURES.items():
+        cfg = cfgs[cname]
+        tr, lst, sgrid = reference_transit(cfg)
+        hs = tr.planet.hostStar
+        g = cfg["Grids"]
+        x, F = synthetic_star_spectrum(g["lower_w"], g["upper_w"])
+        hs.addCLVparameters(star["u1"], star["u2"])
+        hs.addRMparameters(star["vsini"], star["phi_rot"])
+        hs.Fstar_function = interp1d(x, np.log10(F))
+        try:
+            R = tr.sumOverChords(max_memory_gb=2.0)
+        finally:
+            hs.addCLVparameters(0., 0.)
+            hs.addRMparameters(0., 0.)
+            hs.Fstar_function = None
+        _save(name, R=R, wavelength=tr.wavelength, orbphase=sgrid.constructOrbphaseAxis(),
+              config=np.array(json.dumps(cfg)), star=np.array(json.dumps(star)),
+              fstar_sha=np.array(_sha(np.concatenate([x, np.log10(F)]))))
+
+
 def gen_wavelength_grids():
     """Full-size lambda grids C1..C5 (hash + samples; C1 stored whole)."""
     out = {}
@@ -276,7 +302,7 @@ def gen_molecular_kat():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["interp", "tables", "density", "grids", "molecular", "transits"]
+    which = sys.argv[1:] or ["interp", "tables", "density", "grids", "molecular", "transits", "stars"]
     if "interp" in which:
         gen_interp_kats()
     if "tables" in which:
@@ -289,3 +315,5 @@ if __name__ == "__main__":
         gen_molecular_kat()
     if "transits" in which:
         gen_transits()
+    if "stars" in which:
+        gen_stars()

@@ -206,6 +206,10 @@ class Body:
     star_M: float = 0.0
     clv_u1: float = 0.0
     clv_u2: float = 0.0
+    # host star rotation and spectrum (celestialBodies.py:86-95; Fstar_function's .x / .y)
+    vsini: float = 0.0
+    phi_rot: float = 0.0
+    fstar: Optional[tuple] = None
     # moon only
     host: Optional["Body"] = None
     orbphase0: float = 0.0
@@ -415,6 +419,8 @@ def transit_depth(scenarios, doppler, grid, wav, tables, max_memory_gb=2.0,
     orb_idx = np.abs(orb[:, None] - orbphase_axis(grid)).argmin(axis=1)
     mu = np.sqrt(np.clip(1. - rho ** 2 / planet.star_R ** 2, 0, 1))
     clv = 1. - planet.clv_u1 * (1. - mu) - planet.clv_u2 * (1. - mu) ** 2
+    # gasProperties.py:1183-1184
+    star_shifts = doppler_shift(planet.vsini * rho / planet.star_R * np.cos(phi - planet.phi_rot))
     molecular = any("molecule" in c for s in scenarios for c in s.constituents)
     x = x_axis(grid)
     B = chunk_size(len(cg), n_wav, len(x), max_memory_gb, molecular)
@@ -423,7 +429,10 @@ def transit_depth(scenarios, doppler, grid, wav, tables, max_memory_gb=2.0,
     Fout = np.zeros((n_orb, n_wav))
     for i in range(0, len(cg), B):
         s = slice(i, i + B)
-        Fstar = np.ones((len(phi[s]), n_wav))
+        if planet.fstar is None:                       # gasProperties.py:1210-1211
+            Fstar = np.ones((len(phi[s]), n_wav))
+        else:                                          # :1212-1219
+            Fstar = interp_log(wav[None, :] / star_shifts[s, None], planet.fstar[0], planet.fstar[1], 0.0)
         Fstar *= clv[s, None]
         blocked = np.sqrt((y[s] - planet.a * np.sin(orb[s])) ** 2 + z[s] ** 2) < planet.R
         for sc in scenarios:
@@ -531,9 +540,38 @@ def from_setup(cfg: dict, molecular_tables: Optional[dict] = None):
     return out, bool(cfg["Fundamentals"]["DopplerOrbitalMotion"]), grids
 
 
-def run_setup(cfg: dict, molecular_tables: Optional[dict] = None, max_memory_gb=2.0):
-    """prometheus.py:131-143 equivalent: returns (wavelength, orbphase, R)."""
+def apply_star(planet: Body, star: Optional[dict]) -> None:
+    """Star.addCLVparameters / addRMparameters / Fstar_function (celestialBodies.py:76-95, :223-235):
+    ``star`` = {"u1", "u2", "vsini", "phi_rot", "fstar": (x, log10 F) or None}."""
+    if not star:
+        return
+    planet.clv_u1, planet.clv_u2 = star.get("u1", 0.0), star.get("u2", 0.0)
+    planet.vsini, planet.phi_rot = star.get("vsini", 0.0), star.get("phi_rot", 0.0)
+    planet.fstar = star.get("fstar")
+
+
+def synthetic_star_spectrum(lower_w, upper_w, step=1e-10, margin=3e-8, seed=7):
+    """Seeded stand-in for a PHOENIX HiRes slice (the reference fetches it over FTP,
+    celestialBodies.py:128-209; no network here): x = arange(lower_w - margin, upper_w + margin, step)
+    [cm], F = continuum with a 10 % slope times one Gaussian absorption line per 2 A (depth 5-90 %,
+    sigma 0.05-0.4 A) -> (x, F).  Same formula as prometheus_amd.configs.synthetic_star_spectrum."""
+    rng = np.random.default_rng(seed)
+    x = np.arange(lower_w - margin, upper_w + margin, step)
+    n_lines = max(4, int((x[-1] - x[0]) / 2e-8))
+    centre = rng.uniform(x[0], x[-1], n_lines)
+    depth = rng.uniform(0.05, 0.9, n_lines)
+    width = rng.uniform(0.05e-8, 0.4e-8, n_lines)
+    F = 2e14 * (1. + 0.1 * (x - x[0]) / (x[-1] - x[0]))
+    for c, d, w in zip(centre, depth, width):
+        a, b = np.searchsorted(x, [c - 8. * w, c + 8. * w])
+        F[a:b] *= 1. - d * np.exp(-0.5 * ((x[a:b] - c) / w) ** 2)
+    return x, F
+
+
+def run_setup(cfg: dict, molecular_tables: Optional[dict] = None, max_memory_gb=2.0, star=None):
+    """prometheus.py:131-143 equivalent: returns (wavelength, orbphase, R).  ``star``: apply_star."""
     scen, doppler, grids = from_setup(cfg, molecular_tables)
+    apply_star(scen[0].planet, star)
     tabs = build_tables(scen, grids)
     wav = simulation_wavelengths(grids, atomic_species(scen))
     R = transit_depth(scen, doppler, grids, wav, tabs, max_memory_gb)

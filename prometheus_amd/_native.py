@@ -58,9 +58,11 @@ class TransitProblem(C.Structure):
                 ("planet_R", C.c_double), ("n_moons", C.c_int32), ("reserved", C.c_int32),
                 ("moon_y", _dp), ("moon_R", _dp), ("scenarios", C.POINTER(Scenario)),
                 ("cull_tau", C.c_double), ("options", C.c_int32), ("reserved2", C.c_int32),
-                ("k_B", C.c_double)]
+                ("k_B", C.c_double), ("has_star", C.c_int32), ("star_table", C.c_int32),
+                ("chord_rho", _dp), ("chord_clv", _dp), ("chord_star_shift", _dp)]
 
 
+ABI_VERSION = 2
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
 OPT_NO_WINDOW = 4
@@ -127,7 +129,7 @@ def load_library(path: Optional[str] = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.prom_abi_version() != 1:
+        if lib.prom_abi_version() != ABI_VERSION:
             raise NativeUnavailable("ABI version mismatch")
         if path is None:
             _lib = lib
@@ -285,7 +287,7 @@ class TransitInputs:
     """Owns the numpy arrays behind one prom_transit_problem (kept alive while in use)."""
 
     def __init__(self, *, wavelength, chord_y, chord_z, chord_fout, n_orb, x, delta_x, planet_y, planet_R,
-                 moon_y, moon_R, scenarios, cull_tau=0.0, options=0, k_B=0.0):
+                 moon_y, moon_R, scenarios, cull_tau=0.0, options=0, k_B=0.0, star=None):
         keep = []
 
         def arr(a):
@@ -335,6 +337,11 @@ class TransitInputs:
         s.cull_tau = float(cull_tau)
         s.options = int(options)
         s.k_B = float(k_B)
+        if star is not None:
+            # {"table_id", "rho", "clv", "shift"}: stellar spectrum path (prom_hip.h has_star)
+            s.has_star, s.star_table = 1, int(star["table_id"])
+            s.chord_rho, s.chord_clv = _d(arr(star["rho"])), _d(arr(star["clv"]))
+            s.chord_star_shift = _d(arr(star["shift"]))
         self.struct = s
         self.keepalive = keep
         self.n_atoms = n_atoms

@@ -49,11 +49,30 @@ class Star:
 
     def getSpectrum(self):
         raise NotImplementedError("PHOENIX spectra are fetched over FTP by the reference "
-                                  "(celestialBodies.py:128-209); this build has no network and does not "
-                                  "ship them (out of scope, SURVEY.md §8f rank 2)")
+                                  "(celestialBodies.py:128-209); this build has no network: provide the "
+                                  "spectrum with addFstarSpectrum(wavelength, flux) or set Fstar_function")
 
     def addFstarFunction(self, wavelength) -> None:
         self.getSpectrum()
+
+    def addFstarSpectrum(self, wavelength, flux) -> None:
+        """Fstar_function from a spectrum already at hand: the reference keeps
+        interp1d(w_starSEL, log10(F_0)) (celestialBodies.py:223-235) and reads only its .x / .y
+        (gasProperties.py:1212-1219); wavelength [cm] ascending, flux > 0 in any unit (R is a ratio)."""
+        w = np.asarray(wavelength, dtype=np.float64)
+        order = np.argsort(w, kind="mergesort")   # interp1d sorts its x the same way
+        self.Fstar_function = StellarSpectrum(w[order], np.log10(np.asarray(flux, dtype=np.float64))[order])
+
+
+class StellarSpectrum:
+    """(x, y = log10 F) pair standing in for the reference's interp1d (only .x and .y are read)."""
+
+    def __init__(self, x, y) -> None:
+        self.x = np.ascontiguousarray(x, dtype=np.float64)
+        self.y = np.ascontiguousarray(y, dtype=np.float64)
+
+    def __call__(self, w):
+        return np.interp(w, self.x, self.y)
 
 
 class Planet:

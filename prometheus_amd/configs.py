@@ -155,3 +155,40 @@ def synthetic_molecular_table(n_p=22, n_t=27, n_nu=50001, nu_lo=5000., nu_hi=100
     return {"p": np.logspace(-1, 8, n_p), "t": np.linspace(100., 3400., n_t),
             "bin_edges": np.linspace(nu_lo, nu_hi, n_nu),
             "xsecarr": 1e-22 * np.exp(rng.standard_normal((n_p, n_t, n_nu)))}
+
+
+def synthetic_star_spectrum(lower_w, upper_w, step=1e-10, margin=3e-8, seed=7):
+    """Seeded stand-in for a PHOENIX HiRes slice (celestialBodies.py:128-209 fetch it over FTP; no
+    network here): x = arange(lower_w - margin, upper_w + margin, step) [cm], F = continuum with a
+    10 % slope times one Gaussian absorption line per 2 A (depth 5-90 %, sigma 0.05-0.4 A).
+    Returns (x, F); Star.addFstarSpectrum(x, F) installs it."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    x = np.arange(lower_w - margin, upper_w + margin, step)
+    n_lines = max(4, int((x[-1] - x[0]) / 2e-8))
+    centre = rng.uniform(x[0], x[-1], n_lines)
+    depth = rng.uniform(0.05, 0.9, n_lines)
+    width = rng.uniform(0.05e-8, 0.4e-8, n_lines)
+    F = 2e14 * (1. + 0.1 * (x - x[0]) / (x[-1] - x[0]))
+    for c, d, w in zip(centre, depth, width):
+        a, b = np.searchsorted(x, [c - 8. * w, c + 8. * w])
+        F[a:b] *= 1. - d * np.exp(-0.5 * ((x[a:b] - c) / w) ** 2)
+    return x, F
+
+
+# stellar-spectrum fixtures: CLV (mainRetrieval.py:38 coefficients), RM rotation, synthetic spectrum
+STAR_FIXTURES = {
+    "rm_C1": ("C1", {"u1": 0.34, "u2": 0.28, "vsini": 0.0, "phi_rot": 0.0}),
+    "rm_C2r": ("C2rs", {"u1": 0.34, "u2": 0.28, "vsini": 5e6, "phi_rot": 0.4}),
+    "rm_exomoon": ("exomoon_s", {"u1": 0.0, "u2": 0.0, "vsini": 3e6, "phi_rot": -1.1}),
+}
+
+
+def star_fixture_configs():
+    """Setup dicts of the stellar-spectrum fixtures (tests/golden/rm_*.npz)."""
+    return {
+        "C1": c1(),
+        "C2rs": reduced(c2(), orbphase_steps=4, res_low=5e-9, res_high=1e-10, lower_w=5884e-8, upper_w=5900e-8),
+        "exomoon_s": reduced(exomoon(), orbphase_steps=3, res_low=2e-9, res_high=5e-11, lower_w=5886e-8,
+                             upper_w=5898e-8),
+    }

@@ -129,6 +129,7 @@ static void build_directory(prom_ctx* ctx, prom::AtomTable& t, const double* x, 
     d[j] = (int32_t)(std::upper_bound(x, x + n, b) - x);
   }
   upload(t.dir, d.data(), nd + 1, ctx->stream);
+  t.hx.assign(x, x + n);
   t.n_dir = (int32_t)nd;
   t.dir_x0 = x0;
   t.dir_inv_h = span > 0.0 ? 1.0 / h : 0.0;
@@ -436,6 +437,60 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       tr.sigtab_v = prom::SigTabs4{};
       for (size_t i = 0; i < st.size() && i < 4; ++i) tr.sigtab_v.t[i] = st[i];
     }
+    tr.star = pb->has_star != 0;
+    if (tr.star) {
+      // stellar spectrum: chord arrays, the F_star table and, per wavelength tile of the tau kernel, the
+      // slice of table nodes its targets lambda / s_c can reach: s in [s_min, s_max] and IEEE division
+      // is monotone, so fl(lambda / s) lies in [fl(lambda_min / s_max), fl(lambda_max / s_min)]
+      PROM_REQUIRE(pb->chord_rho && pb->chord_clv && pb->chord_star_shift, "transit: stellar chord arrays missing");
+      PROM_REQUIRE(pb->star_table >= 0 && pb->star_table < (int32_t)ctx->tables.size(), "transit: unknown star table id");
+      PROM_REQUIRE(n_mol == 0 && n_atoms <= 8,
+                   "transit: the stellar-spectrum path takes <= 8 atomic constituents and no molecules");
+      const prom::AtomTable& sb = ctx->tables[pb->star_table];
+      tr.star_tab = prom::SigTabDev{sb.x.as<double>(), sb.y.as<double>(), sb.n, sb.offset, nullptr,
+                                    sb.dir.as<int32_t>(), sb.n_dir, 0, sb.dir_x0, sb.dir_inv_h, 0.0, 0.0};
+      upload(tr.crho, pb->chord_rho, tr.n_pr, s);
+      upload(tr.cclv, pb->chord_clv, tr.n_pr, s);
+      upload(tr.cshift, pb->chord_star_shift, tr.n_pr, s);
+      double smin = INFINITY, smax = -INFINITY;
+      bool ok = sb.n >= 2 && (int64_t)sb.hx.size() == sb.n;
+      for (int32_t i = 0; i < tr.n_pr; ++i) {
+        const double v = pb->chord_star_shift[i];
+        if (!(v > 0.0) || !std::isfinite(v)) ok = false;
+        smin = std::min(smin, v);
+        smax = std::max(smax, v);
+      }
+      const int64_t n_tiles = (tr.n_wav + 255) / 256;
+      std::vector<int32_t> sl(3 * n_tiles, 0);
+      const std::vector<double>& X = sb.hx;
+      const int64_t n = sb.n;
+      auto bracket = [&](double t) -> int64_t {   // numpy's j: largest j <= n-2 with X[j] <= t (0 below)
+        int64_t j = (int64_t)(std::upper_bound(X.begin(), X.end(), t) - X.begin()) - 1;
+        return j < 0 ? 0 : (j > n - 2 ? n - 2 : j);
+      };
+      for (int64_t tl = 0; ok && tl < n_tiles; ++tl) {
+        double lmin = INFINITY, lmax = -INFINITY;
+        bool fin = true;
+        for (int64_t w = tl * 256; w < std::min<int64_t>(tr.n_wav, (tl + 1) * 256); ++w) {
+          const double l = pb->wavelength[w];
+          if (!std::isfinite(l)) fin = false;
+          lmin = std::min(lmin, l);
+          lmax = std::max(lmax, l);
+        }
+        if (!fin) continue;
+        const double tlo = lmin / smax, thi = lmax / smin;
+        const int64_t lo = bracket(tlo);
+        const int64_t hi = thi >= X[n - 1] ? n - 1 : bracket(thi) + 1;
+        const int64_t m = hi - lo + 1;
+        if (m < 2 || m > prom::kRmStarMax) continue;   // global lookups for this tile
+        int32_t P = 1;
+        while (P < m) P <<= 1;
+        sl[3 * tl] = (int32_t)lo;
+        sl[3 * tl + 1] = (int32_t)m;
+        sl[3 * tl + 2] = P / 2;
+      }
+      upload(tr.rm_slices, sl.data(), (int64_t)sl.size(), s);
+    }
     tr.tab.ensure(sizeof(double) * std::max<int64_t>(tab_total, 1));
     {
       std::vector<prom::ScDevHost> sd(tr.n_sc);
@@ -455,7 +510,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     // work buffers
     const int64_t nc = n_orb * tr.n_pr;
     tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
-    const bool fast = tr.exp_mode && n_mol == 0 && n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && tr.window;
+    const bool fast = tr.exp_mode && n_mol == 0 && n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && tr.window &&
+                      !tr.star;
     tr.depth = fast ? ctx->pipeline : 1;
     for (int si = 0; si < tr.depth; ++si) {
     prom::RunSlot& rs = tr.slot[si];
@@ -545,7 +601,7 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
         stats->tau_records += recs;
         if (exact) stats->tau_kernel_variant_exact_phases += 1;
         // the device counters cover the non-exact phases of the atomic fast kernel
-        if (exact || tr.n_mol > 0 || !tr.exp_mode || tr.n_atoms > prom::kWinMaxSpecies) unwindowed += recs;
+        if (exact || tr.n_mol > 0 || !tr.exp_mode || tr.n_atoms > prom::kWinMaxSpecies || tr.star) unwindowed += recs;
       }
       for (int i = 0; i < 64; ++i) counted += (int64_t)ev64[i];
       stats->chord_lambda_evals = stats->active_chords * tr.n_wav;

@@ -67,6 +67,9 @@ constexpr int kEnvN = 2048;
 constexpr int kWinMaxSpecies = 4;
 inline int n_tail_moments(int S) { return (S + 1) * (S + 2) * (S + 3) / 6; }
 
+// Stellar-spectrum path: star-table nodes a tau workgroup stages in LDS (prom_api.hip rm_slices).
+constexpr int kRmStarMax = 1024;
+
 // Device-side view of one density model (the prom_density_model scalars).
 struct DensityDev {
   int32_t kind;
@@ -141,6 +144,7 @@ struct AtomTable {
   // bucket directory for O(1) bracketing: dir[j] = #{i : x[i] <= x0 + j h}, j = 0 .. n_dir,
   // h = (x[n-1] - x0) / n_dir (prom_api.hip build_directory)
   DevBuf dir;
+  std::vector<double> hx;   // host copy of x (stellar-spectrum slice bounds)
   int32_t n_dir = 0;
   double dir_x0 = 0.0, dir_inv_h = 0.0;
 };
@@ -210,6 +214,11 @@ struct TransitDev {
   DevBuf mol_na;                            // [n_mol][n_orb][n_pr][n_x] n_abs = n chi
   std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
+  // stellar spectrum (prom_transit_problem.has_star)
+  bool star = false;
+  SigTabDev star_tab{};                     // the F_star table (x, log10 F, offset 0; shift unused)
+  DevBuf crho, cclv, cshift;                // [n_pr]
+  DevBuf rm_slices;                         // [n_wav tiles of kBlock][3] {lo, m, half}: LDS slice
   RunSlot slot[kMaxSlots];
   int depth = 1;                            // slots in use: fast path = pipeline depth, else 1
   int last = 0;                             // slot of the most recent run

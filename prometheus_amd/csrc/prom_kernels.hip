@@ -2022,13 +2022,181 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
   }
 }
 
+// ---- stellar spectrum path (gasProperties.py:1180-1219 with Fstar_function set) ----------------------
+// F(c, w) = rho_c * (F_star(lambda_w / s_c) * clv_c) differs per chord AND wavelength (the Rossiter-
+// McLaughlin shift s_c moves the stellar lines across the disk), so neither the flat-star F_out
+// factorisation nor the windowed tail moments apply: every (chord, phase, wavelength) term is
+// evaluated, in chord order, as in the reference.  One thread per wavelength, kRmP phases per
+// workgroup; F is computed once per (chord, wavelength) and shared by the workgroup's phases, and the
+// phase-independent F_out sum is accumulated beside them.  F_star's np.interp bracket is searched in
+// an LDS copy of the star-table slice that the workgroup's targets lambda / s can reach (prom_api.hip
+// rm_slices), or in global memory (sigma_of's directory) when that slice exceeds kRmStarMax nodes.
+constexpr int kRmP = 8;            // phases per workgroup
+constexpr int kRmChunk = 64;       // chords staged in LDS per sweep
+constexpr int kRmGroup = 4;        // chords whose bracket searches are interleaved
+
+template <int NSMAX, bool OCML>
+__global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__ tabs, int32_t na,
+                                                   const SigTabDev star, const int32_t* __restrict__ slices,
+                                                   const double* __restrict__ wav, int64_t n_wav,
+                                                   const double* __restrict__ crho,
+                                                   const double* __restrict__ cclv,
+                                                   const double* __restrict__ cshift,
+                                                   const int32_t* __restrict__ flags,
+                                                   const double* __restrict__ ncol, int32_t n_pr,
+                                                   int32_t n_orb, int32_t* __restrict__ counts,
+                                                   double* __restrict__ R) {
+  __shared__ double sexp[256];
+  __shared__ double sx[kRmStarMax], sy[kRmStarMax], ssl[kRmStarMax];
+  __shared__ double sRho[kRmChunk], sClv[kRmChunk], sSh[kRmChunk];
+  __shared__ double sN[kRmP * NSMAX * kRmChunk];
+  __shared__ int32_t sFl[kRmP * kRmChunk];
+  __shared__ int32_t scnt[kRmP * 3];
+  sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
+  const int32_t o0 = blockIdx.y * kRmP;
+  const int32_t np = n_orb - o0 < kRmP ? n_orb - o0 : kRmP;
+  const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = w < n_wav;
+  const double lam = wav[live ? w : n_wav - 1];
+  // chord counts per phase (stats), by the first workgroup of each phase group
+  if (blockIdx.x == 0 && counts) {
+    if (threadIdx.x < kRmP * 3) scnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (int p = 0; p < np; ++p)
+      for (int32_t i = threadIdx.x; i < n_pr; i += kBlock) {
+        const int32_t f = flags[(int64_t)(o0 + p) * n_pr + i];
+        atomicAdd(&scnt[p * 3 + (f < 0 ? 0 : (f > 2 ? 2 : f))], 1);
+      }
+    __syncthreads();
+    if (threadIdx.x < np) {
+      int32_t* cp = counts + (int64_t)(o0 + threadIdx.x) * kCnt;
+      cp[0] = scnt[threadIdx.x * 3];
+      cp[1] = scnt[threadIdx.x * 3 + 1];
+      cp[2] = scnt[threadIdx.x * 3 + 2];
+      for (int k = 3; k < kCnt; ++k) cp[k] = 0;
+    }
+  }
+  // star-table slice {lo, m, half}: nodes lo .. lo+m-1 staged, padded with +inf up to 2 * half
+  const int32_t* sl = slices + 3 * (int64_t)blockIdx.x;
+  const int64_t lo = sl[0];
+  const int32_t m = sl[1], half = sl[2];
+  if (m > 0) {
+    for (int i = threadIdx.x; i < 2 * half; i += kBlock) {
+      if (i < m) {
+        const double x0 = star.x[lo + i], f0 = star.y[lo + i];
+        sx[i] = x0;
+        sy[i] = f0;
+        ssl[i] = i + 1 < m ? (star.y[lo + i + 1] - f0) / (star.x[lo + i + 1] - x0) : 0.0;
+      } else {
+        sx[i] = __builtin_inf();
+      }
+    }
+  }
+  // sigma_s at each of this thread's phases (shift_o * lambda, as getLOSopticalDepth_Batch)
+  double sg[kRmP][NSMAX];
+#pragma unroll
+  for (int p = 0; p < kRmP; ++p)
+#pragma unroll
+    for (int s = 0; s < NSMAX; ++s)
+      sg[p][s] = (p < np && s < na) ? sigma_of(tabs[s].shift[o0 + p] * lam, tabs[s]) : 0.0;
+  double in[kRmP];
+#pragma unroll
+  for (int p = 0; p < kRmP; ++p) in[p] = 0.0;
+  double out = 0.0;
+  for (int32_t c0 = 0; c0 < n_pr; c0 += kRmChunk) {
+    const int nch = n_pr - c0 < kRmChunk ? n_pr - c0 : kRmChunk;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nch; i += kBlock) {
+      sRho[i] = crho[c0 + i];
+      sClv[i] = cclv[c0 + i];
+      sSh[i] = cshift[c0 + i];
+    }
+    for (int i = threadIdx.x; i < np * nch; i += kBlock) {
+      const int p = i / nch, c = i - p * nch;
+      sFl[p * kRmChunk + c] = flags[(int64_t)(o0 + p) * n_pr + c0 + c];
+    }
+    for (int i = threadIdx.x; i < na * np * nch; i += kBlock) {
+      const int sp = i / nch, c = i - sp * nch;     // sp = s * np + p
+      const int s = sp / np, p = sp - s * np;
+      sN[(p * NSMAX + s) * kRmChunk + c] = ncol[((int64_t)s * n_orb + o0 + p) * n_pr + c0 + c];
+    }
+    __syncthreads();
+    for (int cg = 0; cg < nch; cg += kRmGroup) {
+      double F[kRmGroup];
+      if (m > 0) {
+        double t[kRmGroup];
+        int pos[kRmGroup];
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) {
+          t[u] = lam / sSh[cg + u < nch ? cg + u : nch - 1];
+          pos[u] = 0;
+        }
+        for (int st = half; st > 0; st >>= 1) {
+#pragma unroll
+          for (int u = 0; u < kRmGroup; ++u) pos[u] += sx[pos[u] + st] <= t[u] ? st : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) {
+          // numpy.interp on the slice: below node 0 only when lo == 0 (fp[0]); at or beyond the last
+          // staged node only when it is the table's last (fp[n-1]); else sx[pos] <= t < sx[pos + 1]
+          const double tu = t[u];
+          const int k = pos[u];
+          double v;
+          if (tu != tu) v = tu;
+          else if (!(tu >= sx[0])) v = sy[0];
+          else if (tu >= sx[m - 1]) v = sy[m - 1];
+          else if (sx[k] == tu) v = sy[k];
+          else {
+            v = ssl[k] * (tu - sx[k]) + sy[k];
+            if (v != v) {
+              v = ssl[k] * (tu - sx[k + 1]) + sy[k + 1];
+              if (v != v && sy[k] == sy[k + 1]) v = sy[k];
+            }
+          }
+          F[u] = exp10(v) - star.offset;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) F[u] = sigma_of(lam / sSh[cg + u < nch ? cg + u : nch - 1], star);
+      }
+#pragma unroll
+      for (int u = 0; u < kRmGroup; ++u) {
+        const int c = cg + u;
+        if (c >= nch) break;
+        const double Fc = sRho[c] * (F[u] * sClv[c]);
+        out += Fc;
+#pragma unroll
+        for (int p = 0; p < kRmP; ++p) {
+          if (p >= np) break;
+          const int32_t fl = sFl[p * kRmChunk + c];
+          if (fl == 1) {
+            in[p] += Fc;                       // transparent: exp(-tau) == 1 to the last ulp
+          } else if (fl == 0) {
+            double tau = 0.0;
+#pragma unroll
+            for (int s = 0; s < NSMAX; ++s)
+              if (s < na) tau += sN[(p * NSMAX + s) * kRmChunk + c] * sg[p][s];
+            if (OCML || !(tau < 700.0 && tau > -700.0)) in[p] += Fc * exp(-tau);
+            else in[p] = acc_exp256(in[p], Fc, tau * kM256Ln2, sexp);
+          }
+        }
+      }
+    }
+  }
+  if (live) {
+#pragma unroll
+    for (int p = 0; p < kRmP; ++p)
+      if (p < np) R[(int64_t)(o0 + p) * n_wav + w] = in[p] / out;
+  }
+}
+
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;
   const bool wpath = tr.exp_mode && tr.n_mol == 0 && tr.n_atoms >= 1 && tr.n_atoms <= kWinMaxSpecies;
   // no orbital Doppler shift: sigma_s(lambda_w) is resampled once per wavelength by extra workgroups
   // of the column kernel (they run beside the chord work) instead of once per phase group
-  const bool pre_sigma = wpath && tr.window && tr.uniform_shift;
+  const bool pre_sigma = wpath && tr.window && tr.uniform_shift && !tr.star;
   const int32_t na = tr.n_atoms;
   *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? (wpath && tr.window ? 20 : 10) : 0);
   // stage events ride on the fast path's dispatch packets (hipExtLaunchKernelGGL start/stop events):
@@ -2089,6 +2257,30 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                        tr.sigma_max_dev.as<double>(), mol_max, tr.cull_tau, rs.ncol.as<double>(),
                        tr.molcol.as<double>(), rs.flags.as<int32_t>());
     PROM_HIP(hipGetLastError());
+  }
+  if (tr.star) {
+    // 2'. stellar spectrum: one exact chord-order kernel over the flags / columns
+    if (ev1) PROM_HIP(hipEventRecord(ev1, s));
+    const SigTabDev star = tr.star_tab;
+    const dim3 g((unsigned)((tr.n_wav + kBlock - 1) / kBlock), (unsigned)((tr.n_orb + kRmP - 1) / kRmP));
+#define PROM_RM(NSV, OC)                                                                                \
+  hipExtLaunchKernelGGL((k_tau_rm<NSV, OC>), g, dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, \
+                        tr.sigtab.as<SigTabDev>(), na, star, tr.rm_slices.as<int32_t>(), tr.wav.as<double>(), \
+                        tr.n_wav, tr.crho.as<double>(), tr.cclv.as<double>(), tr.cshift.as<double>(),     \
+                        rs.flags.as<int32_t>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb,                  \
+                        tr.count_evals ? rs.counts.as<int32_t>() : nullptr, rs.R.as<double>())
+#define PROM_RM_NS(OC)                       \
+  if (na <= 1) PROM_RM(1, OC);               \
+  else if (na == 2) PROM_RM(2, OC);          \
+  else if (na <= 4) PROM_RM(4, OC);          \
+  else PROM_RM(8, OC);
+    PROM_REQUIRE(tr.n_mol == 0 && na <= 8, "transit: the stellar-spectrum path takes <= 8 atomic constituents and no molecules");
+    if (tr.exp_mode) { PROM_RM_NS(false) } else { PROM_RM_NS(true) }
+#undef PROM_RM_NS
+#undef PROM_RM
+    *variant = 40 + (na <= 8 ? na : 0);
+    PROM_HIP(hipGetLastError());
+    return;
   }
   // 2. per-phase compaction, ordering, merging of equal-column chords, window tables
   if (wpath) {

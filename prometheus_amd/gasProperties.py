@@ -519,14 +519,17 @@ class Transit:
     def _host_inputs(self) -> dict:
         g = self.spatialGrid
         star = self.planet.hostStar
-        if star.Fstar_function is not None:
-            raise NotImplementedError("stellar spectrum / RM path (gasProperties.py:1210-1219) is not in this "
-                                      "build (SURVEY.md §8f rank 2)")
         phi, rho = g.getChordPositions()
         y, z = rho * np.sin(phi), rho * np.cos(phi)
         mu = np.sqrt(np.clip(1. - rho ** 2 / star.R ** 2, 0, 1))
         clv = 1. - star.CLV_u1 * (1. - mu) - star.CLV_u2 * (1. - mu) ** 2
         fout = rho * (np.ones_like(clv) * clv)
+        stellar = None
+        if star.Fstar_function is not None:
+            # gasProperties.py:1183-1184: the Rossiter-McLaughlin shift of each chord's stellar spectrum
+            v_star = star.vsiniStarrot * rho / star.R * np.cos(phi - star.phiStarrot)
+            stellar = {"rho": rho, "clv": clv, "shift": const.calculateDopplerShift(v_star),
+                       "table": self._star_table(star.Fstar_function)}
         orb = g.constructOrbphaseAxis()
         moons = [d.moon for d in self.atmosphere.densityDistributionList if d.hasMoon]
         scen = []
@@ -550,10 +553,31 @@ class Transit:
         return {"y": y, "z": z, "fout": fout, "orb": orb, "x": g.constructXaxis(), "dx": g.getDeltaX(),
                 "planet_y": self.planet.a * np.sin(orb), "planet_R": self.planet.R,
                 "moon_y": np.array([m.getPosition(orb)[1] for m in moons]).reshape(len(moons), len(orb)),
-                "moon_R": np.array([m.R for m in moons], dtype=np.float64), "scenarios": scen}
+                "moon_R": np.array([m.R for m in moons], dtype=np.float64), "scenarios": scen,
+                "stellar": stellar}
+
+    def _star_table(self, fn) -> "LookupTable":
+        """Device copies of Fstar_function's (x, log10 F) (offset 0: n_interp_log(..., 0.0)), cached
+        per function object."""
+        cached = getattr(self, "_star_cache", None)
+        if cached is not None and cached[0] is fn:
+            return cached[1]
+        if isinstance(fn, LookupTable):
+            tab = fn
+        else:
+            x = np.ascontiguousarray(np.asarray(fn.x, dtype=np.float64))
+            if np.any(x[1:] < x[:-1]):
+                raise ValueError("Fstar_function.x must be ascending (np.interp, gasProperties.py:1214)")
+            tab = LookupTable(x, np.ascontiguousarray(np.asarray(fn.y, dtype=np.float64)), 0.0)
+        self._star_cache = (fn, tab)
+        return tab
 
     def _problem(self, dev, host: dict, w0: int, w1: int, cull_tau: float,
                  options: int = 0) -> "_native.TransitInputs":
+        star = None
+        if host.get("stellar") is not None:
+            st = host["stellar"]
+            star = {"table_id": st["table"].table_id(dev), "rho": st["rho"], "clv": st["clv"], "shift": st["shift"]}
         scs = []
         for e in host["scenarios"]:
             cons = []
@@ -567,7 +591,7 @@ class Transit:
             wavelength=self.wavelength[w0:w1], chord_y=host["y"], chord_z=host["z"], chord_fout=host["fout"],
             n_orb=len(host["orb"]), x=host["x"], delta_x=host["dx"], planet_y=host["planet_y"],
             planet_R=host["planet_R"], moon_y=host["moon_y"], moon_R=host["moon_R"], scenarios=scs,
-            cull_tau=cull_tau, options=options, k_B=const.k_B)
+            cull_tau=cull_tau, options=options, k_B=const.k_B, star=star)
 
     def sumOverChords(self, max_memory_gb: float = 2.0, devices: Optional[Sequence[int]] = None,
                       cull_tau: float = 0.0, options: int = 0) -> np.ndarray:

@@ -214,3 +214,49 @@ def test_windowed_no_merge_no_window_matches_reference(dev):
     for opt in (0, _native.OPT_NO_MERGE, _native.OPT_NO_WINDOW, _native.OPT_NO_MERGE | _native.OPT_NO_WINDOW):
         R = tr.sumOverChords(devices=[0], options=opt)
         assert rel(R, d["R"]) < R_TOL, opt
+
+
+def _with_star(tr, star, x, F):
+    hs = tr.planet.hostStar
+    hs.addCLVparameters(star["u1"], star["u2"])
+    hs.addRMparameters(star["vsini"], star["phi_rot"])
+    hs.addFstarSpectrum(x, F)
+    return tr
+
+
+@pytest.mark.parametrize("name", ["rm_C1", "rm_C2r", "rm_exomoon"])
+def test_stellar_spectrum_golden(dev, name):
+    """Stellar spectrum with CLV and Rossiter-McLaughlin rotation (gasProperties.py:1180-1219) against
+    the reference's own R; table exp and ocml exp; shards bitwise identical."""
+    from prometheus_amd import _native, configs
+    d = load(name)
+    cfg = json.loads(str(d["config"]))
+    star = json.loads(str(d["star"]))
+    g = cfg["Grids"]
+    x, F = configs.synthetic_star_spectrum(g["lower_w"], g["upper_w"])
+    tr = _with_star(_product_transit(cfg), star, x, F)
+    R = tr.sumOverChords(devices=[0])
+    st = tr.last_stats[-1]
+    err = rel(R, d["R"])
+    print("%s: max rel err %.3e, stats %s" % (name, err, st))
+    assert err < R_TOL
+    assert st["tau_kernel_variant"] >= 40
+    assert st["active_chords"] + st["transparent_chords"] + st["blocked_chords"] == R.shape[0] * tr.spatialGrid.phi_steps * tr.spatialGrid.rho_steps
+    R_o = tr.sumOverChords(devices=[0], options=_native.OPT_OCML_EXP)
+    assert rel(R_o, d["R"]) < R_TOL and rel(R, R_o) < 1e-13
+    assert np.array_equal(R, tr.sumOverChords(devices=[0, 0, 0]))
+
+
+def test_stellar_spectrum_fine_table_global_lookup(dev):
+    """A stellar table too fine for the LDS slice (> 1024 nodes per workgroup) takes the global
+    directory lookup; checked against the oracle."""
+    from prometheus_amd import configs
+    cfg = configs.get("C1")
+    star = {"u1": 0.5, "u2": 0.1, "vsini": 8e6, "phi_rot": 2.0}
+    g = cfg["Grids"]
+    x, F = configs.synthetic_star_spectrum(g["lower_w"], g["upper_w"], step=5e-12)
+    tr = _with_star(_product_transit(cfg), star, x, F)
+    R = tr.sumOverChords(devices=[0])
+    wav, orb, Ro = O.run_setup(cfg, None, star=dict(star, fstar=(x, np.log10(F))))
+    assert np.array_equal(wav, tr.wavelength)
+    assert rel(R, Ro) < R_TOL

@@ -106,3 +106,27 @@ def test_synthetic_table_matches_product_copy():
     b = configs.synthetic_molecular_table(n_nu=101)
     for k in a:
         assert np.array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("name", ["rm_C1", "rm_C2r", "rm_exomoon"])
+def test_stellar_spectrum(name):
+    """CLV + Rossiter-McLaughlin rotation + a stellar spectrum (gasProperties.py:1180-1219): the oracle
+    reproduces the reference bitwise; the synthetic spectrum is the one the fixture was made with."""
+    d = load(name)
+    cfg = json.loads(str(d["config"]))
+    star = json.loads(str(d["star"]))
+    g = cfg["Grids"]
+    x, F = O.synthetic_star_spectrum(g["lower_w"], g["upper_w"])
+    y = np.log10(F)
+    sha = hashlib.sha256(np.ascontiguousarray(np.concatenate([x, y])).tobytes()).hexdigest()
+    assert sha == str(d["fstar_sha"])
+    wav, orb, R = O.run_setup(cfg, None, star=dict(star, fstar=(x, y)))
+    assert np.array_equal(wav, d["wavelength"])
+    assert np.array_equal(R, d["R"]), np.max(np.abs(R / d["R"] - 1))
+
+
+def test_synthetic_star_matches_product_copy():
+    from prometheus_amd import configs
+    a = O.synthetic_star_spectrum(5886e-8, 5890e-8)
+    b = configs.synthetic_star_spectrum(5886e-8, 5890e-8)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
