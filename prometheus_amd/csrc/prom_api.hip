@@ -447,6 +447,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       PROM_REQUIRE(n_mol == 0 && n_atoms <= 8,
                    "transit: the stellar-spectrum path takes <= 8 atomic constituents and no molecules");
       const prom::AtomTable& sb = ctx->tables[pb->star_table];
+      PROM_REQUIRE(sb.offset == 0.0, "transit: the star table must have offset 0 (n_interp_log(..., 0.0))");
       tr.star_tab = prom::SigTabDev{sb.x.as<double>(), sb.y.as<double>(), sb.n, sb.offset, nullptr,
                                     sb.dir.as<int32_t>(), sb.n_dir, 0, sb.dir_x0, sb.dir_inv_h, 0.0, 0.0};
       upload(tr.crho, pb->chord_rho, tr.n_pr, s);
@@ -460,6 +461,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         smin = std::min(smin, v);
         smax = std::max(smax, v);
       }
+      tr.star_uniform = true;
+      for (int32_t i = 1; i < tr.n_pr; ++i)
+        if (!(pb->chord_star_shift[i] == pb->chord_star_shift[0])) tr.star_uniform = false;
       const int64_t n_tiles = (tr.n_wav + 255) / 256;
       std::vector<int32_t> sl(3 * n_tiles, 0);
       const std::vector<double>& X = sb.hx;

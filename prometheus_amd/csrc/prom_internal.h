@@ -216,6 +216,7 @@ struct TransitDev {
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
   // stellar spectrum (prom_transit_problem.has_star)
   bool star = false;
+  bool star_uniform = false;                // every chord's stellar shift equal (no rotation)
   SigTabDev star_tab{};                     // the F_star table (x, log10 F, offset 0; shift unused)
   DevBuf crho, cclv, cshift;                // [n_pr]
   DevBuf rm_slices;                         // [n_wav tiles of kBlock][3] {lo, m, half}: LDS slice

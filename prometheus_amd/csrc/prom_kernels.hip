@@ -2025,17 +2025,36 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
 // ---- stellar spectrum path (gasProperties.py:1180-1219 with Fstar_function set) ----------------------
 // F(c, w) = rho_c * (F_star(lambda_w / s_c) * clv_c) differs per chord AND wavelength (the Rossiter-
 // McLaughlin shift s_c moves the stellar lines across the disk), so neither the flat-star F_out
-// factorisation nor the windowed tail moments apply: every (chord, phase, wavelength) term is
-// evaluated, in chord order, as in the reference.  One thread per wavelength, kRmP phases per
-// workgroup; F is computed once per (chord, wavelength) and shared by the workgroup's phases, and the
-// phase-independent F_out sum is accumulated beside them.  F_star's np.interp bracket is searched in
-// an LDS copy of the star-table slice that the workgroup's targets lambda / s can reach (prom_api.hip
-// rm_slices), or in global memory (sigma_of's directory) when that slice exceeds kRmStarMax nodes.
+// factorisation nor the windowed tail moments apply: every (chord, wavelength) flux is evaluated.
+// One thread per wavelength, kRmP phases per workgroup.  F is computed once per (chord, wavelength)
+// and shared by the workgroup's phases; chords transparent at every phase of the group add F to one
+// shared sum (exp(-tau) == 1 to the last ulp), the others are resolved per phase from a bit mask.
+// F_star(t) = 10^(f_k + slope_k (t - x_k)) is evaluated as 10^f_k * exp(ln10 slope_k (t - x_k)) on the
+// LDS copy of the star-table slice that the workgroup's targets t = lambda / s can reach (prom_api.hip
+// rm_slices), bracketed through a slice-local bucket directory; a tile whose slice exceeds kRmStarMax
+// nodes uses the global lookup (sigma_of).  With one shift for every chord (no rotation) F_star is
+// evaluated once per wavelength.
 constexpr int kRmP = 8;            // phases per workgroup
 constexpr int kRmChunk = 64;       // chords staged in LDS per sweep
-constexpr int kRmGroup = 4;        // chords whose bracket searches are interleaved
+constexpr int kRmDir = 2 * kRmStarMax;   // slice-directory buckets (at most)
+constexpr double kLn10 = 2.302585092994045684;
 
-template <int NSMAX, bool OCML>
+// exp(a) for the F_star interpolation factor (|a| <= ln10 |f_k+1 - f_k|): the 256-entry table scheme of
+// acc_exp256 (relative error ~ |a| 2^-53 from the argument scaling)
+__device__ __forceinline__ double exp_tab(double a, const double* __restrict__ tab) {
+  const double y = a * -kM256Ln2;
+  const double k = __builtin_rint(y);
+  const int ki = (int)k;
+  const double d = y - k;
+  double p = __builtin_fma(d, kE256C5, kE256C4);
+  p = __builtin_fma(d, p, kE256C3);
+  p = __builtin_fma(d, p, kE256C2);
+  p = __builtin_fma(d, p, kE256C1);
+  p = __builtin_fma(d, p, 1.0);
+  return __builtin_amdgcn_ldexp(tab[ki & 255], ki >> 8) * p;
+}
+
+template <int NSMAX, bool OCML, bool UNISTAR>
 __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__ tabs, int32_t na,
                                                    const SigTabDev star, const int32_t* __restrict__ slices,
                                                    const double* __restrict__ wav, int64_t n_wav,
@@ -2047,10 +2066,11 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
                                                    int32_t n_orb, int32_t* __restrict__ counts,
                                                    double* __restrict__ R) {
   __shared__ double sexp[256];
-  __shared__ double sx[kRmStarMax], sy[kRmStarMax], ssl[kRmStarMax];
+  __shared__ double sx[kRmStarMax], sF[kRmStarMax], sc[kRmStarMax];
+  __shared__ int16_t sdir[kRmDir];
   __shared__ double sRho[kRmChunk], sClv[kRmChunk], sSh[kRmChunk];
   __shared__ double sN[kRmP * NSMAX * kRmChunk];
-  __shared__ int32_t sFl[kRmP * kRmChunk];
+  __shared__ int32_t sMask[kRmChunk];
   __shared__ int32_t scnt[kRmP * 3];
   sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
   const int32_t o0 = blockIdx.y * kRmP;
@@ -2076,20 +2096,29 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       for (int k = 3; k < kCnt; ++k) cp[k] = 0;
     }
   }
-  // star-table slice {lo, m, half}: nodes lo .. lo+m-1 staged, padded with +inf up to 2 * half
+  // star-table slice {lo, m, half}: nodes lo .. lo+m-1 as (x_k, 10^f_k, ln10 slope_k) + a directory of
+  // nb = 4 half buckets over [x_0, x_m-1]: sdir[j] = last node <= x_0 + j h
   const int32_t* sl = slices + 3 * (int64_t)blockIdx.x;
   const int64_t lo = sl[0];
-  const int32_t m = sl[1], half = sl[2];
+  const int32_t m = UNISTAR ? 0 : sl[1], half = sl[2];
+  const int32_t nb = 4 * half < kRmDir ? 4 * half : kRmDir;
+  double sx0 = 0.0, inv_h = 0.0;
   if (m > 0) {
-    for (int i = threadIdx.x; i < 2 * half; i += kBlock) {
-      if (i < m) {
-        const double x0 = star.x[lo + i], f0 = star.y[lo + i];
-        sx[i] = x0;
-        sy[i] = f0;
-        ssl[i] = i + 1 < m ? (star.y[lo + i + 1] - f0) / (star.x[lo + i + 1] - x0) : 0.0;
-      } else {
-        sx[i] = __builtin_inf();
-      }
+    for (int i = threadIdx.x; i < m; i += kBlock) {
+      const double x0 = star.x[lo + i], f0 = star.y[lo + i];
+      sx[i] = x0;
+      sF[i] = exp10(f0);                       // star tables have offset 0 (prom_transit_set)
+      sc[i] = i + 1 < m ? ((star.y[lo + i + 1] - f0) / (star.x[lo + i + 1] - x0)) * kLn10 : 0.0;
+    }
+    sx0 = star.x[lo];
+    const double span = star.x[lo + m - 1] - sx0;
+    inv_h = span > 0.0 ? (double)nb / span : 0.0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < nb; j += kBlock) {
+      const double b = sx0 + (double)j * (span / (double)nb);
+      int pos = 0;
+      for (int st = half; st > 0; st >>= 1) pos += (pos + st < m && sx[pos + st] <= b) ? st : 0;
+      sdir[j] = (int16_t)pos;
     }
   }
   // sigma_s at each of this thread's phases (shift_o * lambda, as getLOSopticalDepth_Batch)
@@ -2099,10 +2128,12 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
 #pragma unroll
     for (int s = 0; s < NSMAX; ++s)
       sg[p][s] = (p < np && s < na) ? sigma_of(tabs[s].shift[o0 + p] * lam, tabs[s]) : 0.0;
+  double fstar_uni = 0.0;
+  if constexpr (UNISTAR) fstar_uni = sigma_of(lam / cshift[0], star);
   double in[kRmP];
 #pragma unroll
   for (int p = 0; p < kRmP; ++p) in[p] = 0.0;
-  double out = 0.0;
+  double out = 0.0, tall = 0.0;
   for (int32_t c0 = 0; c0 < n_pr; c0 += kRmChunk) {
     const int nch = n_pr - c0 < kRmChunk ? n_pr - c0 : kRmChunk;
     __syncthreads();
@@ -2110,10 +2141,13 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       sRho[i] = crho[c0 + i];
       sClv[i] = cclv[c0 + i];
       sSh[i] = cshift[c0 + i];
-    }
-    for (int i = threadIdx.x; i < np * nch; i += kBlock) {
-      const int p = i / nch, c = i - p * nch;
-      sFl[p * kRmChunk + c] = flags[(int64_t)(o0 + p) * n_pr + c0 + c];
+      int32_t am = 0, bm = 0;
+      for (int p = 0; p < np; ++p) {
+        const int32_t f = flags[(int64_t)(o0 + p) * n_pr + c0 + i];
+        am |= (f == 0) << p;
+        bm |= (f == 2) << p;
+      }
+      sMask[i] = am | (bm << 8);
     }
     for (int i = threadIdx.x; i < na * np * nch; i += kBlock) {
       const int sp = i / nch, c = i - sp * nch;     // sp = s * np + p
@@ -2121,64 +2155,65 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       sN[(p * NSMAX + s) * kRmChunk + c] = ncol[((int64_t)s * n_orb + o0 + p) * n_pr + c0 + c];
     }
     __syncthreads();
-    for (int cg = 0; cg < nch; cg += kRmGroup) {
-      double F[kRmGroup];
-      if (m > 0) {
-        double t[kRmGroup];
-        int pos[kRmGroup];
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) {
-          t[u] = lam / sSh[cg + u < nch ? cg + u : nch - 1];
-          pos[u] = 0;
-        }
-        for (int st = half; st > 0; st >>= 1) {
-#pragma unroll
-          for (int u = 0; u < kRmGroup; ++u) pos[u] += sx[pos[u] + st] <= t[u] ? st : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) {
-          // numpy.interp on the slice: below node 0 only when lo == 0 (fp[0]); at or beyond the last
-          // staged node only when it is the table's last (fp[n-1]); else sx[pos] <= t < sx[pos + 1]
-          const double tu = t[u];
-          const int k = pos[u];
-          double v;
-          if (tu != tu) v = tu;
-          else if (!(tu >= sx[0])) v = sy[0];
-          else if (tu >= sx[m - 1]) v = sy[m - 1];
-          else if (sx[k] == tu) v = sy[k];
-          else {
-            v = ssl[k] * (tu - sx[k]) + sy[k];
-            if (v != v) {
-              v = ssl[k] * (tu - sx[k + 1]) + sy[k + 1];
-              if (v != v && sy[k] == sy[k + 1]) v = sy[k];
+    for (int c = 0; c < nch; ++c) {
+      double fs;
+      if constexpr (UNISTAR) {
+        fs = fstar_uni;
+      } else if (m > 0) {
+        const double t = lam / sSh[c];
+        if (!(t >= sx0)) {
+          fs = t != t ? t : sF[0];                   // below the table (slice starts at node 0)
+        } else if (t >= sx[m - 1]) {
+          fs = sF[m - 1];                            // at / beyond the table's last node
+        } else {
+          const double fj = (t - sx0) * inv_h;
+          int j = fj >= (double)nb ? nb - 1 : (int)fj;
+          int k = sdir[j > 0 ? j - 1 : 0];
+          k += sx[k + 1] <= t ? 1 : 0;
+          k += sx[k + 1] <= t ? 1 : 0;
+          k += sx[k + 1] <= t ? 1 : 0;
+          if (sx[k + 1] <= t) {                      // crowded bucket: bisect the rest of the slice
+            int a = k + 1, b = m - 1;                // sx[a] <= t < sx[b]
+            while (b - a > 1) {
+              const int mid = (a + b) >> 1;
+              if (sx[mid] <= t) a = mid; else b = mid;
+            }
+            k = a;
+          }
+          const double xk = sx[k];
+          if (xk == t) {
+            fs = sF[k];
+          } else {
+            const double arg = sc[k] * (t - xk);
+            if (__builtin_isfinite(arg)) {
+              fs = sF[k] * exp_tab(arg, sexp);
+            } else {                                 // infinite slope (repeated node): np.interp's rules
+              fs = sigma_of(t, star);
             }
           }
-          F[u] = exp10(v) - star.offset;
         }
       } else {
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) F[u] = sigma_of(lam / sSh[cg + u < nch ? cg + u : nch - 1], star);
+        fs = sigma_of(lam / sSh[c], star);
+      }
+      const double Fc = sRho[c] * (fs * sClv[c]);
+      out += Fc;
+      const int32_t mk = __builtin_amdgcn_readfirstlane(sMask[c]);
+      if (mk == 0) {
+        tall += Fc;                                  // transparent at every phase of the group
+        continue;
       }
 #pragma unroll
-      for (int u = 0; u < kRmGroup; ++u) {
-        const int c = cg + u;
-        if (c >= nch) break;
-        const double Fc = sRho[c] * (F[u] * sClv[c]);
-        out += Fc;
+      for (int p = 0; p < kRmP; ++p) {
+        if (p >= np) break;
+        if ((mk >> p) & 1) {
+          double tau = 0.0;
 #pragma unroll
-        for (int p = 0; p < kRmP; ++p) {
-          if (p >= np) break;
-          const int32_t fl = sFl[p * kRmChunk + c];
-          if (fl == 1) {
-            in[p] += Fc;                       // transparent: exp(-tau) == 1 to the last ulp
-          } else if (fl == 0) {
-            double tau = 0.0;
-#pragma unroll
-            for (int s = 0; s < NSMAX; ++s)
-              if (s < na) tau += sN[(p * NSMAX + s) * kRmChunk + c] * sg[p][s];
-            if (OCML || !(tau < 700.0 && tau > -700.0)) in[p] += Fc * exp(-tau);
-            else in[p] = acc_exp256(in[p], Fc, tau * kM256Ln2, sexp);
-          }
+          for (int s = 0; s < NSMAX; ++s)
+            if (s < na) tau += sN[(p * NSMAX + s) * kRmChunk + c] * sg[p][s];
+          if (OCML || !(tau < 700.0 && tau > -700.0)) in[p] += Fc * exp(-tau);
+          else in[p] = acc_exp256(in[p], Fc, tau * kM256Ln2, sexp);
+        } else if (!((mk >> (p + 8)) & 1)) {
+          in[p] += Fc;                               // transparent at this phase
         }
       }
     }
@@ -2186,7 +2221,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
   if (live) {
 #pragma unroll
     for (int p = 0; p < kRmP; ++p)
-      if (p < np) R[(int64_t)(o0 + p) * n_wav + w] = in[p] / out;
+      if (p < np) R[(int64_t)(o0 + p) * n_wav + w] = (in[p] + tall) / out;
   }
 }
 
@@ -2264,7 +2299,11 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     const SigTabDev star = tr.star_tab;
     const dim3 g((unsigned)((tr.n_wav + kBlock - 1) / kBlock), (unsigned)((tr.n_orb + kRmP - 1) / kRmP));
 #define PROM_RM(NSV, OC)                                                                                \
-  hipExtLaunchKernelGGL((k_tau_rm<NSV, OC>), g, dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, \
+  do {                                                                                                  \
+    if (tr.star_uniform) { PROM_RM2(NSV, OC, true); } else { PROM_RM2(NSV, OC, false); }                 \
+  } while (0)
+#define PROM_RM2(NSV, OC, UV)                                                                           \
+  hipExtLaunchKernelGGL((k_tau_rm<NSV, OC, UV>), g, dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, \
                         tr.sigtab.as<SigTabDev>(), na, star, tr.rm_slices.as<int32_t>(), tr.wav.as<double>(), \
                         tr.n_wav, tr.crho.as<double>(), tr.cclv.as<double>(), tr.cshift.as<double>(),     \
                         rs.flags.as<int32_t>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb,                  \
@@ -2278,6 +2317,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     if (tr.exp_mode) { PROM_RM_NS(false) } else { PROM_RM_NS(true) }
 #undef PROM_RM_NS
 #undef PROM_RM
+#undef PROM_RM2
     *variant = 40 + (na <= 8 ? na : 0);
     PROM_HIP(hipGetLastError());
     return;

@@ -260,3 +260,23 @@ def test_stellar_spectrum_fine_table_global_lookup(dev):
     wav, orb, Ro = O.run_setup(cfg, None, star=dict(star, fstar=(x, np.log10(F))))
     assert np.array_equal(wav, tr.wavelength)
     assert rel(R, Ro) < R_TOL
+
+
+def test_stellar_spectrum_clustered_nodes(dev):
+    """A non-uniform stellar table (a coarse grid plus tight node clusters and repeated nodes) makes
+    the slice directory's buckets crowded (bisection fallback); checked against the oracle."""
+    from prometheus_amd import configs
+    cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5894e-8,
+                          res_low=5e-9, res_high=1e-10)
+    star = {"u1": 0.3, "u2": 0.2, "vsini": 4e6, "phi_rot": 0.7}
+    g = cfg["Grids"]
+    x0, F0 = configs.synthetic_star_spectrum(g["lower_w"], g["upper_w"], step=5e-10)
+    rng = np.random.default_rng(3)
+    extra = np.concatenate([c + np.linspace(0, 2e-11, 100) for c in rng.uniform(x0[5], x0[-5], 4)])
+    x = np.sort(np.concatenate([x0, extra, x0[100:103]]))          # three repeated nodes
+    F = np.interp(x, x0, F0) * (1. + 0.2 * np.sin(x * 3e9))
+    tr = _with_star(_product_transit(cfg), star, x, F)
+    R = tr.sumOverChords(devices=[0])
+    wav, orb, Ro = O.run_setup(cfg, None, star=dict(star, fstar=(x, np.log10(F))))
+    assert np.array_equal(wav, tr.wavelength)
+    assert rel(R, Ro) < R_TOL
