@@ -2036,6 +2036,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
 // evaluated once per wavelength.
 constexpr int kRmP = 8;            // phases per workgroup
 constexpr int kRmChunk = 64;       // chords staged in LDS per sweep
+constexpr int kRmGroup = 4;        // chords whose F_star lookups are interleaved
 constexpr int kRmDir = 2 * kRmStarMax;   // slice-directory buckets (at most)
 constexpr double kLn10 = 2.302585092994045684;
 
@@ -2155,65 +2156,80 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       sN[(p * NSMAX + s) * kRmChunk + c] = ncol[((int64_t)s * n_orb + o0 + p) * n_pr + c0 + c];
     }
     __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-      double fs;
+    for (int cg = 0; cg < nch; cg += kRmGroup) {
+      // F_star for kRmGroup chords at once: their LDS chains (directory -> bracket steps -> node ->
+      // table exp) are independent, so interleaving them hides the LDS latency
+      double fsg[kRmGroup];
       if constexpr (UNISTAR) {
-        fs = fstar_uni;
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) fsg[u] = fstar_uni;
       } else if (m > 0) {
-        const double t = lam / sSh[c];
-        if (!(t >= sx0)) {
-          fs = t != t ? t : sF[0];                   // below the table (slice starts at node 0)
-        } else if (t >= sx[m - 1]) {
-          fs = sF[m - 1];                            // at / beyond the table's last node
-        } else {
-          const double fj = (t - sx0) * inv_h;
-          int j = fj >= (double)nb ? nb - 1 : (int)fj;
-          int k = sdir[j > 0 ? j - 1 : 0];
-          k += sx[k + 1] <= t ? 1 : 0;
-          k += sx[k + 1] <= t ? 1 : 0;
-          k += sx[k + 1] <= t ? 1 : 0;
-          if (sx[k + 1] <= t) {                      // crowded bucket: bisect the rest of the slice
-            int a = k + 1, b = m - 1;                // sx[a] <= t < sx[b]
+        double t[kRmGroup];
+        int k[kRmGroup];
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) {
+          t[u] = lam / sSh[cg + u < nch ? cg + u : nch - 1];
+          const double fj = (t[u] - sx0) * inv_h;
+          const int j = !(fj >= 1.0) ? 1 : (fj >= (double)nb ? nb : (int)fj);
+          k[u] = sdir[j - 1];
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int u = 0; u < kRmGroup; ++u) k[u] += (k[u] + 1 < m && sx[k[u] + 1] <= t[u]) ? 1 : 0;
+        const double xlast = sx[m - 1];
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) {
+          const double tu = t[u];
+          if (!(tu >= sx0) || tu >= xlast) {
+            // below the table (the slice starts at node 0) / at or beyond the table's last node
+            fsg[u] = tu != tu ? tu : (tu >= xlast ? sF[m - 1] : sF[0]);
+            continue;
+          }
+          int kk = k[u];
+          if (sx[kk + 1] <= tu) {                      // crowded bucket: bisect the rest of the slice
+            int a = kk + 1, b = m - 1;                 // sx[a] <= t < sx[b]
             while (b - a > 1) {
               const int mid = (a + b) >> 1;
-              if (sx[mid] <= t) a = mid; else b = mid;
+              if (sx[mid] <= tu) a = mid; else b = mid;
             }
-            k = a;
+            kk = a;
           }
-          const double xk = sx[k];
-          if (xk == t) {
-            fs = sF[k];
-          } else {
-            const double arg = sc[k] * (t - xk);
-            if (__builtin_isfinite(arg)) {
-              fs = sF[k] * exp_tab(arg, sexp);
-            } else {                                 // infinite slope (repeated node): np.interp's rules
-              fs = sigma_of(t, star);
-            }
-          }
+          const double xk = sx[kk];
+          const double arg = sc[kk] * (tu - xk);
+          if (xk == tu) fsg[u] = sF[kk];
+          else if (__builtin_isfinite(arg)) fsg[u] = sF[kk] * exp_tab(arg, sexp);
+          else fsg[u] = sigma_of(tu, star);          // infinite slope (repeated node): np.interp's rules
         }
       } else {
-        fs = sigma_of(lam / sSh[c], star);
-      }
-      const double Fc = sRho[c] * (fs * sClv[c]);
-      out += Fc;
-      const int32_t mk = __builtin_amdgcn_readfirstlane(sMask[c]);
-      if (mk == 0) {
-        tall += Fc;                                  // transparent at every phase of the group
-        continue;
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) fsg[u] = sigma_of(lam / sSh[cg + u < nch ? cg + u : nch - 1], star);
       }
 #pragma unroll
-      for (int p = 0; p < kRmP; ++p) {
-        if (p >= np) break;
-        if ((mk >> p) & 1) {
-          double tau = 0.0;
+      for (int u = 0; u < kRmGroup; ++u) {
+        const int c = cg + u;
+        if (c >= nch) break;
+        const double fs = fsg[u];
+        const double Fc = sRho[c] * (fs * sClv[c]);
+        out += Fc;
+        const int32_t mk = __builtin_amdgcn_readfirstlane(sMask[c]);
+        if (mk == 0) {
+          tall += Fc;                                  // transparent at every phase of the group
+          continue;
+        }
 #pragma unroll
-          for (int s = 0; s < NSMAX; ++s)
-            if (s < na) tau += sN[(p * NSMAX + s) * kRmChunk + c] * sg[p][s];
-          if (OCML || !(tau < 700.0 && tau > -700.0)) in[p] += Fc * exp(-tau);
-          else in[p] = acc_exp256(in[p], Fc, tau * kM256Ln2, sexp);
-        } else if (!((mk >> (p + 8)) & 1)) {
-          in[p] += Fc;                               // transparent at this phase
+        for (int p = 0; p < kRmP; ++p) {
+          if (p >= np) break;
+          if ((mk >> p) & 1) {
+            double tau = 0.0;
+#pragma unroll
+            for (int s = 0; s < NSMAX; ++s)
+              if (s < na) tau += sN[(p * NSMAX + s) * kRmChunk + c] * sg[p][s];
+            if (OCML || !(tau < 700.0 && tau > -700.0)) in[p] += Fc * exp(-tau);
+            else in[p] = acc_exp256(in[p], Fc, tau * kM256Ln2, sexp);
+          } else if (!((mk >> (p + 8)) & 1)) {
+            in[p] += Fc;                               // transparent at this phase
+          }
         }
       }
     }
