@@ -53,6 +53,7 @@ class _FakeH5:
 
 
 def _install_stubs():
+    sys.dont_write_bytecode = True   # nothing is written under the reference tree
     numba = types.ModuleType("numba")
     numba.njit = lambda *a, **k: (a[0] if a and callable(a[0]) else (lambda f: f))
     numba.prange = range

@@ -1,10 +1,12 @@
 #!/bin/bash
 # PMC passes (each its own rocprofv3 run, counters only -- no trace domains) over one tau-kernel
 # variant.  Usage: tools/profile_pmc.sh <tag> [tune_tau args...]
+#        PMC_SCRIPT=tools/rm_bench.py tools/profile_pmc.sh rm C2 --runs 1   (any python script + args)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 TAG=${1:-tau}; shift
 ARGS=${*:-"--variants 1 --exp 1 --reps 5"}
+SCRIPT=${PMC_SCRIPT:-tools/tune_tau.py}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 i=0
@@ -12,7 +14,7 @@ while read -r line; do
   [ -z "$line" ] && continue
   i=$((i+1))
   echo "== pass $i: $line"
-  timeout -k 10 300 rocprofv3 --pmc $line --output-format csv -d $OUT/p$i -o p$i -- python3 tools/tune_tau.py $ARGS > $OUT/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $line --output-format csv -d $OUT/p$i -o p$i -- python3 $SCRIPT $ARGS > $OUT/p$i.log 2>&1
   rc=$?
   echo "rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $OUT/p$i.log; exit $rc; fi
