@@ -204,6 +204,15 @@ int32_t prom_transit_result(prom_ctx* ctx, double* R_out);
 /* Column densities N[s][o][ip] of the last run (atomic constituents in scenario order); testing aid. */
 int32_t prom_transit_columns(prom_ctx* ctx, double* N_out);
 
+/* Band statistics of the last run's R on the device, for light curves (the band-averaged transit
+ * depth of mainRetrieval.py:76-93) without copying R to the host.  Phase o selects the wavelengths
+ * with bounds[o][b][0] <= lambda <= bounds[o][b][1] for any band b; sum_out[o] is the sum of R over
+ * them, count_out[o] their number and max_out[o] the maximum of R over ALL wavelengths of the problem
+ * (NaN if any R is NaN, like numpy.max).  Over wavelength shards the sums and counts add and the
+ * maxima combine with max; the light curve is (sum / count) / max. */
+int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bounds, double* sum_out,
+                                int64_t* count_out, double* max_out);
+
 /* Live per-run timing of the tau kernel without per-run synchronisation: between prom_timing_begin
  * and prom_timing_end every prom_transit_run carries start/stop events on its tau kernel's dispatch;
  * prom_timing_end waits for them and returns ms[run][4] = {NaN, NaN, tau, NaN} for up to max_runs

@@ -456,6 +456,20 @@ def transit_depth(scenarios, doppler, grid, wav, tables, max_memory_gb=2.0,
     return Fin / Fout
 
 
+def lightcurve(R, wav, orbphase, planet: Body, centers=(5891.583253e-8, 5897.558147e-8), bandwidth=0.75e-8):
+    """Band-averaged light curve restated from mainRetrieval.py:76-93: per phase, mean of R over the
+    wavelengths within +-bandwidth/2 (inclusive) of any line centre times the planet's Doppler factor,
+    divided by the maximum of R at that phase."""
+    shift = doppler_shift(planet_los_velocity(planet, np.asarray(orbphase)))
+    out = []
+    for i in range(len(orbphase)):
+        sel = np.zeros(len(wav), dtype=bool)
+        for c in centers:
+            sel |= (wav >= c * shift[i] - bandwidth / 2.) & (wav <= c * shift[i] + bandwidth / 2.)
+        out.append(np.mean(R[i, sel]) / np.max(R[i, :]))
+    return np.array(out)
+
+
 def build_tables(scenarios, grid):
     """Per-constituent lookup tables (gasProperties.py:717-725, :783-787)."""
     tabs = {}

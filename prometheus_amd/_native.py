@@ -103,6 +103,7 @@ SIGNATURES = {
     "prom_transit_run": (C.c_int32, [C.c_void_p, C.POINTER(TransitStats)]),
     "prom_transit_result": (C.c_int32, [C.c_void_p, _dp]),
     "prom_transit_columns": (C.c_int32, [C.c_void_p, _dp]),
+    "prom_transit_band_stats": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _dp, C.POINTER(C.c_int64), _dp]),
     "prom_timing_begin": (C.c_int32, [C.c_void_p]),
     "prom_timing_end": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _ip]),
 }
@@ -281,6 +282,18 @@ class Device:
         out = np.empty((self._n_atoms, self._shape[0], self._n_pr))
         self._check(self.lib.prom_transit_columns(self.h, _d(out)), "prom_transit_columns")
         return out
+
+    def transit_band_stats(self, bounds):
+        """(sum, count, max) per phase of the last run's R over the band windows bounds[o][b] = (lo, hi)."""
+        b = _f64(bounds)
+        n_orb = self._shape[0]
+        if b.ndim != 3 or b.shape[0] != n_orb or b.shape[2] != 2:
+            raise ValueError("bounds must be [n_orb][n_bands][2]")
+        s, c, m = np.empty(n_orb), np.empty(n_orb, dtype=np.int64), np.empty(n_orb)
+        self._check(self.lib.prom_transit_band_stats(self.h, b.shape[1], _d(b), _d(s),
+                                                     c.ctypes.data_as(C.POINTER(C.c_int64)), _d(m)),
+                    "prom_transit_band_stats")
+        return s, c, m
 
 
 class TransitInputs:

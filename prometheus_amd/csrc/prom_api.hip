@@ -637,6 +637,30 @@ int32_t prom_transit_columns(prom_ctx* ctx, double* N_out) {
   });
 }
 
+int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bounds, double* sum_out,
+                                int64_t* count_out, double* max_out) {
+  return guarded(ctx, [&] {
+    prom::TransitDev& tr = ctx->tr;
+    if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_band_stats: no completed run");
+    PROM_REQUIRE(n_bands >= 0 && (n_bands == 0 || bounds) && sum_out && count_out && max_out,
+                 "prom_transit_band_stats: bad arguments");
+    const int32_t n_orb = tr.n_orb;
+    // the last run's stream orders the reduction after it; scratch[0..2] are free between calls
+    const hipStream_t st = ctx->streams[tr.last];
+    upload(ctx->scratch[0], bounds, (int64_t)n_orb * n_bands * 2, st);
+    ctx->scratch[1].ensure(sizeof(double) * n_orb);
+    ctx->scratch[2].ensure(sizeof(int64_t) * n_orb);
+    ctx->scratch[3].ensure(sizeof(double) * n_orb);
+    prom::launch_band_stats(st, tr.slot[tr.last].R.as<double>(), tr.wav.as<double>(), n_orb, tr.n_wav, n_bands,
+                            ctx->scratch[0].as<double>(), ctx->scratch[1].as<double>(),
+                            ctx->scratch[2].as<int64_t>(), ctx->scratch[3].as<double>());
+    download(sum_out, ctx->scratch[1], n_orb, st);
+    download(count_out, ctx->scratch[2], n_orb, st);
+    download(max_out, ctx->scratch[3], n_orb, st);
+    PROM_HIP(hipStreamSynchronize(st));
+  });
+}
+
 int32_t prom_timing_begin(prom_ctx* ctx) {
   return guarded(ctx, [&] {
     ctx->timing = true;

@@ -260,5 +260,8 @@ void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, 
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
+// per phase: sum / count of R over the band-selected wavelengths, max of R over all (prom_transit_band_stats)
+void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,
+                       int32_t n_bands, const double* bounds, double* sum, int64_t* count, double* mx);
 
 }  // namespace prom

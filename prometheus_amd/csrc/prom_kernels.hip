@@ -2241,6 +2241,56 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
   }
 }
 
+// ---- light-curve band statistics (mainRetrieval.py:76-93) -------------------------------------------
+// One workgroup per phase: strided partial sums / counts / maxima, then a fixed-order LDS tree, so the
+// result does not depend on scheduling.  The max propagates NaN (numpy.max).
+__global__ void __launch_bounds__(kBlock) k_band_stats(const double* __restrict__ R, const double* __restrict__ wav,
+                                                       int64_t n_wav, int32_t n_bands,
+                                                       const double* __restrict__ bounds, double* __restrict__ sum,
+                                                       int64_t* __restrict__ count, double* __restrict__ mx) {
+  __shared__ double ss[kBlock], sm[kBlock];
+  __shared__ int64_t sc[kBlock];
+  const int32_t o = blockIdx.x;
+  const double* b = bounds + (int64_t)o * n_bands * 2;
+  const double* r = R + (int64_t)o * n_wav;
+  double acc = 0.0, m = -__builtin_inf();
+  int64_t cnt = 0;
+  for (int64_t w = threadIdx.x; w < n_wav; w += kBlock) {
+    const double v = r[w], l = wav[w];
+    m = (v > m || v != v || m != m) ? (m != m ? m : v) : m;
+    bool sel = false;
+    for (int32_t k = 0; k < n_bands; ++k) sel = sel || (l >= b[2 * k] && l <= b[2 * k + 1]);
+    if (sel) {
+      acc += v;
+      ++cnt;
+    }
+  }
+  ss[threadIdx.x] = acc;
+  sm[threadIdx.x] = m;
+  sc[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int h = kBlock / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      ss[threadIdx.x] += ss[threadIdx.x + h];
+      sc[threadIdx.x] += sc[threadIdx.x + h];
+      const double a = sm[threadIdx.x], c = sm[threadIdx.x + h];
+      sm[threadIdx.x] = (a != a || c != c) ? __builtin_nan("") : (c > a ? c : a);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sum[o] = ss[0];
+    count[o] = sc[0];
+    mx[o] = sm[0];
+  }
+}
+
+void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,
+                       int32_t n_bands, const double* bounds, double* sum, int64_t* count, double* mx) {
+  hipLaunchKernelGGL(k_band_stats, dim3(n_orb), dim3(kBlock), 0, s, R, wav, n_wav, n_bands, bounds, sum, count, mx);
+  PROM_HIP(hipGetLastError());
+}
+
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;

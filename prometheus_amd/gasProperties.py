@@ -600,6 +600,28 @@ class Transit:
         ``devices``: GPU ids to shard the wavelength axis over (default: all visible GPUs when
         there are >= 65,536 wavelengths per GPU, else GPU 0).  ``max_memory_gb`` bounds the
         device working set of one shard step; larger shards are processed in several steps."""
+        return self._integrate(max_memory_gb, devices, cull_tau, options, None)[0]
+
+    def bandLightcurve(self, line_centers: Sequence[float] = None, bandwidth: float = None,
+                       shifts=None, max_memory_gb: float = 2.0, devices: Optional[Sequence[int]] = None,
+                       cull_tau: float = 0.0, options: int = 0, return_spectrum: bool = False):
+        """Light curve: per phase, the mean of R over windows of ``bandwidth`` about the Doppler-shifted
+        ``line_centers`` divided by the maximum of R (mainRetrieval.py:76-93; defaults Na D2/D1 and
+        0.75 A, shifted by the planet's line-of-sight velocity).  The band reduction runs on the device
+        over R in HBM; with ``return_spectrum`` R is copied back as well.  Returns the light curve
+        [n_orb] (and R)."""
+        from . import lightcurve as lc
+        if not hasattr(self, "wavelength"):
+            self.addWavelength()
+        orb = self.spatialGrid.constructOrbphaseAxis()
+        if shifts is None:
+            shifts = lc.planet_shifts(self.planet, orb)
+        bounds = lc.band_bounds(shifts, line_centers or (lc.NA_D2, lc.NA_D1),
+                                lc.BANDWIDTH if bandwidth is None else bandwidth)
+        R, acc = self._integrate(max_memory_gb, devices, cull_tau, options, bounds, want_R=return_spectrum)
+        return (acc.lightcurve(), R) if return_spectrum else acc.lightcurve()
+
+    def _integrate(self, max_memory_gb, devices, cull_tau, options, bounds, want_R=True):
         if not hasattr(self, "wavelength"):
             self.addWavelength()
         host = self._host_inputs()
@@ -614,7 +636,12 @@ class Transit:
                       if not c.isMolecule)
         per_wav = 8 * n_orb * (2 + max(1, n_atoms))
         chunk = max(4096, int(max_memory_gb * 1e9) // per_wav) // WAVE_ALIGN * WAVE_ALIGN
-        R = np.empty((n_orb, n_wav))
+        R = np.empty((n_orb, n_wav)) if want_R else None
+        acc = None
+        if bounds is not None:
+            from .lightcurve import BandAccumulator
+            acc = BandAccumulator(n_orb)
+        acc_lock = threading.Lock()
         shards = _split(n_wav, len(devices))
         errors: List[BaseException] = []
         self.last_stats = []
@@ -627,7 +654,12 @@ class Transit:
                         b = min(hi, a + chunk)
                         dev.transit_set(self._problem(dev, host, a, b, cull_tau, options))
                         st = dev.transit_run(stats=True)
-                        R[:, a:b] = dev.transit_result()
+                        if R is not None:
+                            R[:, a:b] = dev.transit_result()
+                        if acc is not None:
+                            part = dev.transit_band_stats(bounds)
+                            with acc_lock:
+                                acc.add(*part)
                         st.update(device=dev_id, w0=a, w1=b)
                         self.last_stats.append(st)
             except BaseException as ex:  # re-raised in the caller
@@ -643,4 +675,4 @@ class Transit:
                 t.join()
         if errors:
             raise errors[0]
-        return R
+        return R, acc

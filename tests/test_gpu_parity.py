@@ -280,3 +280,19 @@ def test_stellar_spectrum_clustered_nodes(dev):
     wav, orb, Ro = O.run_setup(cfg, None, star=dict(star, fstar=(x, np.log10(F))))
     assert np.array_equal(wav, tr.wavelength)
     assert rel(R, Ro) < R_TOL
+
+
+@pytest.mark.parametrize("name", ["exomoon", "C2r"])
+def test_band_lightcurve(dev, name):
+    """Transit.bandLightcurve (device band reduction over R in HBM, mainRetrieval.py:76-93) against the
+    oracle's light curve of the reference's R; sharded and with the spectrum returned."""
+    d = load("transit_" + name)
+    cfg = json.loads(str(d["config"]))
+    tr = _product_transit(cfg)
+    scen, _, _ = O.from_setup(cfg)
+    ref = O.lightcurve(d["R"], d["wavelength"], d["orbphase"], scen[0].planet)
+    lc1 = tr.bandLightcurve(devices=[0])
+    lc2, R = tr.bandLightcurve(devices=[0, 0], return_spectrum=True)
+    assert rel(lc1, ref) < R_TOL and rel(lc2, ref) < R_TOL
+    assert rel(R, d["R"]) < R_TOL
+    print(name, "light curve", lc1)

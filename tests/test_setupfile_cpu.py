@@ -55,3 +55,31 @@ def test_run_without_gpu_fails_loudly(tmp_path, monkeypatch):
     with pytest.raises(_native.NativeUnavailable):
         setupfile.run("c1", path=str(tmp_path))
     assert not (tmp_path / "output").exists()
+
+
+def test_lightcurve_host_logic():
+    """Band windows and the shard combination of the device partials (sum, count, max) reproduce the
+    oracle's light curve (mainRetrieval.py:76-93) on a golden R; partials formed here with numpy."""
+    import json
+    import os
+    import numpy as np
+    from oracle import prom_oracle as O
+    from prometheus_amd import lightcurve as lc
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "transit_exomoon.npz"))
+    cfg = json.loads(str(d["config"]))
+    R, wav, orb = d["R"], d["wavelength"], d["orbphase"]
+    scen, _, _ = O.from_setup(cfg)
+    ref = O.lightcurve(R, wav, orb, scen[0].planet)
+    from prometheus_amd import celestialBodies as bodies
+    planet = bodies.AvailablePlanets().findPlanet(cfg["Architecture"]["planetName"])
+    bounds = lc.band_bounds(lc.planet_shifts(planet, orb))
+    acc = lc.BandAccumulator(len(orb))
+    for a, b in ((0, 700), (700, 1500), (1500, len(wav))):          # three "shards"
+        w = wav[a:b]
+        sel = np.zeros((len(orb), b - a), dtype=bool)
+        for k in range(bounds.shape[1]):
+            sel |= (w[None, :] >= bounds[:, k, 0:1]) & (w[None, :] <= bounds[:, k, 1:2])
+        acc.add((R[:, a:b] * sel).sum(axis=1), sel.sum(axis=1), R[:, a:b].max(axis=1))
+    got = acc.lightcurve()
+    assert np.all(acc.count > 0)
+    assert np.max(np.abs(got / ref - 1)) < 1e-13
