@@ -20,6 +20,7 @@ for s in $STEPS; do
   case $s in
     tests) step pytest_gpu 900 python -m pytest tests -q -m gpu -rA ;;
     rmtests) step pytest_rm 600 python -m pytest tests -q -m gpu -rA -k "stellar or native_loaded" -s ;;
+    newtests) step pytest_new 600 python -m pytest tests -q -m gpu -rA -k "${KSEL:-native_loaded}" -s ;;
     rmbench) step rm_bench 600 python tools/rm_bench.py C2 --runs 3 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
