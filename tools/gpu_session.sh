@@ -25,6 +25,7 @@ for s in $STEPS; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     benchfast) step bench 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    traffic) step traffic 700 bash tools/bench_traffic.sh ${TAG:-r01c} ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
   esac
 done
