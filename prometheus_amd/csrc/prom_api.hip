@@ -537,6 +537,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       }
       rs.evals.ensure(sizeof(unsigned long long) * 64);
       rs.sig.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * tr.n_wav);
+      const int64_t n_wtiles = (tr.n_wav + 127) / 128;
+      rs.tq.ensure(sizeof(float) * 2 * n_wtiles);
+      rs.win.ensure(sizeof(int32_t) * 2 * n_orb * n_wtiles);
       rs.tsum.ensure(sizeof(double) * n_orb);
       rs.fsum.ensure(sizeof(double) * n_orb);
       rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);

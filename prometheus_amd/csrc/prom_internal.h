@@ -174,6 +174,8 @@ struct RunSlot {
   DevBuf wmom;                              // [n_orb][n_pr + 1][K] suffix tail moments
   DevBuf evals;                             // [64] uint64 exp-evaluation counters (stats runs)
   DevBuf sig;                               // no orbital Doppler shift: sigma_s(lambda_w) [n_atoms][n_wav]
+  DevBuf tq;                                // no orbital Doppler shift: Q range per 128-lambda tile [n_tiles] float2
+  DevBuf win;                               // ... and each tile's tau window {h, t} per phase [n_orb][n_tiles] int2
   DevBuf R;                                 // [n_orb][n_wav]
 };
 

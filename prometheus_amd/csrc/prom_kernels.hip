@@ -25,6 +25,8 @@
 namespace prom {
 
 constexpr int kBlock = 256;
+constexpr int kTW = 128;   // k_tau_w: wavelengths per workgroup (one window tile)
+constexpr int kTP = 4;     // k_tau_w: phases per workgroup (one per wavefront)
 
 // Optional in-kernel timing (build with -DPROM_TRACE, tools/trace_kernels.py): wall-clock stamps
 // (100 MHz) of workgroup 0's steps and per-wavefront cycle counters in a device array.
@@ -553,7 +555,7 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
                                  const double* __restrict__ moon_R, const double* __restrict__ sig_max,
                                  double cull, double* __restrict__ ncol, int32_t* __restrict__ flags,
                                  const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
-                                 double* __restrict__ sig) {
+                                 double* __restrict__ sig, float2* __restrict__ tq) {
   // Eight lanes per chord; lane j holds samples j, j + 8, ..., j + 8 (SPL - 1).  That is numpy's
   // pairwise_sum layout (loops_utils.h.src) for 8 <= n_x < 128: lane j accumulates r[j] = a[j] +
   // a[j+8] + ... sequentially, the eight partial sums combine as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
@@ -564,12 +566,39 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
     // trailing workgroups: sigma_s(shift_s lambda_w) for problems without orbital Doppler shift
     const unsigned cb = (unsigned)(((int64_t)n_orb * n_pr + G - 1) / G);
     if (blockIdx.x >= cb) {
+      // ... and each kTW-wavelength tile's range of Q = sum_s max(sigma_s / c_s, 0) (float, widened by
+      // 2^-20; {-1, 0} when Q is not finite), from which k_order picks the tile's tau window.  Lanes
+      // past n_wav take the last wavelength, as k_tau_w's do.
+      __shared__ float tqs[kBlock / 64][2];
+      __shared__ int32_t tqb[kBlock / 64];
       const int64_t w = (int64_t)(blockIdx.x - cb) * kBlock + threadIdx.x;
-      if (w < n_wav) {
-        const double lam = wav[w];
+      const bool live = w < n_wav;
+      const double lam = wav[live ? w : n_wav - 1];
+      double Q = 0.0;
 #pragma unroll
-        for (int s = 0; s < NSIG; ++s)
-          sig[(int64_t)s * n_wav + w] = sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
+      for (int s = 0; s < NSIG; ++s) {
+        const double sv = sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
+        if (live) sig[(int64_t)s * n_wav + w] = sv;
+        const double qs = sv * tabv.t[s].nscale;
+        Q += qs > 0.0 ? qs : 0.0;
+      }
+      const float qf = (float)Q;
+      float qh = qf * (1.0f + 0x1p-20f), ql = qf * (1.0f - 0x1p-20f);
+      for (int off = 32; off > 0; off >>= 1) {
+        qh = fmaxf(qh, __shfl_xor(qh, off, 64));
+        ql = fminf(ql, __shfl_xor(ql, off, 64));
+      }
+      const bool bad = __ballot(!(Q <= 1.0e100)) != 0ull;
+      const int wv = threadIdx.x >> 6;
+      if ((threadIdx.x & 63) == 0) { tqs[wv][0] = ql; tqs[wv][1] = qh; tqb[wv] = bad ? 1 : 0; }
+      __syncthreads();
+      static_assert(kBlock == 2 * kTW, "two window tiles per sigma workgroup");
+      if (threadIdx.x < 2) {
+        const int a = 2 * threadIdx.x;
+        const int64_t tl = 2 * (int64_t)(blockIdx.x - cb) + threadIdx.x;
+        if (tl * kTW < n_wav)
+          tq[tl] = (tqb[a] | tqb[a + 1]) ? make_float2(-1.0f, 0.0f)
+                                         : make_float2(fminf(tqs[a][0], tqs[a + 1][0]), fmaxf(tqs[a][1], tqs[a + 1][1]));
       }
       return;
     }
@@ -903,6 +932,15 @@ __device__ __forceinline__ int32_t env_slot(double v) {
 }
 constexpr double kTauSat = 40.0;
 
+// Table index of a positive float threshold: the largest v with X_v = double(bits v << 49) <= x;
+// below the table for zero/denormal x, above it for +inf.
+__device__ __forceinline__ int env_floor(float x) {
+  if (!(x >= 1.17549435e-38f)) return -(1 << 28);
+  if (!(x <= 3.40282347e+38f)) return 1 << 28;
+  return (int)(__builtin_bit_cast(uint32_t, x) >> 20) + 7168;
+}
+
+
 template <int NS>
 struct Monos {
   static constexpr int K = (NS + 1) * (NS + 2) * (NS + 3) / 6;
@@ -1021,7 +1059,9 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
                                                    double* __restrict__ tfrac,
                                                    double* __restrict__ fsum,
                                                    int32_t* __restrict__ wenv,
-                                                   double* __restrict__ wmom) {
+                                                   double* __restrict__ wmom,
+                                                   const float2* __restrict__ tq, int32_t n_tiles,
+                                                   int2* __restrict__ win) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
@@ -1396,6 +1436,32 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         et[tid * PT + k] = cb[k] + bc;
         et[kEnvN + tid * PT + k] = ca_[k] + ac;
       }
+      if (tq) {
+        // the tables stay in LDS (over the histograms) for the per-tile windows below
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+          hB[tid * PT + k] = cb[k] + bc;
+          hA[tid * PT + k] = ca_[k] + ac;
+        }
+      }
+    }
+  }
+  if (tq) {
+    // ---- 7. tau window [h, t) of every wavelength tile for this phase (no orbital Doppler shift:
+    //         Q per tile from k_columns8), exactly as k_tau_w would pick it from the tables
+    __syncthreads();
+    const bool wtab = sorted && window;
+    for (int32_t tl = tid; tl < n_tiles; tl += kWBlock) {
+      const float2 q = tq[tl];
+      int32_t h = 0, t = sorted ? G : nact;
+      if (wtab && q.x >= 0.0f) {
+        const int vt = env_floor((float)kTailEps / q.y * (1.0f - 0x1p-20f));
+        const int vh = env_floor((float)kTauSat / q.x * (1.0f + 0x1p-20f));
+        t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : hB[vt - kEnvVmin]);
+        h = vh >= kEnvVmax ? 0 : hA[vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin];
+      }
+      win[(int64_t)o * n_tiles + tl] = make_int2(h < t ? h : t, t);
     }
   }
   if (tid == 0) {
@@ -1461,14 +1527,6 @@ __device__ __forceinline__ double acc_exp256(double acc, double F, double y, con
 
 __device__ __forceinline__ void fill_exp_table(double* etab) {
   for (int i = threadIdx.x; i < PROM_EXP2_TABLE_N; i += kBlock) etab[i] = kExp2TableDev[i];
-}
-
-// Table index of a positive float threshold: the largest v with X_v = double(bits v << 49) <= x;
-// below the table for zero/denormal x, above it for +inf.
-__device__ __forceinline__ int env_floor(float x) {
-  if (!(x >= 1.17549435e-38f)) return -(1 << 28);
-  if (!(x <= 3.40282347e+38f)) return 1 << 28;
-  return (int)(__builtin_bit_cast(uint32_t, x) >> 20) + 7168;
 }
 
 // Fused sigma lookup -> tau -> exp(-tau) -> disk sum -> ratio.
@@ -1684,8 +1742,6 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabs4 tabv, const SigTa
 //      Doppler shift): sigma was resampled once per wavelength by the column kernel, one load;
 //   4. the wavefront's window [h, t): threshold tables at its Q range (DPP max/min);
 //   5. records [h, t) and the tail moments at t (scalar loads, shared by the 4 wavelengths of a lane).
-constexpr int kTW = 128;   // wavelengths per workgroup
-constexpr int kTP = 4;     // phases per workgroup (one per wavefront)
 constexpr int kLPT = kTW / 64;
 
 template <int NS, bool UNI>
@@ -1701,6 +1757,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
                                                   const int32_t* __restrict__ wenv,
                                                   const double* __restrict__ wmom,
                                                   const double* __restrict__ sig,
+                                                  const int2* __restrict__ win, int32_t n_tiles,
                                                   unsigned long long* __restrict__ evals,
                                                   double* __restrict__ R) {
   constexpr Monos<NS> M{};
@@ -1724,6 +1781,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
     live[j] = w < n_wav;
     lam[j] = wav[live[j] ? w : n_wav - 1];
   }
+  int2 hw = make_int2(0, 0);
+  if constexpr (UNI) hw = win[(int64_t)oo * n_tiles + blockIdx.x];   // window chosen by k_order
   const int32_t* cp = counts + oo * kCnt;
   const int32_t cA = cp[0], cG = cp[4];
   const int32_t cF = (cp[5] ? 1 : 0) | (cp[6] ? 2 : 0) | (cp[3] ? 4 : 0);
@@ -1749,35 +1808,43 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
   __syncthreads();   // sexp
   if (!ph) return;
   PROM_CLK(tk1);
-  // ---- 4. window (q_s = sigma_s / c_s, Q = sum_s max(q_s, 0))
-  bool bad = false;
-  float qh = 0.0f, ql = 3.4e38f;
-#pragma unroll
-  for (int j = 0; j < kLPT; ++j) {
-    double Qj = 0.0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const double qs = sg[j][s] * tabv.t[s].nscale;
-      Qj += qs > 0.0 ? qs : 0.0;
-    }
-    bad = bad || !(Qj <= 1.0e100);
-    const float qf = (float)Qj;
-    qh = fmaxf(qh, qf * (1.0f + 0x1p-20f));
-    ql = fminf(ql, qf * (1.0f - 0x1p-20f));
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    qh = fmaxf(qh, __shfl_xor(qh, off, 64));
-    ql = fminf(ql, __shfl_xor(ql, off, 64));
-  }
-  bad = __ballot(bad) != 0ull;
+  // ---- 4. window (q_s = sigma_s / c_s, Q = sum_s max(q_s, 0)); without orbital Doppler shift k_order
+  //         has already picked it per tile
   const int32_t G = cG;
-  int32_t h = 0, t = (cF & 1) ? G : cA;
-  if ((cF & 2) && !bad) {
-    const int vt = env_floor((float)kTailEps / qh * (1.0f - 0x1p-20f));
-    const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
-    const int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
-    t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : et[vt - kEnvVmin]);
-    h = vh >= kEnvVmax ? 0 : et[kEnvN + (vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin)];
+  int32_t h, t;
+  if constexpr (UNI) {
+    h = hw.x;
+    t = hw.y;
+  } else {
+    bool bad = false;
+    float qh = 0.0f, ql = 3.4e38f;
+#pragma unroll
+    for (int j = 0; j < kLPT; ++j) {
+      double Qj = 0.0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const double qs = sg[j][s] * tabv.t[s].nscale;
+        Qj += qs > 0.0 ? qs : 0.0;
+      }
+      bad = bad || !(Qj <= 1.0e100);
+      const float qf = (float)Qj;
+      qh = fmaxf(qh, qf * (1.0f + 0x1p-20f));
+      ql = fminf(ql, qf * (1.0f - 0x1p-20f));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      qh = fmaxf(qh, __shfl_xor(qh, off, 64));
+      ql = fminf(ql, __shfl_xor(ql, off, 64));
+    }
+    bad = __ballot(bad) != 0ull;
+    h = 0;
+    t = (cF & 1) ? G : cA;
+    if ((cF & 2) && !bad) {
+      const int vt = env_floor((float)kTailEps / qh * (1.0f - 0x1p-20f));
+      const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
+      const int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
+      t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : et[vt - kEnvVmin]);
+      h = vh >= kEnvVmax ? 0 : et[kEnvN + (vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin)];
+    }
   }
   h = __builtin_amdgcn_readfirstlane(h < t ? h : t);
   t = __builtin_amdgcn_readfirstlane(t);
@@ -2297,7 +2364,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   const bool wpath = tr.exp_mode && tr.n_mol == 0 && tr.n_atoms >= 1 && tr.n_atoms <= kWinMaxSpecies;
   // no orbital Doppler shift: sigma_s(lambda_w) is resampled once per wavelength by extra workgroups
   // of the column kernel (they run beside the chord work) instead of once per phase group
-  const bool pre_sigma = wpath && tr.window && tr.uniform_shift && !tr.star;
+  const bool cols8 = tr.n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4;
+  const bool pre_sigma = cols8 && wpath && tr.window && tr.uniform_shift && !tr.star;
   const int32_t na = tr.n_atoms;
   *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? (wpath && tr.window ? 20 : 10) : 0);
   // stage events ride on the fast path's dispatch packets (hipExtLaunchKernelGGL start/stop events):
@@ -2306,7 +2374,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   hipEvent_t ev1 = (ev && stage_events) ? ev[1] : nullptr;
   // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
-  if (tr.n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4) {
+  if (cols8) {
     const unsigned sig_blocks = pre_sigma ? grid_for(tr.n_wav) : 0u;
 #define PROM_COLS(SV, NSV)                                                                               \
   hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
@@ -2316,7 +2384,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
                      tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
                      tr.moon_R.as<double>(), tr.sigma_max_dev.as<double>(), tr.cull_tau, rs.ncol.as<double>(), \
-                     rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>())
+                     rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>(), \
+                     pre_sigma ? rs.tq.as<float2>() : nullptr)
 #define PROM_COLS_L(NSV)                       \
   if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
   else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
@@ -2388,7 +2457,9 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     PROM_HIP(hipGetLastError());
     return;
   }
-  // 2. per-phase compaction, ordering, merging of equal-column chords, window tables
+  // 2. per-phase compaction, ordering, merging of equal-column chords, window tables (and, without
+  //    orbital Doppler shift, every tile's window)
+  const int32_t n_wtiles = (int32_t)((tr.n_wav + kTW - 1) / kTW);
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
   hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev1, 0,                \
@@ -2396,7 +2467,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
                      tr.window ? 1 : 0, tr.sigtab_v, rs.recs.as<double>(),                               \
                      rs.act_ip.as<int32_t>(), rs.mrecs.as<double>(), rs.counts.as<int32_t>(),            \
-                     rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>())
+                     rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>(), \
+                     pre_sigma ? rs.tq.as<float2>() : nullptr, n_wtiles, rs.win.as<int2>())
     switch (tr.n_atoms) {
       case 1: PROM_CHW(1); break;
       case 2: PROM_CHW(2); break;
@@ -2475,7 +2547,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0,                  \
                      tr.sigtab_v, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                     \
                      tr.n_orb, tr.n_wav, rs.wenv.as<int32_t>(), rs.wmom.as<double>(), rs.sig.as<double>(),  \
-                     tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
+                     rs.win.as<int2>(), n_wtiles, tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
 #define PROM_TAUW_NS(PMV, UV)            \
   switch (na) {                          \
     case 1: PROM_TAUW(1, PMV, UV); break; \

@@ -296,3 +296,17 @@ def test_band_lightcurve(dev, name):
     assert rel(lc1, ref) < R_TOL and rel(lc2, ref) < R_TOL
     assert rel(R, d["R"]) < R_TOL
     print(name, "light curve", lc1)
+
+
+def test_many_los_samples_generic_columns(dev):
+    """n_x > 64 takes the generic density / column kernels (k_ntot + k_columns) in front of the
+    windowed tau kernel; checked against the oracle."""
+    from prometheus_amd import configs
+    cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
+                          res_low=5e-9, res_high=1e-10)
+    cfg["Grids"]["x_steps"] = 80
+    tr = _product_transit(cfg)
+    R = tr.sumOverChords(devices=[0])
+    scen, dop, grids = O.from_setup(cfg)
+    Ro = O.transit_depth(scen, dop, grids, tr.wavelength, O.build_tables(scen, grids))
+    assert rel(R, Ro) < R_TOL
