@@ -63,21 +63,25 @@ def global_config(name: str, world: int) -> dict:
     return cfg
 
 
+TAU_TIMING_STRIDE = 8
+
+
 def flops_per_eval(n_atoms: int) -> int:
-    """FP64 flops (FMA = 2) of one exact chord-wavelength evaluation in k_tau_w's window:
-    y = -tau 256/ln2 = sum_s N_s sy_s -> 2S - 1;  2^(y/256): rint, d = y - k, 5-FMA polynomial, ldexp -> 13;
-    F * S -> 1;  acc fma -> 2."""
-    return 2 * n_atoms - 1 + 16
+    """FP64 flops (FMA = 2) of one exact chord-wavelength evaluation in the tau kernel's window
+    (DESIGN.md): y = -tau 1024/ln2 = sum_s N_s sy_s -> 2S - 1;  2^(y/1024): rint, d = y - k, 3-FMA
+    polynomial, ldexp -> 9;  F * S -> 1;  acc fma -> 2."""
+    return 2 * n_atoms - 1 + 12
 
 
-def tau_bytes_per_launch(n_wav: int, n_orb: int, n_atoms: int) -> int:
-    """Algorithmic HBM bytes of one k_tau_w launch (DESIGN.md "Roofline"): R[n_orb][n_wav] written,
-    lambda and sigma_s (resampled by the column kernel) read once per wavelength; window records and
-    tail moments (<= 1 %) are not counted."""
-    return 8 * n_orb * n_wav + 8 * n_wav * (1 + n_atoms)
+def tau_bytes_per_launch(n_wav: int, n_orb: int, n_sigma: int) -> int:
+    """Algorithmic HBM bytes of one tau-kernel launch (DESIGN.md "Roofline"): R[n_orb][n_wav] written
+    and the n_sigma cross-section arrays the column kernel resampled (one per species, or one for
+    merged species) read once per wavelength; window records, windows and tail moments (~1 %) are not
+    counted."""
+    return 8 * n_orb * n_wav + 8 * n_wav * n_sigma
 
 
-def latest_profile_traffic(kernel: str = "prom::k_tau_w"):
+def latest_profile_traffic(kernel: str = "prom::k_tau_p"):
     """Measured HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC summary
     (profiles/*traffic_all_kernels.json, tools/bench_traffic.sh), or None."""
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*traffic_all_kernels.json")), reverse=True):
@@ -159,7 +163,9 @@ def main():
     if dist:
         dist.barrier()
     sync()
-    dev.timing_begin()
+    # the tau kernel's duration is sampled on every TAU_TIMING_STRIDE-th run (events on a dispatch cost
+    # the host ~13 us, more than a run's GPU time: timing every run would measure the host)
+    dev.timing_begin(stride=TAU_TIMING_STRIDE)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         dev.transit_run()
@@ -172,16 +178,19 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_pts * args.steps / elapsed
 
-    # dominant kernel: k_tau_w (windowed tau/exp/disk-sum); mean launch duration from the start/stop
-    # events carried on its own dispatch packets over the timed runs
+    # dominant kernel: k_tau_p (planned windowed tau/exp/disk-sum; k_tau_w when the planned path does
+    # not apply); mean launch duration from the start/stop events carried on its own dispatch packets
+    # over the timed runs
+    tau_kernel = "k_tau_p" if st.get("tau_kernel_variant", 0) // 10 == 3 else "k_tau_w"
     tau_ms = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
-    n_atoms = prob.n_atoms
+    # species the tau kernel integrates: variant = 10 * path + effective species (merged species: 1)
+    n_atoms = st["tau_kernel_variant"] % 10 or prob.n_atoms
     cle = st["chord_lambda_evals"]
     evals = st["exp_evals"]
     tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, n_atoms)
     achieved_gbs = tau_bytes / (tau_ms * 1e-3) / 1e9
     flops = evals * flops_per_eval(n_atoms)
-    traffic = latest_profile_traffic()
+    traffic = latest_profile_traffic("prom::" + tau_kernel)
     # end-to-end (host prep + H2D + run + D2H) for reference, one call
     t_e2e = time.perf_counter()
     R = tr.sumOverChords(devices=[local_rank]) if world == 1 else None
@@ -204,9 +213,10 @@ def main():
                    "global_wavelengths": n_wav_global, "orbital_phases": n_orb,
                    "chords_per_phase": len(host["y"]), "los_samples": len(host["x"]),
                    "parallelism": "wavelength shards x%d (no collective)" % world},
-        "roofline": {"bound": "hbm", "kernel": "k_tau_w", "achieved": achieved_gbs,
+        "roofline": {"bound": "hbm", "kernel": tau_kernel, "achieved": achieved_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
                      "traffic": traffic, "algorithmic_bytes": tau_bytes, "tau_ms": tau_ms,
+                     "tau_ms_sampled_runs": int(len(ms_runs)),
                      "exp_evals": evals, "chord_lambda_evals": cle,
                      "valu": {"flops": flops, "flops_per_exp_eval": flops_per_eval(n_atoms),
                               "achieved_tflops": flops / (tau_ms * 1e-3) / 1e12,

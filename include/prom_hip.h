@@ -216,9 +216,13 @@ int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bo
 /* Live per-run timing of the tau kernel without per-run synchronisation: between prom_timing_begin
  * and prom_timing_end every prom_transit_run carries start/stop events on its tau kernel's dispatch;
  * prom_timing_end waits for them and returns ms[run][4] = {NaN, NaN, tau, NaN} for up to max_runs
- * runs (n_runs receives the count).  Stage times of a single run come from prom_transit_run's stats. */
+ * runs (n_runs receives the count).  Stage times of a single run come from prom_transit_run's stats.
+ * prom_timing_stride(ctx, k) (k >= 1, default 1, kept until changed) times only every k-th run of the
+ * window: events on a dispatch cost the host ~13 us, more than a run's GPU time, so a throughput
+ * measurement samples the kernel durations instead of timing every run. */
 int32_t prom_timing_begin(prom_ctx* ctx);
 int32_t prom_timing_end(prom_ctx* ctx, int32_t max_runs, double* ms, int32_t* n_runs);
+int32_t prom_timing_stride(prom_ctx* ctx, int32_t stride);
 
 #ifdef __cplusplus
 }

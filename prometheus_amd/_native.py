@@ -106,6 +106,7 @@ SIGNATURES = {
     "prom_transit_band_stats": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _dp, C.POINTER(C.c_int64), _dp]),
     "prom_timing_begin": (C.c_int32, [C.c_void_p]),
     "prom_timing_end": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _ip]),
+    "prom_timing_stride": (C.c_int32, [C.c_void_p, C.c_int32]),
 }
 
 _lib = None
@@ -268,7 +269,9 @@ class Device:
         self._check(self.lib.prom_transit_result(self.h, _d(out)), "prom_transit_result")
         return out
 
-    def timing_begin(self):
+    def timing_begin(self, stride: int = 1):
+        """Start a timing window; events ride on every ``stride``-th run's tau dispatch."""
+        self._check(self.lib.prom_timing_stride(self.h, int(stride)), "prom_timing_stride")
         self._check(self.lib.prom_timing_begin(self.h), "prom_timing_begin")
 
     def timing_end(self, max_runs: int = 4096) -> np.ndarray:

@@ -316,6 +316,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.exp_mode = (pb->options & PROM_OPT_OCML_EXP) ? 0 : 1;
     tr.merge = (pb->options & PROM_OPT_NO_MERGE) == 0;
     tr.window = (pb->options & PROM_OPT_NO_WINDOW) == 0;
+    {
+      const char* e = std::getenv("PROM_TAU_PLAN");
+      tr.plan = !(e && std::atoi(e) == 0);
+      const char* m = std::getenv("PROM_SPECIES_MERGE");
+      tr.species_merge_ok = !(m && std::atoi(m) == 0);   // narrowed below
+    }
     PROM_REQUIRE(pb->n_pr < (1 << 24), "transit: n_pr must be < 2^24");
     tr.terms.clear();
     tr.dens.clear();
@@ -425,7 +431,37 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         const double inv = (c > 0.0 && std::isfinite(c)) ? bound : 0.0;
         st.push_back({tb.x.as<double>(), tb.y.as<double>(), tb.n, tb.offset,
                       tr.shift.as<double>() + (int64_t)t.scenario * n_orb, tb.dir.as<int32_t>(), tb.n_dir, 0,
-                      tb.dir_x0, tb.dir_inv_h, std::isfinite(c) ? c : 0.0, inv});
+                      tb.dir_x0, tb.dir_inv_h, std::isfinite(c) ? c : 0.0, inv, t.chi});
+      }
+      // species merging: one scenario carries every atomic constituent (and there are >= 2 of them)
+      int32_t sc0 = -1;
+      bool one_sc = n_atoms >= 2 && n_mol == 0;
+      double smax_m = 0.0;
+      for (const auto& t : tr.terms) {
+        if (t.is_molecule) continue;
+        if (sc0 < 0) sc0 = t.scenario;
+        if (t.scenario != sc0 || !(std::isfinite(t.chi) && t.chi >= 0.0)) one_sc = false;
+        smax_m += t.chi * tr.atom_sigma_max[t.slot];
+      }
+      tr.species_merge_ok = tr.species_merge_ok && one_sc && tr.n_sc <= 4;
+      if (tr.species_merge_ok) {
+        const double bound = nref[sc0] * (double)tr.n_x * tr.delta_x;
+        const double c = (bound > 0.0 && std::isfinite(bound)) ? 1.0 / bound : 0.0;
+        if (!std::isfinite(bound) || (bound > 0.0 && !(c > 0.0)) || !std::isfinite(smax_m)) tr.species_merge_ok = false;
+        tr.sigtab_m = prom::SigTabs4{};
+        tr.sigtab_m.t[0] = st[0];
+        tr.sigtab_m.t[0].ncoef = std::isfinite(c) ? c : 0.0;
+        tr.sigtab_m.t[0].nscale = (c > 0.0 && std::isfinite(c)) ? bound : 0.0;
+        tr.sigtab_m.t[0].chi = 1.0;
+        tr.colargs_m = prom::ColArgs{};
+        prom::TermDev tm{};
+        tm.scenario = sc0;
+        tm.is_molecule = 0;
+        tm.slot = 0;
+        tm.table = -1;
+        tm.chi = 1.0;
+        tr.colargs_m.t[0] = tm;
+        upload(tr.sigma_max_m, &smax_m, 1, s);
       }
       upload(tr.sigtab, st.data(), (int64_t)st.size(), s);
       tr.uniform_shift = true;
@@ -505,6 +541,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       upload(tr.scdev, sd.data(), (int64_t)sd.size(), s);
       tr.colargs = prom::ColArgs{};
       for (int32_t i = 0; i < tr.n_sc && i < 4; ++i) tr.colargs.sc[i] = sd[i];
+      for (int32_t i = 0; i < tr.n_sc && i < 4; ++i) tr.colargs_m.sc[i] = sd[i];
       for (int32_t i = 0; i < tr.n_terms && i < 8; ++i) tr.colargs.t[i] = tr.terms[i];
     }
     for (int32_t sc = 0; sc < tr.n_sc; ++sc)
@@ -533,13 +570,17 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       rs.mrecs.ensure(sizeof(double) * nc * (1 + n_atoms));
       if (n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && n_mol == 0) {
         rs.wenv.ensure(sizeof(int32_t) * n_orb * 2 * prom::kEnvN);
-        rs.wmom.ensure(sizeof(double) * n_orb * (tr.n_pr + 1) * prom::n_tail_moments(n_atoms));
+        rs.wmom.ensure(sizeof(double) * n_orb * (tr.n_pr + 1) *
+                       std::max(prom::n_tail_moments(n_atoms), prom::n_tail_moments(1)));   // merged species: 1
       }
       rs.evals.ensure(sizeof(unsigned long long) * 64);
       rs.sig.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * tr.n_wav);
       const int64_t n_wtiles = (tr.n_wav + 127) / 128;
       rs.tq.ensure(sizeof(float) * 2 * n_wtiles);
       rs.win.ensure(sizeof(int32_t) * 2 * n_orb * n_wtiles);
+      rs.hlist.ensure(sizeof(int32_t) * 4 * n_orb * n_wtiles);
+      rs.hcnt.ensure(sizeof(int32_t) * n_orb);
+      tr.taup_resident = 0;
       rs.tsum.ensure(sizeof(double) * n_orb);
       rs.fsum.ensure(sizeof(double) * n_orb);
       rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);
@@ -556,7 +597,8 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     if (!tr.ready) throw Error(PROM_E_STATE, "prom_transit_run: call prom_transit_set first");
     int variant = 0;
     hipEvent_t* ev = ctx->ev;
-    if (ctx->timing) {
+    const bool timed = ctx->timing && (ctx->window_runs++ % ctx->timing_stride) == 0;
+    if (timed) {
       const size_t need = 4 * (size_t)(ctx->timed_runs + 1);
       while (ctx->tev.size() < need) {
         hipEvent_t e;
@@ -573,7 +615,7 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     const hipStream_t st = ctx->streams[si];
     prom::RunSlot& rs = tr.slot[si];
     if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
-    prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, (stats || ctx->timing) ? ev : nullptr, &variant,
+    prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, (stats || timed) ? ev : nullptr, &variant,
                          stats != nullptr);
     tr.last = si;
     tr.count_evals = false;
@@ -668,6 +710,14 @@ int32_t prom_timing_begin(prom_ctx* ctx) {
   return guarded(ctx, [&] {
     ctx->timing = true;
     ctx->timed_runs = 0;
+    ctx->window_runs = 0;
+  });
+}
+
+int32_t prom_timing_stride(prom_ctx* ctx, int32_t stride) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(stride >= 1, "prom_timing_stride: stride must be >= 1");
+    ctx->timing_stride = stride;
   });
 }
 

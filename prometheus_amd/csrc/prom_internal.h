@@ -61,11 +61,12 @@ constexpr int kCnt = 8;   // int32 counters per phase in TransitDev::counts
 
 // Windowed integration (prom_kernels.hip, "windowed integration"): per-phase ordering limit, the
 // size of the per-phase threshold -> record-index tables, and the number of tail moments for S
-// atomic species (monomials of total degree <= 3 in S variables).
+// atomic species.
 constexpr int kWinMax = 4096;
 constexpr int kEnvN = 2048;
 constexpr int kWinMaxSpecies = 4;
-inline int n_tail_moments(int S) { return (S + 1) * (S + 2) * (S + 3) / 6; }
+// (prom_kernels.hip Monos / TailDeg: degree 7 for one effective species, 3 otherwise)
+inline int n_tail_moments(int S) { return S == 1 ? 8 : (S + 1) * (S + 2) * (S + 3) / 6; }
 
 // Stellar-spectrum path: star-table nodes a tau workgroup stages in LDS (prom_api.hip rm_slices).
 constexpr int kRmStarMax = 1024;
@@ -105,6 +106,7 @@ struct SigTabDev {
   double dir_x0, dir_inv_h;
   double ncoef;          // c_s: column normalisation of the windowed integration (n = c_s N <= 1)
   double nscale;         // 1 / c_s (0 when c_s == 0)
+  double chi;            // the constituent's mixing ratio (species merging: Y = sum_s chi_s sigma_s)
 };
 
 // Per molecular slot of a transit problem.
@@ -176,6 +178,9 @@ struct RunSlot {
   DevBuf sig;                               // no orbital Doppler shift: sigma_s(lambda_w) [n_atoms][n_wav]
   DevBuf tq;                                // no orbital Doppler shift: Q range per 128-lambda tile [n_tiles] float2
   DevBuf win;                               // ... and each tile's tau window {h, t} per phase [n_orb][n_tiles] int2
+  DevBuf hlist;                             // ... (tile, phase) units with long windows {tile, h, t, flags}
+                                            //     [n_orb][n_tiles] int4, listed per phase by k_order
+  DevBuf hcnt;                              // ... their count per phase [n_orb] int32
   DevBuf R;                                 // [n_orb][n_wav]
 };
 
@@ -210,6 +215,16 @@ struct TransitDev {
   bool window = true;                       // windowed integration with tail moments
   bool uniform_shift = false;               // every atomic species' Doppler factor equal at all phases
   bool count_evals = false;
+  bool plan = true;                         // planned tau integration where it applies (PROM_TAU_PLAN=0: off)
+  // Species merging (PROM_SPECIES_MERGE=0: off): when every atomic constituent belongs to one density
+  // scenario, tau_c(lambda) = N_c Y(lambda) with N_c = dx sum_x n and Y = sum_s chi_s sigma_s, so the
+  // no-Doppler fast path integrates one effective absorber: one column per chord, one resampled
+  // cross-section per wavelength, scalar windows and 4 tail moments.
+  bool species_merge_ok = false;
+  ColArgs colargs_m{};                      // the single chi = 1 term
+  SigTabs4 sigtab_m{};                      // t[0]: the effective absorber's normalisation (ncoef, nscale)
+  DevBuf sigma_max_m;                       // [1] sum_s chi_s sigma_max_s
+  int32_t taup_resident = 0;                // k_tau_p wavefronts resident at once (set at the first run)
   DevBuf molslot;                           // [n_mol] MolSlotDev
   DevBuf mol_ip;                            // [n_mol][n_orb][n_pr][n_x] int32 P bracket (-1: out of table)
   DevBuf mol_wp;                            // [n_mol][n_orb][n_pr][n_x] P weight
@@ -243,6 +258,8 @@ struct prom_ctx {
   bool timing = false;
   std::vector<hipEvent_t> tev;   // pool, 4 per timed run
   int32_t timed_runs = 0;
+  int32_t timing_stride = 1;     // prom_timing_stride: events on every k-th run of a timing window
+  int64_t window_runs = 0;       // runs since prom_timing_begin
 };
 
 namespace prom {

@@ -27,6 +27,7 @@ namespace prom {
 constexpr int kBlock = 256;
 constexpr int kTW = 128;   // k_tau_w: wavelengths per workgroup (one window tile)
 constexpr int kTP = 4;     // k_tau_w: phases per workgroup (one per wavefront)
+constexpr int kHeavy = 8;  // k_tau_p: windows longer than this go to the heavy wavefronts
 
 // Optional in-kernel timing (build with -DPROM_TRACE, tools/trace_kernels.py): wall-clock stamps
 // (100 MHz) of workgroup 0's steps and per-wavefront cycle counters in a device array.
@@ -555,7 +556,8 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
                                  const double* __restrict__ moon_R, const double* __restrict__ sig_max,
                                  double cull, double* __restrict__ ncol, int32_t* __restrict__ flags,
                                  const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
-                                 double* __restrict__ sig, float2* __restrict__ tq) {
+                                 double* __restrict__ sig, float2* __restrict__ tq, int32_t merge_sp,
+                                 double nscale_m) {
   // Eight lanes per chord; lane j holds samples j, j + 8, ..., j + 8 (SPL - 1).  That is numpy's
   // pairwise_sum layout (loops_utils.h.src) for 8 <= n_x < 128: lane j accumulates r[j] = a[j] +
   // a[j+8] + ... sequentially, the eight partial sums combine as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
@@ -575,12 +577,22 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
       const bool live = w < n_wav;
       const double lam = wav[live ? w : n_wav - 1];
       double Q = 0.0;
+      if (merge_sp) {
+        // species merging: the effective absorber's cross-section Y = sum_s chi_s sigma_s
+        double Y = 0.0;
 #pragma unroll
-      for (int s = 0; s < NSIG; ++s) {
-        const double sv = sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
-        if (live) sig[(int64_t)s * n_wav + w] = sv;
-        const double qs = sv * tabv.t[s].nscale;
-        Q += qs > 0.0 ? qs : 0.0;
+        for (int s = 0; s < NSIG; ++s) Y += tabv.t[s].chi * sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
+        if (live) sig[w] = Y;
+        const double qs = Y * nscale_m;
+        Q = qs > 0.0 ? qs : 0.0;
+      } else {
+#pragma unroll
+        for (int s = 0; s < NSIG; ++s) {
+          const double sv = sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
+          if (live) sig[(int64_t)s * n_wav + w] = sv;
+          const double qs = sv * tabv.t[s].nscale;
+          Q += qs > 0.0 ? qs : 0.0;
+        }
       }
       const float qf = (float)Q;
       float qh = qf * (1.0f + 0x1p-20f), ql = qf * (1.0f - 0x1p-20f);
@@ -922,7 +934,12 @@ constexpr int kWBlock = 512;
 constexpr int kWPer = kWinMax / kWBlock;           // sorted positions per thread
 constexpr int kEnvVmax = 8184;                     // bits(1.0) >> 49
 constexpr int kEnvVmin = kEnvVmax - kEnvN + 1;     // X_vmin = 2^-(kEnvN / 8)
-constexpr double kTailEps = 0x1p-10;
+// Tail of the window (records with tau < eps at every wavelength of the wavefront): the Taylor
+// polynomial of degree D in q_s over suffix moments, truncation <= eps^(D+1)/(D+1)! per unit weight.
+// One effective species (NS == 1, e.g. merged species): D = 7, eps = 2^-4 (5.8e-15); otherwise
+// D = 3, eps = 2^-10 (3.5e-14) -- (NS+D choose D) moments per record either way stays small.
+template <int NS> struct TailDeg { static constexpr int D = NS == 1 ? 7 : 3; };
+template <int NS> __host__ __device__ constexpr double tail_eps() { return NS == 1 ? 0x1p-4 : 0x1p-10; }
 
 // histogram slot of a non-negative envelope value: 1 + (table index of its 1/8-octave bucket), 0 below
 // the table, kEnvN + 1 above it.  v >= X_e  <=>  (bits(v) >> 49) >= kEnvVmin + e.
@@ -941,20 +958,28 @@ __device__ __forceinline__ int env_floor(float x) {
 }
 
 
+__host__ __device__ constexpr int binom_c(int n, int k) {
+  int r = 1;
+  for (int i = 1; i <= k; ++i) r = r * (n - k + i) / i;
+  return r;
+}
+
+// Monomials of total degree <= D in NS variables, by degree then lexicographically; c[k] = (-1)^j / prod e_s!
 template <int NS>
 struct Monos {
-  static constexpr int K = (NS + 1) * (NS + 2) * (NS + 3) / 6;
+  static constexpr int D = TailDeg<NS>::D;
+  static constexpr int K = binom_c(NS + D, D);
   int e[K][NS];
   double c[K];
   constexpr Monos() : e{}, c{} {
     int total = 1;
-    for (int s = 0; s < NS; ++s) total *= 4;
+    for (int s = 0; s < NS; ++s) total *= D + 1;
     int k = 0;
-    for (int j = 0; j <= 3; ++j)
+    for (int j = 0; j <= D; ++j)
       for (int idx = 0; idx < total; ++idx) {
         int d[NS] = {};
         int r = idx, sum = 0;
-        for (int s = NS - 1; s >= 0; --s) { d[s] = r % 4; r /= 4; sum += d[s]; }
+        for (int s = NS - 1; s >= 0; --s) { d[s] = r % (D + 1); r /= D + 1; sum += d[s]; }
         if (sum != j) continue;
         double f = 1.0;
         for (int s = 0; s < NS; ++s) {
@@ -967,14 +992,47 @@ struct Monos {
   }
 };
 
-// prod_s p[s][e_s] for monomial k (p[s][j] = x_s^j)
+// p[s][j] = v_s^j, formed as ((v v) v) ...
 template <int NS>
-__device__ __forceinline__ double mono_eval(const Monos<NS>& M, int k, const double (&p)[NS][4]) {
+__device__ __forceinline__ void tail_pows(const double (&v)[NS], double (&p)[NS][TailDeg<NS>::D + 1]) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    p[s][0] = 1.0;
+    p[s][1] = v[s];
+#pragma unroll
+    for (int j = 2; j <= TailDeg<NS>::D; ++j) p[s][j] = p[s][j - 1] * v[s];
+  }
+}
+
+// prod_s p[s][e_s] for monomial k
+template <int NS>
+__device__ __forceinline__ double mono_eval(const Monos<NS>& M, int k, const double (&p)[NS][TailDeg<NS>::D + 1]) {
   double r = 1.0;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
     if (M.e[k][s]) r *= p[s][M.e[k][s]];
   return r;
+}
+
+// The tail sum_k mm[k] q^e_k (mm already carries c[k]): Horner for one species, monomials otherwise.
+// Every tau kernel evaluates it through this function, so they agree bit for bit.
+template <int NS>
+__device__ __forceinline__ double tail_eval(const double (&mm)[Monos<NS>::K], const double (&q)[NS]) {
+  constexpr Monos<NS> M{};
+  constexpr int K = Monos<NS>::K;
+  if constexpr (NS == 1) {
+    double tl = mm[K - 1];
+#pragma unroll
+    for (int k = K - 2; k >= 0; --k) tl = __builtin_fma(tl, q[0], mm[k]);
+    return tl;
+  } else {
+    double p[NS][TailDeg<NS>::D + 1];
+    tail_pows<NS>(q, p);
+    double tl = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) tl = __builtin_fma(mm[k], mono_eval<NS>(M, k, p), tl);
+    return tl;
+  }
 }
 
 struct OpAdd { template <typename T> __device__ T operator()(T a, T b) const { return a + b; } };
@@ -1061,7 +1119,8 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
                                                    int32_t* __restrict__ wenv,
                                                    double* __restrict__ wmom,
                                                    const float2* __restrict__ tq, int32_t n_tiles,
-                                                   int2* __restrict__ win) {
+                                                   int2* __restrict__ win, int4* __restrict__ hlist,
+                                                   int32_t* __restrict__ hcnt) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
@@ -1295,7 +1354,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       bv[k] = 0.0; av[k] = 1.0e308;
       if (k >= cnt) continue;
       bool head = !merge || (i0 + k) == 0;
-      double pw[NS][4];
+      double pw[NS][TailDeg<NS>::D + 1], vv[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const double prev = k == 0 ? Np[s] : Nv[k > 0 ? k - 1 : 0][s];
@@ -1303,8 +1362,9 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         const double v = Nv[k][s] * cs[s];
         bv[k] = v > bv[k] ? v : bv[k];
         av[k] = v < av[k] ? v : av[k];
-        pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
+        vv[s] = v;
       }
+      tail_pows<NS>(vv, pw);
       Fv[k] = Fv[k] / fs;
       if (!lds_pay) sF[i0 + k] = Fv[k];   // (payload path: sF already holds F_out by position)
       sHead[i0 + k] = head ? 1 : 0;
@@ -1374,12 +1434,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       for (int k = kWPer - 1; k >= 0; --k) {
         if (k >= cnt) continue;
         if (window) {
-          double pw[NS][4];
+          double pw[NS][TailDeg<NS>::D + 1], vv[NS];
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const double v = Nv[k][s] * cs[s];
-            pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = v * v * v;
-          }
+          for (int s = 0; s < NS; ++s) vv[s] = Nv[k][s] * cs[s];
+          tail_pows<NS>(vv, pw);
 #pragma unroll
           for (int m = 0; m < K; ++m) msum[m] += Fv[k] * mono_eval<NS>(M, m, pw);
         }
@@ -1449,19 +1507,33 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   }
   if (tq) {
     // ---- 7. tau window [h, t) of every wavelength tile for this phase (no orbital Doppler shift:
-    //         Q per tile from k_columns8), exactly as k_tau_w would pick it from the tables
+    //         Q per tile from k_columns8), exactly as k_tau_w would pick it from the tables; with
+    //         hlist, the tiles whose window holds more than kHeavy records are listed for k_tau_p's
+    //         heavy wavefronts (in any order: an LDS counter)
+    __shared__ int32_t shc;
+    if (tid == 0) shc = 0;
     __syncthreads();
     const bool wtab = sorted && window;
+    const int32_t wfl = (sorted ? 1 : 0);
     for (int32_t tl = tid; tl < n_tiles; tl += kWBlock) {
       const float2 q = tq[tl];
       int32_t h = 0, t = sorted ? G : nact;
       if (wtab && q.x >= 0.0f) {
-        const int vt = env_floor((float)kTailEps / q.y * (1.0f - 0x1p-20f));
+        const int vt = env_floor((float)tail_eps<NS>() / q.y * (1.0f - 0x1p-20f));
         const int vh = env_floor((float)kTauSat / q.x * (1.0f + 0x1p-20f));
         t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : hB[vt - kEnvVmin]);
         h = vh >= kEnvVmax ? 0 : hA[vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin];
       }
-      win[(int64_t)o * n_tiles + tl] = make_int2(h < t ? h : t, t);
+      h = h < t ? h : t;
+      win[(int64_t)o * n_tiles + tl] = make_int2(h, t);
+      if (hlist && nnf == 0 && t - h > kHeavy) {
+        const int32_t k = atomicAdd(&shc, 1);
+        hlist[(int64_t)o * n_tiles + k] = make_int4(tl, h, t, wfl | ((wtab && t < G) ? 2 : 0));
+      }
+    }
+    if (hlist) {
+      __syncthreads();
+      if (tid == 0) hcnt[o] = shc;
     }
   }
   if (tid == 0) {
@@ -1522,6 +1594,25 @@ __device__ __forceinline__ double acc_exp256(double acc, double F, double y, con
   p = __builtin_fma(d, p, kE256C1);
   p = __builtin_fma(d, p, 1.0);
   const double S = __builtin_amdgcn_ldexp(tab[ki & 255], ki >> 8);
+  return __builtin_fma(F * S, p, acc);
+}
+
+// acc + F * exp(-tau) with y = -tau * 1024 / ln2 given: 2^(y/1024) = 2^(k >> 10) T[k & 1023] exp(d ln2/1024),
+// k = rint(y), d in [-1/2, 1/2], cubic Taylor polynomial (truncation (ln2/2048)^4/24 = 5.5e-16 relative),
+// T[i] = 2^(i/1024) = the 2048-entry table at 2i (LDS, 8 KB).  About 10 FP64 operations.
+constexpr double kE1024C1 = 0x1.62e42fefa39efp-11;  // (ln2/1024)^1 / 1!
+constexpr double kE1024C2 = 0x1.ebfbdff82c58fp-23;  // (ln2/1024)^2 / 2!
+constexpr double kE1024C3 = 0x1.c6b08d704a0c0p-35;  // (ln2/1024)^3 / 3!
+constexpr double kM1024Ln2 = -0x1.71547652b82fep+10; // -1024 / ln2
+
+__device__ __forceinline__ double acc_exp1024(double acc, double F, double y, const double* __restrict__ tab) {
+  const double k = __builtin_rint(y);
+  const int ki = (int)k;
+  const double d = y - k;
+  double p = __builtin_fma(d, kE1024C3, kE1024C2);
+  p = __builtin_fma(d, p, kE1024C1);
+  p = __builtin_fma(d, p, 1.0);
+  const double S = __builtin_amdgcn_ldexp(tab[ki & 1023], ki >> 10);
   return __builtin_fma(F * S, p, acc);
 }
 
@@ -1617,7 +1708,7 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabs4 tabv, const SigTa
           }
           if (__ballot(bad) == 0ull) {
             const int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
-            const int vt = env_floor((float)kTailEps / qh * (1.0f - 0x1p-20f));
+            const int vt = env_floor((float)tail_eps<NS>() / qh * (1.0f - 0x1p-20f));
             const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
             int32_t t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? n_act : et[vt - kEnvVmin]);
             int32_t h = vh >= kEnvVmax ? 0 : et[kEnvN + (vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin)];
@@ -1646,16 +1737,12 @@ __global__ void __launch_bounds__(kBlock) k_tau(const SigTabs4 tabv, const SigTa
         }
         PROM_CLK(tc3);
         if (win && i_hi < n_act) {
-          // records [t, G): cubic Taylor polynomial in q from the suffix moments
-          constexpr Monos<NS> M{};
-          const double* mm = wmom + ((int64_t)o * (n_pr + 1) + i_hi) * Monos<NS>::K;
-          double p[NS][4];
+          // records [t, G): Taylor polynomial in q from the suffix moments
+          const double* mp = wmom + ((int64_t)o * (n_pr + 1) + i_hi) * Monos<NS>::K;
+          double mm[Monos<NS>::K];
 #pragma unroll
-          for (int s = 0; s < NS; ++s) { p[s][0] = 1.0; p[s][1] = q[s]; p[s][2] = q[s] * q[s]; p[s][3] = p[s][2] * q[s]; }
-          double tl = 0.0;
-#pragma unroll
-          for (int k = 0; k < Monos<NS>::K; ++k) tl = __builtin_fma(mm[k], mono_eval<NS>(M, k, p), tl);
-          acc += tl;
+          for (int k = 0; k < Monos<NS>::K; ++k) mm[k] = mp[k];
+          acc += tail_eval<NS>(mm, q);
         }
 #ifdef PROM_TRACE
         {
@@ -1764,14 +1851,22 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
   constexpr int K = Monos<NS>::K;
   constexpr int ST = 1 + NS;
   __shared__ double srec[kTP][2 * 64 * ST];   // per wavefront: two chunks of 64 records
-  __shared__ double sexp[256];                 // 2^(i/256)
-  sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
+  __shared__ double sexp[1024];                // 2^(i/1024)
+#ifdef PROM_TRACE
+  const unsigned long long wt0 = wall_clock64();
+#endif
+  // the table's loads are issued with the first round of loads below and stored to LDS after them, so
+  // the wave does not wait for them before issuing its other loads
+  double etv[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) etv[m] = kExp2TableDev[2 * (threadIdx.x + kBlock * m)];   // kBlock == 256
   PROM_CLK(tk0);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar loads below
   const int64_t tile = (int64_t)blockIdx.x * kTW;
-  const int32_t o = blockIdx.y * kTP + wid;
-  const bool ph = o < n_orb;             // this wavefront has a phase
-  const int32_t oo = ph ? o : n_orb - 1;
+  const int32_t o_raw = blockIdx.y * kTP + wid;
+  const bool ph = o_raw < n_orb;         // this wavefront has a phase (else it mirrors the last one, unwritten)
+  const int32_t o = ph ? o_raw : n_orb - 1;
   // ---- 1.
   double lam[kLPT];
   bool live[kLPT];
@@ -1782,11 +1877,11 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
     lam[j] = wav[live[j] ? w : n_wav - 1];
   }
   int2 hw = make_int2(0, 0);
-  if constexpr (UNI) hw = win[(int64_t)oo * n_tiles + blockIdx.x];   // window chosen by k_order
-  const int32_t* cp = counts + oo * kCnt;
+  if constexpr (UNI) hw = win[(int64_t)o * n_tiles + blockIdx.x];   // window chosen by k_order
+  const int32_t* cp = counts + o * kCnt;
   const int32_t cA = cp[0], cG = cp[4];
   const int32_t cF = (cp[5] ? 1 : 0) | (cp[6] ? 2 : 0) | (cp[3] ? 4 : 0);
-  const double tf = tfrac[oo];
+  const double tf = tfrac[o];
   // ---- 2.-3. sigma
   double sg[kLPT][NS];
   if constexpr (UNI) {
@@ -1800,13 +1895,11 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
   } else {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const double sh = tabv.t[s].shift[oo];
+      const double sh = tabv.t[s].shift[o];
 #pragma unroll
       for (int j = 0; j < kLPT; ++j) sg[j][s] = sigma_of(sh * lam[j], tabv.t[s]);
     }
   }
-  __syncthreads();   // sexp
-  if (!ph) return;
   PROM_CLK(tk1);
   // ---- 4. window (q_s = sigma_s / c_s, Q = sum_s max(q_s, 0)); without orbital Doppler shift k_order
   //         has already picked it per tile
@@ -1839,7 +1932,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
     h = 0;
     t = (cF & 1) ? G : cA;
     if ((cF & 2) && !bad) {
-      const int vt = env_floor((float)kTailEps / qh * (1.0f - 0x1p-20f));
+      const int vt = env_floor((float)tail_eps<NS>() / qh * (1.0f - 0x1p-20f));
       const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
       const int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
       t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : et[vt - kEnvVmin]);
@@ -1849,7 +1942,26 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
   h = __builtin_amdgcn_readfirstlane(h < t ? h : t);
   t = __builtin_amdgcn_readfirstlane(t);
   PROM_CLK(tk2);
-  // ---- 5. integrate
+  // ---- 5. integrate.  Every wavefront issues its first chunk of records [h, h + 64) and the tail moments
+  //         at t together (one round trip), then stores the exp table to LDS; the workgroup barrier is
+  //         unconditional.
+  const double* rb = ((cF & 1) ? mrecs : recs) + (int64_t)o * n_pr * ST;
+  const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;   // t <= G <= n_pr: the row exists
+  double mm[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) mm[k] = mp[k];
+  const double* src = rb + (int64_t)h * ST;
+  const int32_t nel = (cF & 4) ? 0 : (t - h) * ST;
+  double nx[ST];
+#pragma unroll
+  for (int c = 0; c < ST; ++c) {
+    const int32_t e = 64 * c + lane;
+    nx[c] = e < nel ? src[e] : 0.0;
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
+  __syncthreads();   // sexp
+  if (!ph) return;
   double acc[kLPT];
 #pragma unroll
   for (int j = 0; j < kLPT; ++j) acc[j] = 0.0;
@@ -1872,26 +1984,16 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
 #pragma unroll
     for (int j = 0; j < kLPT; ++j) acc[j] = (acc[j] + tf * fs) / fs;
   } else {
-    const double* rb = ((cF & 1) ? mrecs : recs) + (int64_t)o * n_pr * ST;
     const bool tail = (cF & 2) && t < G;
-    const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
     // records staged through this wavefront's LDS slice in chunks of 64: one coalesced vector load per
     // chunk (the next chunk's load is in flight while this one is integrated), broadcast LDS reads
     if (h < t) {
-      double sy[kLPT][NS];   // -sigma 256/ln2: y = -tau 256/ln2 = sum_s N_s sy_s
+      double sy[kLPT][NS];   // -sigma 1024/ln2: y = -tau 1024/ln2 = sum_s N_s sy_s
 #pragma unroll
       for (int j = 0; j < kLPT; ++j)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) sy[j][s] = sg[j][s] * kM256Ln2;
+        for (int s = 0; s < NS; ++s) sy[j][s] = sg[j][s] * kM1024Ln2;
       double* sr = srec[wid];
-      const double* src = rb + (int64_t)h * ST;
-      const int32_t nel = (t - h) * ST;
-      double nx[ST];
-#pragma unroll
-      for (int c = 0; c < ST; ++c) {
-        const int32_t e = 64 * c + lane;
-        nx[c] = e < nel ? src[e] : 0.0;
-      }
       for (int32_t c0 = 0; c0 < t - h; c0 += 64) {
         const int32_t nr = (t - h - c0) < 64 ? (t - h - c0) : 64;
         double* buf = sr + ((c0 >> 6) & 1) * 64 * ST;
@@ -1917,7 +2019,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
             double y = Nr[0] * sy[j][0];
 #pragma unroll
             for (int s = 1; s < NS; ++s) y = __builtin_fma(Nr[s], sy[j][s], y);
-            acc[j] = acc_exp256(acc[j], F, y, sexp);
+            acc[j] = acc_exp1024(acc[j], F, y, sexp);
           }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1926,16 +2028,10 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
     if (tail) {
 #pragma unroll
       for (int j = 0; j < kLPT; ++j) {
-        double pw[NS][4];
+        double qv[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          const double v = sg[j][s] * tabv.t[s].nscale;
-          pw[s][0] = 1.0; pw[s][1] = v; pw[s][2] = v * v; pw[s][3] = pw[s][2] * v;
-        }
-        double tl = 0.0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) tl = __builtin_fma(mp[k], mono_eval<NS>(M, k, pw), tl);
-        acc[j] += tl;
+        for (int s = 0; s < NS; ++s) qv[s] = sg[j][s] * tabv.t[s].nscale;
+        acc[j] += tail_eval<NS>(mm, qv);
       }
     }
 #pragma unroll
@@ -1962,6 +2058,356 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
     PROM_ACC(wv + 5, t - h);
     PROM_ACC(wv + 6, tk3 - tk0);
     PROM_ACC(wv + 7, 1);
+    // wave timeline: wall-clock start/end (100 MHz) and HW_ID | XCC_ID << 32
+    const int64_t wl = 700000 + 4 * (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kTP + wid);
+    if (lane == 0 && wl + 3 < (1 << 20)) {
+      g_trace[wl] = wt0;
+      g_trace[wl + 1] = wall_clock64();
+      g_trace[wl + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)) |
+                        ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32);
+      g_trace[wl + 3] = (unsigned long long)(t - h) * kLPT;
+    }
+  }
+#endif
+}
+
+// ---- planned tau integration (no orbital Doppler shift) ------------------------------------------------
+// k_tau_w gives every (128-wavelength tile, phase) one wavefront: a run is ~1.6 rounds of resident
+// wavefronts and its end is set by the few windows at line cores (up to ~70 records, 30x the median)
+// that start in the second round.  k_tau_p instead:
+//   - static wavefronts, one per (tile, group of 4 phases): every phase whose window holds at most
+//     kHeavy records (nearly all) is integrated there; the records of the group's phases travel as one
+//     packed load;
+//   - heavy wavefronts, first in the grid: the (tile, phase) units with longer windows, which k_order
+//     lists per phase (hlist / hcnt), each split into two items of 64 wavelengths (one per lane).
+// Each (phase, wavelength) is integrated with k_tau_w's operations in k_tau_w's order, whichever
+// wavefront takes it, so R does not depend on the split.
+
+// The integration of one phase at LPL wavelengths per lane: records [h, t) staged through this
+// wavefront's LDS slice `sr` in chunks of 64 (the first chunk `nx` already loaded), the tail polynomial
+// from the moments mm, the transparent sum tf -- k_tau_w's operations in k_tau_w's order.
+template <int NS, int LPL>
+__device__ __forceinline__ void tau_phase(const double (&sg)[LPL][NS], const SigTabs4& tabv, const double* __restrict__ src,
+                                          int32_t n, double (&nx)[1 + NS], bool tail, const double (&mm)[Monos<NS>::K], double tf,
+                                          int lane, double* __restrict__ sr, const double* __restrict__ sexp,
+                                          double (&acc)[LPL]) {
+  constexpr Monos<NS> M{};
+  constexpr int K = Monos<NS>::K;
+  constexpr int ST = 1 + NS;
+#pragma unroll
+  for (int j = 0; j < LPL; ++j) acc[j] = 0.0;
+  if (n > 0) {
+    double sy[LPL][NS];
+#pragma unroll
+    for (int j = 0; j < LPL; ++j)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sy[j][s] = sg[j][s] * kM1024Ln2;
+    const int32_t nel = n * ST;
+    for (int32_t c0 = 0; c0 < n; c0 += 64) {
+      const int32_t nr = (n - c0) < 64 ? (n - c0) : 64;
+      double* buf = sr + ((c0 >> 6) & 1) * 64 * ST;
+#pragma unroll
+      for (int c = 0; c < ST; ++c) buf[64 * c + lane] = nx[c];
+      if (c0 + 64 < n) {
+#pragma unroll
+        for (int c = 0; c < ST; ++c) {
+          const int32_t e = (c0 + 64) * ST + 64 * c + lane;
+          nx[c] = e < nel ? src[e] : 0.0;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int32_t r = 0; r < nr; ++r) {
+        const double F = buf[r * ST];
+        double Nr[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) Nr[s] = buf[r * ST + 1 + s];
+#pragma unroll
+        for (int j = 0; j < LPL; ++j) {
+          double y = Nr[0] * sy[j][0];
+#pragma unroll
+          for (int s = 1; s < NS; ++s) y = __builtin_fma(Nr[s], sy[j][s], y);
+          acc[j] = acc_exp1024(acc[j], F, y, sexp);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (tail) {
+#pragma unroll
+    for (int j = 0; j < LPL; ++j) {
+      double qv[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) qv[s] = sg[j][s] * tabv.t[s].nscale;
+      acc[j] += tail_eval<NS>(mm, qv);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < LPL; ++j) acc[j] += tf;
+}
+
+template <int LPL>
+__device__ __forceinline__ void tau_count(unsigned long long* __restrict__ evals, int gw, int lane, int32_t n,
+                                          const bool (&live)[LPL]) {
+  if (!evals) return;
+  int nl = 0;
+#pragma unroll
+  for (int j = 0; j < LPL; ++j) nl += __popcll(__ballot(live[j]));
+  if (lane == 0) atomicAdd(&evals[gw & 63], (unsigned long long)n * (unsigned long long)nl);
+}
+
+
+// A heavy item: phase o, 64 wavelengths of a tile (half hf), one per lane, window [h, t) of any length.
+template <int NS>
+__device__ __forceinline__ void tau_heavy(int32_t tile, int32_t hf, int32_t o, int32_t h, int32_t t, int32_t fl,
+                                          const SigTabs4& tabv, const double* __restrict__ sig,
+                                          const double* __restrict__ recs, const double* __restrict__ mrecs,
+                                          const double* __restrict__ tfrac, int32_t n_pr, int64_t n_wav,
+                                          const double* __restrict__ wmom, unsigned long long* __restrict__ evals,
+                                          int lane, int gw, double* __restrict__ sr,
+                                          const double* __restrict__ sexp, double* __restrict__ R) {
+  constexpr int K = Monos<NS>::K;
+  constexpr int ST = 1 + NS;
+  const int64_t w = (int64_t)tile * kTW + 64 * hf + lane;
+  bool live[1] = {w < n_wav};
+  double sg[1][NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sg[0][s] = sig[(int64_t)s * n_wav + (live[0] ? w : n_wav - 1)];
+  const double* src = ((fl & 1) ? mrecs : recs) + ((int64_t)o * n_pr + h) * ST;
+  const int32_t nel = (t - h) * ST;
+  double nx[ST];
+#pragma unroll
+  for (int c = 0; c < ST; ++c) {
+    const int32_t e = 64 * c + lane;
+    nx[c] = e < nel ? src[e] : 0.0;
+  }
+  const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;   // t <= G <= n_pr: the row exists
+  double mm[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) mm[k] = mp[k];
+  const double tf = tfrac[o];
+  double acc[1];
+  tau_phase<NS, 1>(sg, tabv, src, t - h, nx, (fl & 2) != 0, mm, tf, lane, sr, sexp, acc);
+  tau_count<1>(evals, gw, lane, t - h, live);
+  if (live[0]) R[(int64_t)o * n_wav + w] = acc[0];
+}
+
+// Grid: n_heavy heavy wavefronts (blockIdx first), then one static wavefront per (tile, group of 4
+// phases).  Static wavefront: round trip 1 = its phases' windows and flags, sigma at its 128
+// wavelengths (2 per lane), the exp table; round trip 2 = the packed records of its light phases and
+// their tail moments.  Heavy wavefront: the per-phase counts, then its unit, then records and sigma.
+template <int NS>
+__global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs4 tabv, const double* __restrict__ sig,
+                                                                   const double* __restrict__ recs,
+                                                                   const double* __restrict__ mrecs,
+                                                                   const int32_t* __restrict__ act_ip,
+                                                                   const double* __restrict__ fout,
+                                                                   const int32_t* __restrict__ counts,
+                                                                   const double* __restrict__ tfrac,
+                                                                   const double* __restrict__ fsum, int32_t n_pr,
+                                                                   int32_t n_orb, int64_t n_wav,
+                                                                   const double* __restrict__ wmom,
+                                                                   const int2* __restrict__ win, int32_t n_tiles,
+                                                                   const int4* __restrict__ hlist,
+                                                                   const int32_t* __restrict__ hcnt,
+                                                                   int32_t n_heavy,
+                                                                   unsigned long long* __restrict__ evals,
+                                                                   double* __restrict__ R) {
+  constexpr Monos<NS> M{};
+  constexpr int K = Monos<NS>::K;
+  constexpr int ST = 1 + NS;
+  constexpr int PQ = (4 * kHeavy * ST + 63) / 64;   // packed record loads per lane
+  constexpr int MV = (4 * K + 63) / 64;             // packed moment loads per lane
+  static_assert(4 * kHeavy * ST <= 2 * 64 * ST, "a group's packed records fit the wavefront's LDS slice");
+  __shared__ double srec[kTP][2 * 64 * ST];   // per wavefront: two chunks of 64 records
+  __shared__ double sexp[1024];                // 2^(i/1024)
+#ifdef PROM_TRACE
+  const unsigned long long wt0 = wall_clock64();
+  long long wrk = 0;
+#endif
+  double etv[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) etv[m] = kExp2TableDev[2 * (threadIdx.x + kBlock * m)];   // kBlock == 256
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int32_t gw = blockIdx.x * kTP + wid;
+  double* sr = srec[wid];
+  if (gw < n_heavy) {
+    // ---- heavy wavefronts: items e = gw, gw + n_heavy, ... over 2 x (sum of hcnt) halves
+    int32_t U = 0;
+    for (int32_t o = 0; o < n_orb; ++o) U += hcnt[o];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
+    __syncthreads();
+    for (int32_t e = gw; e < 2 * U; e += n_heavy) {
+      int32_t u = e >> 1, o = 0;
+      for (; o < n_orb - 1; ++o) {
+        const int32_t c = hcnt[o];
+        if (u < c) break;
+        u -= c;
+      }
+      const int4 en = hlist[(int64_t)o * n_tiles + u];
+      const int32_t tile = __builtin_amdgcn_readfirstlane(en.x), h = __builtin_amdgcn_readfirstlane(en.y);
+      const int32_t t = __builtin_amdgcn_readfirstlane(en.z), fl = __builtin_amdgcn_readfirstlane(en.w);
+#ifdef PROM_TRACE
+      wrk += t - h;
+#endif
+      tau_heavy<NS>(tile, e & 1, o, h, t, fl, tabv, sig, recs, mrecs, tfrac, n_pr, n_wav, wmom, evals, lane, e, sr,
+                    sexp, R);
+    }
+  } else {
+    // ---- static wavefront: tile, phases o0 .. o0 + np - 1
+    const int32_t sw = gw - n_heavy;
+    const int32_t tile = sw % n_tiles, o0 = (sw / n_tiles) * 4;
+    const bool has = o0 < n_orb;
+    const int32_t np = has ? min(4, n_orb - o0) : 0;
+    int32_t h[4], t[4], fl[4], n[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      h[p] = 0; t[p] = 0; fl[p] = 0;
+      if (p < np) {
+        const int32_t o = o0 + p;
+        const int2 wv = win[(int64_t)o * n_tiles + tile];
+        const int32_t* cp = counts + o * kCnt;
+        h[p] = wv.x; t[p] = wv.y;
+        fl[p] = (cp[5] ? 1 : 0) | ((cp[6] && wv.y < cp[4]) ? 2 : 0) | (cp[3] ? 4 : 0);
+      }
+    }
+    bool live[2];
+    double sg[2][NS];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
+      live[j] = w < n_wav;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sg[j][s] = sig[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)];
+    }
+    double tfv[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) tfv[p] = p < np ? tfrac[o0 + p] : 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
+    __syncthreads();
+    // light phases (window <= kHeavy records, not exact): packed; heavy ones are another wavefront's
+    int32_t off[5];
+    off[0] = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int32_t c = t[p] - h[p];
+      const bool light = p < np && !(fl[p] & 4) && c <= kHeavy;
+      n[p] = light ? c : -1;
+      off[p + 1] = off[p] + (light ? c * ST : 0);
+    }
+    double pre[PQ];
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      const int32_t e = 64 * q + lane;
+      pre[q] = 0.0;
+      if (e < off[4]) {
+        const int p = e < off[1] ? 0 : (e < off[2] ? 1 : (e < off[3] ? 2 : 3));
+        const int32_t hp = p == 0 ? h[0] : (p == 1 ? h[1] : (p == 2 ? h[2] : h[3]));
+        const int32_t fp = p == 0 ? fl[0] : (p == 1 ? fl[1] : (p == 2 ? fl[2] : fl[3]));
+        const int32_t op = p == 0 ? off[0] : (p == 1 ? off[1] : (p == 2 ? off[2] : off[3]));
+        pre[q] = ((fp & 1) ? mrecs : recs)[((int64_t)(o0 + p) * n_pr + hp) * ST + (e - op)];
+      }
+    }
+    double mv[MV];
+#pragma unroll
+    for (int q = 0; q < MV; ++q) {
+      const int32_t e = 64 * q + lane;
+      const int p = e / K, k = e - p * K;
+      mv[q] = 0.0;
+      if (p < np) {
+        const int32_t tp = p == 0 ? t[0] : (p == 1 ? t[1] : (p == 2 ? t[2] : t[3]));
+        const int32_t np_ = p == 0 ? n[0] : (p == 1 ? n[1] : (p == 2 ? n[2] : n[3]));
+        if (np_ >= 0) mv[q] = wmom[((int64_t)(o0 + p) * (n_pr + 1) + tp) * K + k];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) sr[64 * q + lane] = pre[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double sy[2][NS];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sy[j][s] = sg[j][s] * kM1024Ln2;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p >= np) continue;
+      const int32_t o = o0 + p;
+      if (n[p] >= 0) {
+        const double* buf = sr + off[p];
+        double acc[2] = {0.0, 0.0};
+        for (int32_t r = 0; r < n[p]; ++r) {
+          const double F = buf[r * ST];
+          double Nr[NS];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) Nr[s] = buf[r * ST + 1 + s];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            double y = Nr[0] * sy[j][0];
+#pragma unroll
+            for (int s = 1; s < NS; ++s) y = __builtin_fma(Nr[s], sy[j][s], y);
+            acc[j] = acc_exp1024(acc[j], F, y, sexp);
+          }
+        }
+        if (fl[p] & 2) {
+          double mm[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) mm[k] = lane_read(mv[(p * K + k) >> 6], (p * K + k) & 63);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            double qv[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) qv[s] = sg[j][s] * tabv.t[s].nscale;
+            acc[j] += tail_eval<NS>(mm, qv);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[j] += tfv[p];
+          if (live[j]) R[(int64_t)o * n_wav + (int64_t)tile * kTW + 64 * j + lane] = acc[j];
+        }
+        tau_count<2>(evals, gw, lane, n[p], live);
+#ifdef PROM_TRACE
+        wrk += 2 * n[p];
+#endif
+      } else if (fl[p] & 4) {
+        // non-finite column densities: exact reference order over the chord-order records
+        const double* rb = recs + (int64_t)o * n_pr * ST;
+        const int32_t* ipl = act_ip + (int64_t)o * n_pr;
+        double acc[2] = {0.0, 0.0};
+        for (int32_t i = 0; i < t[p]; ++i) {
+          const double* r = rb + (int64_t)i * ST;
+          const double F = fout[ipl[i]];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            double tau = r[1] * sg[j][0];
+#pragma unroll
+            for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[j][s];
+            acc[j] = acc[j] + F * exp(-tau);
+          }
+        }
+        const double fs = fsum[o];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (live[j]) R[(int64_t)o * n_wav + (int64_t)tile * kTW + 64 * j + lane] = (acc[j] + tfv[p] * fs) / fs;
+      }
+    }
+  }
+#ifdef PROM_TRACE
+  {
+    const int64_t wl = 700000 + 4 * (int64_t)gw;
+    if (lane == 0 && wl + 3 < (1 << 20)) {
+      g_trace[wl] = wt0;
+      g_trace[wl + 1] = wall_clock64();
+      g_trace[wl + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)) |
+                        ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32);
+      g_trace[wl + 3] = (unsigned long long)wrk | (gw < n_heavy ? (1ull << 62) : 0ull);
+    }
   }
 #endif
 }
@@ -2366,7 +2812,15 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // of the column kernel (they run beside the chord work) instead of once per phase group
   const bool cols8 = tr.n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4;
   const bool pre_sigma = cols8 && wpath && tr.window && tr.uniform_shift && !tr.star;
-  const int32_t na = tr.n_atoms;
+  // species merging (TransitDev::species_merge_ok) on the no-Doppler fast path: downstream of the
+  // column kernel there is one effective absorber
+  const bool msp = pre_sigma && tr.species_merge_ok;
+  const int32_t nsig = tr.n_atoms;                 // species the column kernel resamples
+  const int32_t na = msp ? 1 : tr.n_atoms;         // species the ordering and tau kernels see
+  const ColArgs& cargs = msp ? tr.colargs_m : tr.colargs;
+  const int32_t n_terms = msp ? 1 : tr.n_terms;
+  const double* smax = msp ? tr.sigma_max_m.as<double>() : tr.sigma_max_dev.as<double>();
+  const SigTabs4& tabs4 = msp ? tr.sigtab_m : tr.sigtab_v;
   *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? (wpath && tr.window ? 20 : 10) : 0);
   // stage events ride on the fast path's dispatch packets (hipExtLaunchKernelGGL start/stop events):
   // no separate event packets between the kernels
@@ -2379,22 +2833,22 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #define PROM_COLS(SV, NSV)                                                                               \
   hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
                      dim3((unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8)) + sig_blocks),                \
-                     dim3(kBlock), 0, s, ev0, nullptr, 0, tr.colargs, tr.n_terms,                         \
+                     dim3(kBlock), 0, s, ev0, nullptr, 0, cargs, n_terms,                                 \
                      tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
                      tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
                      tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
-                     tr.moon_R.as<double>(), tr.sigma_max_dev.as<double>(), tr.cull_tau, rs.ncol.as<double>(), \
+                     tr.moon_R.as<double>(), smax, tr.cull_tau, rs.ncol.as<double>(),                       \
                      rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>(), \
-                     pre_sigma ? rs.tq.as<float2>() : nullptr)
+                     pre_sigma ? rs.tq.as<float2>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale)
 #define PROM_COLS_L(NSV)                       \
   if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
   else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
   else if (tr.n_x <= 32) PROM_COLS(4, NSV);    \
   else PROM_COLS(8, NSV);
     if (!pre_sigma) { PROM_COLS_L(0) }
-    else if (na == 1) { PROM_COLS_L(1) }
-    else if (na == 2) { PROM_COLS_L(2) }
-    else if (na == 3) { PROM_COLS_L(3) }
+    else if (nsig == 1) { PROM_COLS_L(1) }
+    else if (nsig == 2) { PROM_COLS_L(2) }
+    else if (nsig == 3) { PROM_COLS_L(3) }
     else { PROM_COLS_L(4) }
 #undef PROM_COLS_L
 #undef PROM_COLS
@@ -2465,11 +2919,13 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev1, 0,                \
                      rs.flags.as<int32_t>(),                                                              \
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
-                     tr.window ? 1 : 0, tr.sigtab_v, rs.recs.as<double>(),                               \
+                     tr.window ? 1 : 0, tabs4, rs.recs.as<double>(),                                     \
                      rs.act_ip.as<int32_t>(), rs.mrecs.as<double>(), rs.counts.as<int32_t>(),            \
                      rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>(), \
-                     pre_sigma ? rs.tq.as<float2>() : nullptr, n_wtiles, rs.win.as<int2>())
-    switch (tr.n_atoms) {
+                     pre_sigma ? rs.tq.as<float2>() : nullptr, n_wtiles, rs.win.as<int2>(),             \
+                     (pre_sigma && tr.plan) ? rs.hlist.as<int4>() : nullptr,                           \
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr)
+    switch (na) {
       case 1: PROM_CHW(1); break;
       case 2: PROM_CHW(2); break;
       case 3: PROM_CHW(3); break;
@@ -2545,7 +3001,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #define PROM_TAUW(NSV, PMV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_tau_w<NSV, UV>), dim3((unsigned)((tr.n_wav + kTW - 1) / kTW), (unsigned)((tr.n_orb + kTP - 1) / kTP)), \
                      dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0,                  \
-                     tr.sigtab_v, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                     \
+                     tabs4, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                           \
                      tr.n_orb, tr.n_wav, rs.wenv.as<int32_t>(), rs.wmom.as<double>(), rs.sig.as<double>(),  \
                      rs.win.as<int2>(), n_wtiles, tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
 #define PROM_TAUW_NS(PMV, UV)            \
@@ -2555,7 +3011,42 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     case 3: PROM_TAUW(3, PMV, UV); break; \
     default: PROM_TAUW(4, PMV, UV); break; \
   }
-    if (pre_sigma) { PROM_TAUW_NS(8, true) } else { PROM_TAUW_NS(2, false) }
+    if (pre_sigma && tr.plan) {
+      // planned: heavy wavefronts over k_order's lists of long windows, static ones over (tile, 4 phases)
+      if (tr.taup_resident == 0) {
+        int cus = 0, nb = 0;
+        int dev = 0;
+        PROM_HIP(hipGetDevice(&dev));
+        PROM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        switch (na) {
+          case 1: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<1>, kBlock, 0)); break;
+          case 2: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<2>, kBlock, 0)); break;
+          case 3: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<3>, kBlock, 0)); break;
+          default: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<4>, kBlock, 0)); break;
+        }
+        tr.taup_resident = std::max(1, cus) * std::max(1, nb) * kTP;
+      }
+      const int64_t n_static = (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
+      // heavy wavefronts: what the static ones leave of one resident round, at least a quarter of it
+      int64_t n_heavy = std::max<int64_t>(tr.taup_resident / 4, tr.taup_resident - n_static);
+      n_heavy = (n_heavy + kTP - 1) / kTP * kTP;
+      const unsigned blocks = (unsigned)((n_heavy + n_static + kTP - 1) / kTP);
+      *variant = 30 + (na <= 4 ? na : 0);
+#define PROM_TAUP(NSV)                                                                                  \
+  hipExtLaunchKernelGGL((k_tau_p<NSV>), dim3(blocks), dim3(kBlock), 0, s,                                 \
+                        ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, tabs4, rs.sig.as<double>(),        \
+                        recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
+                        rs.wmom.as<double>(), rs.win.as<int2>(), n_wtiles, rs.hlist.as<int4>(),          \
+                        rs.hcnt.as<int32_t>(), (int32_t)n_heavy,                                         \
+                        tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
+      switch (na) {
+        case 1: PROM_TAUP(1); break;
+        case 2: PROM_TAUP(2); break;
+        case 3: PROM_TAUP(3); break;
+        default: PROM_TAUP(4); break;
+      }
+#undef PROM_TAUP
+    } else if (pre_sigma) { PROM_TAUW_NS(8, true) } else { PROM_TAUW_NS(2, false) }
 #undef PROM_TAUW_NS
 #undef PROM_TAUW
     PROM_HIP(hipGetLastError());

@@ -310,3 +310,49 @@ def test_many_los_samples_generic_columns(dev):
     scen, dop, grids = O.from_setup(cfg)
     Ro = O.transit_depth(scen, dop, grids, tr.wavelength, O.build_tables(scen, grids))
     assert rel(R, Ro) < R_TOL
+
+
+@pytest.mark.parametrize("name", ["C1", "C2r", "exomoon", "C2"])
+def test_planned_tau_bitwise(dev, name, monkeypatch):
+    """The planned tau kernel (k_tau_p: static (tile, 4-phase) wavefronts + heavy-window wavefronts from
+    k_order's lists) computes every (phase, wavelength) with k_tau_w's operations in k_tau_w's order:
+    R is bitwise identical with the planned path off (PROM_TAU_PLAN=0), and the exp count is equal."""
+    from prometheus_amd import configs
+    if name == "C2":
+        cfg = configs.get("C2")
+    else:
+        cfg = json.loads(str(load("transit_" + name)["config"]))
+    tr = _product_transit(cfg)
+    monkeypatch.setenv("PROM_TAU_PLAN", "1")
+    R_p = tr.sumOverChords(devices=[0])
+    st_p = tr.last_stats[-1]
+    monkeypatch.setenv("PROM_TAU_PLAN", "0")
+    R_w = tr.sumOverChords(devices=[0])
+    st_w = tr.last_stats[-1]
+    print(name, "variants", st_p["tau_kernel_variant"], st_w["tau_kernel_variant"], "exp evals", st_p["exp_evals"])
+    if not cfg["Fundamentals"]["DopplerOrbitalMotion"]:
+        assert st_p["tau_kernel_variant"] // 10 == 3 and st_w["tau_kernel_variant"] // 10 == 2
+    assert np.array_equal(R_p, R_w)
+    assert st_p["exp_evals"] == st_w["exp_evals"]
+
+
+@pytest.mark.parametrize("name", ["C2r", "C2"])
+def test_species_merge(dev, name, monkeypatch):
+    """Constituents of one density scenario collapse into one effective absorber (tau = N Y with
+    Y = sum_s chi_s sigma_s): R agrees with the per-species integration to rounding (1e-13 relative)
+    and with the reference to R_TOL; the merged run has one effective species (variant 31)."""
+    from prometheus_amd import configs
+    cfg = configs.get("C2") if name == "C2" else json.loads(str(load("transit_" + name)["config"]))
+    tr = _product_transit(cfg)
+    monkeypatch.setenv("PROM_SPECIES_MERGE", "1")
+    R_m = tr.sumOverChords(devices=[0])
+    st_m = tr.last_stats[-1]
+    monkeypatch.setenv("PROM_SPECIES_MERGE", "0")
+    R_s = tr.sumOverChords(devices=[0])
+    st_s = tr.last_stats[-1]
+    print(name, "variants", st_m["tau_kernel_variant"], st_s["tau_kernel_variant"],
+          "exp evals %d -> %d" % (st_s["exp_evals"], st_m["exp_evals"]), "max rel diff %.3e" % rel(R_m, R_s))
+    assert st_m["tau_kernel_variant"] == 31 and st_s["tau_kernel_variant"] == 32
+    assert rel(R_m, R_s) < 1e-13
+    if name != "C2":
+        assert rel(R_m, load("transit_" + name)["R"]) < R_TOL

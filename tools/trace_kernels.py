@@ -18,7 +18,9 @@ from prometheus_amd import build  # noqa: E402
 
 out = os.path.join(REPO, "prometheus_amd", "libprom_hip_trace.so")
 cmd = [build.hipcc()] + build.FLAGS + ["-DPROM_TRACE", "-o", out] + [os.path.join(build.HERE, s) for s in build.SOURCES]
-subprocess.run(cmd, check=True, cwd=build.HERE)
+srcs = [os.path.join(build.HERE, s) for s in build.SOURCES]
+if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(f) for f in srcs):
+    subprocess.run(cmd, check=True, cwd=build.HERE)
 os.environ["PROMETHEUS_AMD_LIB"] = out
 
 from prometheus_amd import _native, configs, gasProperties, setupfile  # noqa: E402
@@ -52,22 +54,48 @@ for o in range(n_orb):
     print("  phase %2d: total %6.2f  steps %s" % (o, (t[8] - t[0]) * 0.01, " ".join("%5.2f" % v for v in d)))
 kt = a[65536:600000 - (600000 - 65536) % 8].reshape(-1, 8)
 kt = kt[kt[:, 7] > 0]
-wall = (a[4000] - a[4002]) * 10.0  # ns, block 0 wave 0 lifetime
-clk = a[4001] - a[4003]
-print("clock64 ticks per ns (block 0 wave 0): %.3f" % (clk / max(wall, 1)))
-pairs = kt[:, 4].sum()
-print("k_tau_w per (wave, phase) mean ticks: sigma+windows %.0f, -, phases %.0f, -; records/phase %.1f; pairs %d"
-      % tuple([kt[:, i].sum() / pairs for i in range(4) if i in (0, 2)] + [kt[:, 5].sum() / pairs, pairs]))
-tot = kt[:, 6]
-win = kt[:, 5]
-print("window records per wave: p50 %.0f p90 %.0f p99 %.0f max %.0f" % tuple(np.percentile(win, [50, 90, 99, 100])))
-for lo, hi in [(0, 4), (4, 16), (16, 64), (64, 256), (256, 10**9)]:
-    m = (win >= lo) & (win < hi)
-    if m.any():
-        print("  window [%d,%d): %5d waves, lifetime mean %.0f max %.0f ticks" % (lo, hi, m.sum(), tot[m].mean(), tot[m].max()))
-print("k_tau per wave lifetime ticks: mean %.0f  p10 %.0f  p50 %.0f  p90 %.0f  max %.0f  (%d waves)"
-      % (tot.mean(), *np.percentile(tot, [10, 50, 90, 100]), len(tot)))
+if len(kt):
+    tot = kt[:, 6]
+    win = kt[:, 5]
+    print("k_tau_w per wave: records p50 %.0f p90 %.0f p99 %.0f max %.0f; lifetime ticks mean %.0f p50 %.0f p90 %.0f max %.0f"
+          % (*np.percentile(win, [50, 90, 99, 100]), tot.mean(), *np.percentile(tot, [50, 90, 100])))
 kc = a[600000:600000 + 2 * 100000].reshape(-1, 2)
 kc = kc[kc[:, 1] > 0]
 print("k_columns8 per wave lifetime ticks: mean %.0f p50 %.0f p90 %.0f (%d waves)"
       % (kc[:, 0].mean(), np.percentile(kc[:, 0], 50), np.percentile(kc[:, 0], 90), len(kc)))
+
+# tau kernel wave timeline (wall clock, 10 ns ticks): start, end, HW_ID | XCC_ID << 32, record-lambda work
+tl = a[700000:700000 + 4 * 80000].reshape(-1, 4)
+tl = tl[tl[:, 1] > 0]
+if len(tl):
+    t0 = tl[:, 0].min()
+    st = (tl[:, 0] - t0) * 0.01
+    en = (tl[:, 1] - t0) * 0.01
+    hw = tl[:, 2]
+    heavy = (tl[:, 3] >> 62) & 1
+    wk = tl[:, 3] & ((1 << 62) - 1)
+    xcc = (hw >> 32) & 0xF
+    print("tau kernel timeline (us): %d waves, span %.2f; starts p50 %.2f p90 %.2f max %.2f; ends p50 %.2f p90 %.2f p99 %.2f max %.2f"
+          % (len(tl), en.max(), np.percentile(st, 50), np.percentile(st, 90), st.max(), *np.percentile(en, [50, 90, 99, 100])))
+    dur = en - st
+    print("  wave duration us: p10 %.2f p50 %.2f p90 %.2f max %.2f" % tuple(np.percentile(dur, [10, 50, 90, 100])))
+    print("  record-lambda work per wave: p50 %.0f p90 %.0f p99 %.0f max %.0f, total %d" % (*np.percentile(wk, [50, 90, 99, 100]), wk.sum()))
+    for t in np.arange(0, en.max() + 1, 1.0):
+        print("  t=%5.1f us: %5d waves live, %5d started, %5d done" % (t, ((st <= t) & (en > t)).sum(), (st <= t).sum(), (en <= t).sum()))
+    for x in range(8):
+        m = xcc == x
+        if m.any():
+            print("  xcc %d: %5d waves, last end %.2f us, mean dur %.2f" % (x, m.sum(), en[m].max(), dur[m].mean()))
+    for cls, m in (("heavy", heavy == 1), ("static", heavy == 0)):
+        if m.any():
+            busy = m & (wk > 0)
+            print("  %s waves: %d (%d with work); duration p10 %.2f p50 %.2f p90 %.2f max %.2f; end p50 %.2f max %.2f; work p50 %.0f max %.0f"
+                  % (cls, m.sum(), busy.sum(), *np.percentile(dur[m], [10, 50, 90, 100]), np.percentile(en[m], 50), en[m].max(),
+                     np.percentile(wk[m], 50), wk[m].max()))
+            if busy.any():
+                for lo, hi in ((0, 8), (8, 16), (16, 32), (32, 64), (64, 1 << 30)):
+                    mm = busy & (wk >= lo) & (wk < hi)
+                    if mm.any():
+                        print("    work [%d,%d): %5d waves, duration mean %.2f max %.2f" % (lo, hi, mm.sum(), dur[mm].mean(), dur[mm].max()))
+    late = np.argsort(en)[-10:]
+    print("  last-finishing waves (start, end, work):", [(round(float(st[i]), 2), round(float(en[i]), 2), int(wk[i])) for i in late])
