@@ -92,10 +92,21 @@ int32_t prom_create(int32_t device, prom_ctx** out) {
   return PROM_OK;
 }
 
+static void drop_graphs(prom::TransitDev& tr) {
+  for (auto& g : tr.gexec)
+    if (g) {
+      (void)hipGraphExecDestroy(g);
+      g = nullptr;
+    }
+}
+
 void prom_destroy(prom_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  for (auto st : ctx->streams)
+    if (st) (void)hipStreamSynchronize(st);
+  drop_graphs(ctx->tr);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->tev) (void)hipEventDestroy(e);
@@ -313,6 +324,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.planet_R = pb->planet_R;
     tr.cull_tau = pb->cull_tau > 0.0 ? pb->cull_tau : std::ldexp(1.0, -60);
     for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));   // pipelined runs may still read the old problem
+    drop_graphs(tr);   // captured against the old problem's buffers and arguments
+    {
+      // measured on MI355X (tools/host_overhead.py, C2): hipGraphLaunch costs the host ~16 us per run
+      // against ~8.5 us for the three direct launches, so graphs are opt-in (PROM_GRAPH=1)
+      const char* e = std::getenv("PROM_GRAPH");
+      tr.graphs = e && std::atoi(e) != 0;
+    }
     tr.exp_mode = (pb->options & PROM_OPT_OCML_EXP) ? 0 : 1;
     tr.merge = (pb->options & PROM_OPT_NO_MERGE) == 0;
     tr.window = (pb->options & PROM_OPT_NO_WINDOW) == 0;
@@ -615,8 +633,28 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     const hipStream_t st = ctx->streams[si];
     prom::RunSlot& rs = tr.slot[si];
     if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
-    prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, (stats || timed) ? ev : nullptr, &variant,
-                         stats != nullptr);
+    if (!stats && !timed && tr.graphs && tr.depth > 1) {
+      // untimed fast-path run: replay the slot's graph (captured here the first time)
+      if (!tr.gexec[si]) {
+        hipGraph_t g = nullptr;
+        PROM_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        try {
+          prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, nullptr, &variant, false);
+        } catch (...) {
+          (void)hipStreamEndCapture(st, &g);
+          if (g) (void)hipGraphDestroy(g);
+          throw;
+        }
+        PROM_HIP(hipStreamEndCapture(st, &g));
+        const hipError_t ie = hipGraphInstantiate(&tr.gexec[si], g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        PROM_HIP(ie);
+      }
+      PROM_HIP(hipGraphLaunch(tr.gexec[si], st));
+    } else {
+      prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, (stats || timed) ? ev : nullptr, &variant,
+                           stats != nullptr);
+    }
     tr.last = si;
     tr.count_evals = false;
 

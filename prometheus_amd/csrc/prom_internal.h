@@ -238,6 +238,10 @@ struct TransitDev {
   DevBuf crho, cclv, cshift;                // [n_pr]
   DevBuf rm_slices;                         // [n_wav tiles of kBlock][3] {lo, m, half}: LDS slice
   RunSlot slot[kMaxSlots];
+  // PROM_GRAPH=1: a fast-path run is one hipGraph per slot, captured at the slot's first untimed run
+  // and replayed (one host call instead of three launches; slower on ROCm 7.2, so off by default)
+  hipGraphExec_t gexec[kMaxSlots] = {};
+  bool graphs = false;
   int depth = 1;                            // slots in use: fast path = pipeline depth, else 1
   int last = 0;                             // slot of the most recent run
 };

@@ -23,10 +23,10 @@ for s in $STEPS; do
     newtests) step pytest_new 600 python -m pytest tests -q -m gpu -rA -k "${KSEL:-native_loaded}" -s ;;
     rmbench) step rm_bench 600 python tools/rm_bench.py C2 --runs 3 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
-    benchfast) step bench 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    bench) step bench 600 python bench.py ;;
+    benchfast) step bench 600 python bench.py --no-cpu-baseline ;;
     traffic) step traffic 700 bash tools/bench_traffic.sh ${TAG:-r01c} ;;
-    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
   esac
 done
 exit 0
