@@ -593,11 +593,15 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       }
       rs.evals.ensure(sizeof(unsigned long long) * 64);
       rs.sig.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * tr.n_wav);
+      rs.zfl.ensure((size_t)tr.n_wav);
       const int64_t n_wtiles = (tr.n_wav + 127) / 128;
       rs.tq.ensure(sizeof(float) * 2 * n_wtiles);
       rs.win.ensure(sizeof(int32_t) * 2 * n_orb * n_wtiles);
       rs.hlist.ensure(sizeof(int32_t) * 4 * n_orb * n_wtiles);
-      rs.hcnt.ensure(sizeof(int32_t) * n_orb);
+      rs.hcnt.ensure(sizeof(int32_t) * 4);
+      if (n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && n_mol == 0)
+        rs.trec.ensure(sizeof(double) * n_orb * n_wtiles *
+                       (2 + std::max(prom::n_tail_moments(n_atoms), prom::n_tail_moments(1))));
       tr.taup_resident = 0;
       rs.tsum.ensure(sizeof(double) * n_orb);
       rs.fsum.ensure(sizeof(double) * n_orb);

@@ -162,7 +162,7 @@ struct MolTable {
 // Work and output buffers of one run.  Fast-path problems rotate consecutive runs over `depth` slots
 // and as many streams (PROM_PIPELINE, default 4), so that a run's column / ordering kernels overlap
 // the previous runs' tau kernels; every run is complete and independent.
-constexpr int kMaxSlots = 4;
+constexpr int kMaxSlots = 8;
 struct RunSlot {
   DevBuf ncol;                              // [n_atoms][n_orb][n_pr]
   DevBuf flags;                             // [n_orb][n_pr] int32: 0 active, 1 transparent, 2 blocked
@@ -176,11 +176,14 @@ struct RunSlot {
   DevBuf wmom;                              // [n_orb][n_pr + 1][K] suffix tail moments
   DevBuf evals;                             // [64] uint64 exp-evaluation counters (stats runs)
   DevBuf sig;                               // no orbital Doppler shift: sigma_s(lambda_w) [n_atoms][n_wav]
+  DevBuf zfl;                               // merged species: some chi_s sigma_s(lambda_w) not > 0 [n_wav] uint8
   DevBuf tq;                                // no orbital Doppler shift: Q range per 128-lambda tile [n_tiles] float2
   DevBuf win;                               // ... and each tile's tau window {h, t} per phase [n_orb][n_tiles] int2
-  DevBuf hlist;                             // ... (tile, phase) units with long windows {tile, h, t, flags}
-                                            //     [n_orb][n_tiles] int4, listed per phase by k_order
-  DevBuf hcnt;                              // ... their count per phase [n_orb] int32
+  DevBuf trec;                              // ... tile records {h, t}, {flags, 0}, tail moments at t
+                                            //     [n_orb][n_tiles][2 + K] (k_order, for k_tau_p)
+  DevBuf hlist;                             // ... (tile, phase) units with long windows
+                                            //     {tile, h, t, flags | phase << 8} [n_orb * n_tiles] int4
+  DevBuf hcnt;                              // ... their count (int32; zeroed by k_columns8)
   DevBuf R;                                 // [n_orb][n_wav]
 };
 

@@ -557,7 +557,8 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
                                  double cull, double* __restrict__ ncol, int32_t* __restrict__ flags,
                                  const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
                                  double* __restrict__ sig, float2* __restrict__ tq, int32_t merge_sp,
-                                 double nscale_m) {
+                                 double nscale_m, int32_t* __restrict__ hcnt, uint8_t* __restrict__ zfl) {
+  if (hcnt && blockIdx.x == 0 && threadIdx.x == 0) hcnt[0] = 0;   // k_order's heavy-unit counter
   // Eight lanes per chord; lane j holds samples j, j + 8, ..., j + 8 (SPL - 1).  That is numpy's
   // pairwise_sum layout (loops_utils.h.src) for 8 <= n_x < 128: lane j accumulates r[j] = a[j] +
   // a[j+8] + ... sequentially, the eight partial sums combine as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
@@ -580,9 +581,17 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
       if (merge_sp) {
         // species merging: the effective absorber's cross-section Y = sum_s chi_s sigma_s
         double Y = 0.0;
+        bool z = false;   // some chi_s sigma_s not > 0: an infinite column gives NaN there (inf * 0)
 #pragma unroll
-        for (int s = 0; s < NSIG; ++s) Y += tabv.t[s].chi * sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
-        if (live) sig[w] = Y;
+        for (int s = 0; s < NSIG; ++s) {
+          const double v = tabv.t[s].chi * sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
+          z = z || !(v > 0.0);
+          Y += v;
+        }
+        if (live) {
+          sig[w] = Y;
+          zfl[w] = z ? 1 : 0;
+        }
         const double qs = Y * nscale_m;
         Q = qs > 0.0 ? qs : 0.0;
       } else {
@@ -1120,7 +1129,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
                                                    double* __restrict__ wmom,
                                                    const float2* __restrict__ tq, int32_t n_tiles,
                                                    int2* __restrict__ win, int4* __restrict__ hlist,
-                                                   int32_t* __restrict__ hcnt) {
+                                                   int32_t* __restrict__ hcnt, double* __restrict__ trec) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
@@ -1507,14 +1516,14 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   }
   if (tq) {
     // ---- 7. tau window [h, t) of every wavelength tile for this phase (no orbital Doppler shift:
-    //         Q per tile from k_columns8), exactly as k_tau_w would pick it from the tables; with
-    //         hlist, the tiles whose window holds more than kHeavy records are listed for k_tau_p's
-    //         heavy wavefronts (in any order: an LDS counter)
-    __shared__ int32_t shc;
-    if (tid == 0) shc = 0;
-    __syncthreads();
+    //         Q per tile from k_columns8), exactly as k_tau_w would pick it from the tables.  With
+    //         trec (the planned tau kernel): the tile record {h, t, flags, tail moments at t}, and the
+    //         tiles whose window holds more than kHeavy records go to the heavy-unit list (one global
+    //         counter, zeroed by k_columns8; any order)
+    __syncthreads();   // moments (step 6) visible to the whole workgroup
     const bool wtab = sorted && window;
-    const int32_t wfl = (sorted ? 1 : 0);
+    const int32_t pfl = (sorted ? 1 : 0) | (nnf ? 4 : 0);
+    constexpr int TRS = 2 + K;
     for (int32_t tl = tid; tl < n_tiles; tl += kWBlock) {
       const float2 q = tq[tl];
       int32_t h = 0, t = sorted ? G : nact;
@@ -1526,14 +1535,21 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       }
       h = h < t ? h : t;
       win[(int64_t)o * n_tiles + tl] = make_int2(h, t);
-      if (hlist && nnf == 0 && t - h > kHeavy) {
-        const int32_t k = atomicAdd(&shc, 1);
-        hlist[(int64_t)o * n_tiles + k] = make_int4(tl, h, t, wfl | ((wtab && t < G) ? 2 : 0));
+      if (trec) {
+        const int32_t fl = pfl | ((wtab && t < G) ? 2 : 0);
+        double* r = trec + ((int64_t)o * n_tiles + tl) * TRS;
+        r[0] = __builtin_bit_cast(double, make_int2(h, t));
+        r[1] = __builtin_bit_cast(double, make_int2(fl, 0));
+        if (fl & 2) {
+          const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
+#pragma unroll
+          for (int k = 0; k < K; ++k) r[2 + k] = mp[k];
+        }
+        if (!nnf && t - h > kHeavy) {
+          const int32_t k = atomicAdd(hcnt, 1);
+          hlist[k] = make_int4(tl, h, t, fl | (o << 8));
+        }
       }
-    }
-    if (hlist) {
-      __syncthreads();
-      if (tid == 0) hcnt[o] = shc;
     }
   }
   if (tid == 0) {
@@ -1549,6 +1565,15 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     counts[o * kCnt + 7] = 0;
   }
   PROM_TS(o * 16 + 8);
+}
+
+// tau of one chord in the exact (non-finite column) path.  With merged species (zf != nullptr) the
+// single column is N = dx sum_x n and Y = sum_s chi_s sigma_s: the reference's sum_s (N chi_s) sigma_s is
+// NaN for an infinite N wherever some chi_s sigma_s is not > 0 (zf[w]), which N Y alone would miss.
+__device__ __forceinline__ double exact_tau_merged(double N, double Y, const uint8_t* __restrict__ zf, int64_t w) {
+  double tau = N * Y;
+  if (zf && !__builtin_isfinite(N) && zf[w]) tau = __builtin_nan("");
+  return tau;
 }
 
 // ---- fast exp: acc + F * 2^(y/2048) with a 2048-entry table in LDS --------------------------------
@@ -1845,6 +1870,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
                                                   const double* __restrict__ wmom,
                                                   const double* __restrict__ sig,
                                                   const int2* __restrict__ win, int32_t n_tiles,
+                                                  const uint8_t* __restrict__ zfl,
                                                   unsigned long long* __restrict__ evals,
                                                   double* __restrict__ R) {
   constexpr Monos<NS> M{};
@@ -1977,6 +2003,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
         double tau = r[1] * sg[j][0];
 #pragma unroll
         for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[j][s];
+        if (NS == 1 && zfl) tau = exact_tau_merged(r[1], sg[j][0], zfl, live[j] ? tile + 64 * j + lane : n_wav - 1);
         acc[j] = acc[j] + F * exp(-tau);
       }
     }
@@ -2194,9 +2221,10 @@ __device__ __forceinline__ void tau_heavy(int32_t tile, int32_t hf, int32_t o, i
 }
 
 // Grid: n_heavy heavy wavefronts (blockIdx first), then one static wavefront per (tile, group of 4
-// phases).  Static wavefront: round trip 1 = its phases' windows and flags, sigma at its 128
-// wavelengths (2 per lane), the exp table; round trip 2 = the packed records of its light phases and
-// their tail moments.  Heavy wavefront: the per-phase counts, then its unit, then records and sigma.
+// phases).  Static wavefront: round trip 1 = its phases' tile records {h, t, flags, tail moments}
+// (k_order), sigma at its 128 wavelengths (2 per lane), the exp table; a second round trip only for
+// the packed records of non-empty light windows.  Heavy wavefront: the unit count and its first unit,
+// then records, sigma and moments.
 template <int NS>
 __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs4 tabv, const double* __restrict__ sig,
                                                                    const double* __restrict__ recs,
@@ -2208,17 +2236,18 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
                                                                    const double* __restrict__ fsum, int32_t n_pr,
                                                                    int32_t n_orb, int64_t n_wav,
                                                                    const double* __restrict__ wmom,
-                                                                   const int2* __restrict__ win, int32_t n_tiles,
-                                                                   const int4* __restrict__ hlist,
+                                                                   const double* __restrict__ trec, int32_t n_tiles,
+                                                                   const int4* __restrict__ hlist, int32_t hcap,
                                                                    const int32_t* __restrict__ hcnt,
-                                                                   int32_t n_heavy,
+                                                                   int32_t n_heavy, const uint8_t* __restrict__ zfl,
                                                                    unsigned long long* __restrict__ evals,
                                                                    double* __restrict__ R) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int ST = 1 + NS;
   constexpr int PQ = (4 * kHeavy * ST + 63) / 64;   // packed record loads per lane
-  constexpr int MV = (4 * K + 63) / 64;             // packed moment loads per lane
+  constexpr int TRS = 2 + K;                        // tile record: {h, t}, {flags, 0}, K moments
+  constexpr int TV = (4 * TRS + 63) / 64;           // tile-record loads per lane (four records)
   static_assert(4 * kHeavy * ST <= 2 * 64 * ST, "a group's packed records fit the wavefront's LDS slice");
   __shared__ double srec[kTP][2 * 64 * ST];   // per wavefront: two chunks of 64 records
   __shared__ double sexp[1024];                // 2^(i/1024)
@@ -2234,27 +2263,22 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
   const int32_t gw = blockIdx.x * kTP + wid;
   double* sr = srec[wid];
   if (gw < n_heavy) {
-    // ---- heavy wavefronts: items e = gw, gw + n_heavy, ... over 2 x (sum of hcnt) halves
-    int32_t U = 0;
-    for (int32_t o = 0; o < n_orb; ++o) U += hcnt[o];
+    // ---- heavy wavefronts: items e = gw, gw + n_heavy, ... over the 2 U halves of the U listed units;
+    //      the first unit is read with the count
+    const int32_t U = hcnt[0];
+    int4 en = hlist[min(gw >> 1, hcap - 1)];
 #pragma unroll
     for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
     __syncthreads();
     for (int32_t e = gw; e < 2 * U; e += n_heavy) {
-      int32_t u = e >> 1, o = 0;
-      for (; o < n_orb - 1; ++o) {
-        const int32_t c = hcnt[o];
-        if (u < c) break;
-        u -= c;
-      }
-      const int4 en = hlist[(int64_t)o * n_tiles + u];
+      if (e != gw) en = hlist[e >> 1];
       const int32_t tile = __builtin_amdgcn_readfirstlane(en.x), h = __builtin_amdgcn_readfirstlane(en.y);
-      const int32_t t = __builtin_amdgcn_readfirstlane(en.z), fl = __builtin_amdgcn_readfirstlane(en.w);
+      const int32_t t = __builtin_amdgcn_readfirstlane(en.z), w4 = __builtin_amdgcn_readfirstlane(en.w);
 #ifdef PROM_TRACE
       wrk += t - h;
 #endif
-      tau_heavy<NS>(tile, e & 1, o, h, t, fl, tabv, sig, recs, mrecs, tfrac, n_pr, n_wav, wmom, evals, lane, e, sr,
-                    sexp, R);
+      tau_heavy<NS>(tile, e & 1, w4 >> 8, h, t, w4 & 255, tabv, sig, recs, mrecs, tfrac, n_pr, n_wav, wmom, evals,
+                    lane, e, sr, sexp, R);
     }
   } else {
     // ---- static wavefront: tile, phases o0 .. o0 + np - 1
@@ -2262,17 +2286,12 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
     const int32_t tile = sw % n_tiles, o0 = (sw / n_tiles) * 4;
     const bool has = o0 < n_orb;
     const int32_t np = has ? min(4, n_orb - o0) : 0;
-    int32_t h[4], t[4], fl[4], n[4];
+    // element p TRS + i (lane e & 63 of tv[e >> 6]) holds double i of phase p's tile record
+    double tv[TV];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      h[p] = 0; t[p] = 0; fl[p] = 0;
-      if (p < np) {
-        const int32_t o = o0 + p;
-        const int2 wv = win[(int64_t)o * n_tiles + tile];
-        const int32_t* cp = counts + o * kCnt;
-        h[p] = wv.x; t[p] = wv.y;
-        fl[p] = (cp[5] ? 1 : 0) | ((cp[6] && wv.y < cp[4]) ? 2 : 0) | (cp[3] ? 4 : 0);
-      }
+    for (int q = 0; q < TV; ++q) {
+      const int e = 64 * q + lane, p = e / TRS;
+      tv[q] = p < np ? trec[((int64_t)(o0 + p) * n_tiles + tile) * TRS + (e - p * TRS)] : 0.0;
     }
     bool live[2];
     double sg[2][NS];
@@ -2289,6 +2308,15 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
 #pragma unroll
     for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
     __syncthreads();
+    int32_t h[4], t[4], fl[4], n[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int2 ht = __builtin_bit_cast(int2, lane_read(tv[(p * TRS) >> 6], (p * TRS) & 63));
+      const int2 ff = __builtin_bit_cast(int2, lane_read(tv[(p * TRS + 1) >> 6], (p * TRS + 1) & 63));
+      h[p] = p < np ? ht.x : 0;
+      t[p] = p < np ? ht.y : 0;
+      fl[p] = p < np ? ff.x : 0;
+    }
     // light phases (window <= kHeavy records, not exact): packed; heavy ones are another wavefront's
     int32_t off[5];
     off[0] = 0;
@@ -2310,18 +2338,6 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
         const int32_t fp = p == 0 ? fl[0] : (p == 1 ? fl[1] : (p == 2 ? fl[2] : fl[3]));
         const int32_t op = p == 0 ? off[0] : (p == 1 ? off[1] : (p == 2 ? off[2] : off[3]));
         pre[q] = ((fp & 1) ? mrecs : recs)[((int64_t)(o0 + p) * n_pr + hp) * ST + (e - op)];
-      }
-    }
-    double mv[MV];
-#pragma unroll
-    for (int q = 0; q < MV; ++q) {
-      const int32_t e = 64 * q + lane;
-      const int p = e / K, k = e - p * K;
-      mv[q] = 0.0;
-      if (p < np) {
-        const int32_t tp = p == 0 ? t[0] : (p == 1 ? t[1] : (p == 2 ? t[2] : t[3]));
-        const int32_t np_ = p == 0 ? n[0] : (p == 1 ? n[1] : (p == 2 ? n[2] : n[3]));
-        if (np_ >= 0) mv[q] = wmom[((int64_t)(o0 + p) * (n_pr + 1) + tp) * K + k];
       }
     }
 #pragma unroll
@@ -2357,7 +2373,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
         if (fl[p] & 2) {
           double mm[K];
 #pragma unroll
-          for (int k = 0; k < K; ++k) mm[k] = lane_read(mv[(p * K + k) >> 6], (p * K + k) & 63);
+          for (int k = 0; k < K; ++k) mm[k] = lane_read(tv[(p * TRS + 2 + k) >> 6], (p * TRS + 2 + k) & 63);
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             double qv[NS];
@@ -2388,6 +2404,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
             double tau = r[1] * sg[j][0];
 #pragma unroll
             for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[j][s];
+            if (NS == 1 && zfl)
+              tau = exact_tau_merged(r[1], sg[j][0], zfl, live[j] ? (int64_t)tile * kTW + 64 * j + lane : n_wav - 1);
             acc[j] = acc[j] + F * exp(-tau);
           }
         }
@@ -2839,7 +2857,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
                      tr.moon_R.as<double>(), smax, tr.cull_tau, rs.ncol.as<double>(),                       \
                      rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>(), \
-                     pre_sigma ? rs.tq.as<float2>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale)
+                     pre_sigma ? rs.tq.as<float2>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale,    \
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, rs.zfl.as<uint8_t>())
 #define PROM_COLS_L(NSV)                       \
   if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
   else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
@@ -2924,7 +2943,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>(), \
                      pre_sigma ? rs.tq.as<float2>() : nullptr, n_wtiles, rs.win.as<int2>(),             \
                      (pre_sigma && tr.plan) ? rs.hlist.as<int4>() : nullptr,                           \
-                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr)
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr,                         \
+                     (pre_sigma && tr.plan) ? rs.trec.as<double>() : nullptr)
     switch (na) {
       case 1: PROM_CHW(1); break;
       case 2: PROM_CHW(2); break;
@@ -3003,7 +3023,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0,                  \
                      tabs4, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                           \
                      tr.n_orb, tr.n_wav, rs.wenv.as<int32_t>(), rs.wmom.as<double>(), rs.sig.as<double>(),  \
-                     rs.win.as<int2>(), n_wtiles, tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
+                     rs.win.as<int2>(), n_wtiles, msp ? rs.zfl.as<uint8_t>() : nullptr,                     \
+                     tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
 #define PROM_TAUW_NS(PMV, UV)            \
   switch (na) {                          \
     case 1: PROM_TAUW(1, PMV, UV); break; \
@@ -3036,8 +3057,9 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   hipExtLaunchKernelGGL((k_tau_p<NSV>), dim3(blocks), dim3(kBlock), 0, s,                                 \
                         ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, tabs4, rs.sig.as<double>(),        \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
-                        rs.wmom.as<double>(), rs.win.as<int2>(), n_wtiles, rs.hlist.as<int4>(),          \
-                        rs.hcnt.as<int32_t>(), (int32_t)n_heavy,                                         \
+                        rs.wmom.as<double>(), rs.trec.as<double>(), n_wtiles, rs.hlist.as<int4>(),      \
+                        (int32_t)(tr.n_orb * n_wtiles), rs.hcnt.as<int32_t>(), (int32_t)n_heavy,        \
+                        msp ? rs.zfl.as<uint8_t>() : nullptr,                                            \
                         tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
       switch (na) {
         case 1: PROM_TAUP(1); break;

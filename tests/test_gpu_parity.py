@@ -356,3 +356,76 @@ def test_species_merge(dev, name, monkeypatch):
     assert rel(R_m, R_s) < 1e-13
     if name != "C2":
         assert rel(R_m, load("transit_" + name)["R"]) < R_TOL
+
+
+@pytest.mark.parametrize("plan", ["1", "0"])
+def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
+    """A user density plugin (host-tabulated n(c, x)) with one infinite sample: that chord's column is
+    inf, its phase takes the exact chord-order path (ocml exp, no windows), e^{-inf sigma} = 0 and
+    inf * 0 = NaN where sigma == 0, as in the reference dataflow (oracle on the same tabulated input).
+    Both the planned (k_tau_p) and the k_tau_w fast path."""
+    import copy
+    from prometheus_amd import configs
+    monkeypatch.setenv("PROM_TAU_PLAN", plan)
+    cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
+                          res_low=5e-9, res_high=1e-10)
+    tr = _product_transit(cfg)
+    scen, dop, grids = O.from_setup(cfg)
+    base = scen[0]
+    cg = O.chord_grid(grids)
+    x = O.x_axis(grids)
+    col = O.number_density(base, x, cg[:, 0], cg[:, 1], cg[:, 2]).sum(axis=1)
+    orbs = O.orbphase_axis(grids)
+    pl = base.planet
+    y, z = cg[:, 1] * np.sin(cg[:, 0]), cg[:, 1] * np.cos(cg[:, 0])
+    blocked = np.sqrt((y - pl.a * np.sin(cg[:, 2])) ** 2 + z ** 2) < pl.R
+    cand = np.where((cg[:, 2] == orbs[1]) & ~blocked)[0]
+    k0 = cand[np.argmax(col[cand])]   # the unblocked chord of phase 1 with the largest column
+    tphi, trho, torb = cg[k0]
+
+    def fn(x_, phi_, rho_, orb_):
+        n = np.array(O.number_density(base, x_, phi_, rho_, orb_), dtype=np.float64)
+        m = (np.isclose(phi_, tphi, rtol=1e-12, atol=0) & np.isclose(rho_, trho, rtol=1e-12, atol=0) &
+             np.isclose(orb_, torb, rtol=1e-12, atol=1e-15))
+        n[m, 3] = np.inf
+        return n
+
+    tab = O.Scenario("tabulated", base.planet, {}, constituents=base.constituents, T=base.T, tabulated_fn=fn)
+    Ro = O.transit_depth([tab], dop, grids, tr.wavelength, O.build_tables([tab], grids))
+    d0 = tr.atmosphere.densityDistributionList[0]
+
+    class Plug(type(d0)):
+        def densityModel(self):
+            raise NotImplementedError
+
+        def calculateNumberDensity(self, x_, phi_, rho_, orb_):
+            return fn(x_, phi_, rho_, orb_)
+
+    p = copy.copy(d0)
+    p.__class__ = Plug
+    tr.atmosphere.densityDistributionList[0] = p
+    R = tr.sumOverChords(devices=[0])
+    st = tr.last_stats[-1]
+    print("plan", plan, "exact phases", st["exact_phases"], "NaN points", int(np.isnan(Ro).sum()), "variant",
+          st["tau_kernel_variant"])
+    assert st["exact_phases"] == 1
+    assert np.array_equal(np.isnan(R), np.isnan(Ro))
+    m = ~np.isnan(Ro)
+    assert rel(R[m], Ro[m]) < R_TOL
+
+
+def test_graph_replay_matches(dev, monkeypatch):
+    """PROM_GRAPH=1: untimed fast-path runs replay one captured hipGraph per pipeline slot; every
+    replayed run's R is bitwise the directly launched run's."""
+    monkeypatch.setenv("PROM_GRAPH", "1")
+    d = load("transit_C2r")
+    tr = _product_transit(json.loads(str(d["config"])))
+    host = tr._host_inputs()
+    dev.transit_set(tr._problem(dev, host, 0, len(tr.wavelength), 0.0))
+    dev.transit_run(stats=True)
+    R0 = dev.transit_result()
+    for _ in range(9):
+        dev.transit_run()
+        dev.synchronize()
+        assert np.array_equal(dev.transit_result(), R0)
+    assert rel(R0, d["R"]) < R_TOL
