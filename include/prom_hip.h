@@ -214,9 +214,12 @@ int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bo
                                 int64_t* count_out, double* max_out);
 
 /* Live per-run timing of the tau kernel without per-run synchronisation: between prom_timing_begin
- * and prom_timing_end every prom_transit_run carries start/stop events on its tau kernel's dispatch;
- * prom_timing_end waits for them and returns ms[run][4] = {NaN, NaN, tau, NaN} for up to max_runs
- * runs (n_runs receives the count).  Stage times of a single run come from prom_transit_run's stats.
+ * and prom_timing_end every timed prom_transit_run carries a HIP event pair (the ordering kernel's
+ * completion -> the tau kernel's completion) and, for the planned tau kernel k_tau_p, device-clock
+ * stamps of its workgroups; prom_timing_end waits for them and returns ms[run][4] =
+ * {NaN, NaN, tau_events, tau_device} for up to max_runs runs (n_runs receives the count).
+ * tau_events includes the tau kernel's dispatch behind the ordering kernel; tau_device is the span
+ * from its first workgroup's start to its last workgroup's end (NaN for other tau kernels).  Stage times of a single run come from prom_transit_run's stats.
  * prom_timing_stride(ctx, k) (k >= 1, default 1, kept until changed) times only every k-th run of the
  * window: events on a dispatch cost the host ~13 us, more than a run's GPU time, so a throughput
  * measurement samples the kernel durations instead of timing every run. */

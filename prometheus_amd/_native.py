@@ -275,7 +275,9 @@ class Device:
         self._check(self.lib.prom_timing_begin(self.h), "prom_timing_begin")
 
     def timing_end(self, max_runs: int = 4096) -> np.ndarray:
-        """ms[run] = (density, sigma, tau, total) of every run since timing_begin (live hipEvents)."""
+        """ms[run] = (NaN, NaN, tau_events, tau_device) of every timed run since timing_begin: the HIP
+        event interval from the ordering kernel's completion to the tau kernel's, and the tau kernel's
+        span on the device clock (first workgroup start -> last workgroup end; NaN unless k_tau_p)."""
         ms = np.zeros((max_runs, 4))
         n = C.c_int32(0)
         self._check(self.lib.prom_timing_end(self.h, max_runs, _d(ms), C.byref(n)), "prom_timing_end")

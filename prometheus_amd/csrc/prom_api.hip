@@ -628,6 +628,15 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
         ctx->tev.push_back(e);
       }
       ev = &ctx->tev[4 * (size_t)ctx->timed_runs];
+      constexpr int32_t kTsCap = 8192;   // workgroups a tau launch may stamp
+      if (ctx->tsbuf.size() <= (size_t)ctx->timed_runs) {
+        ctx->tsbuf.emplace_back();
+        ctx->tsbuf.back().ensure(sizeof(unsigned long long) * 2 * kTsCap);
+      }
+      if (ctx->ts_blocks.size() <= (size_t)ctx->timed_runs) ctx->ts_blocks.resize(ctx->timed_runs + 1);
+      ctx->tr.ts_out = ctx->tsbuf[ctx->timed_runs].as<unsigned long long>();
+      ctx->tr.ts_cap = kTsCap;
+      ctx->tr.ts_blocks = 0;
       ++ctx->timed_runs;
     }
     tr.count_evals = stats != nullptr;
@@ -661,6 +670,9 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     }
     tr.last = si;
     tr.count_evals = false;
+    if (timed) ctx->ts_blocks[ctx->timed_runs - 1] = tr.ts_blocks;
+    tr.ts_out = nullptr;
+    tr.ts_blocks = 0;
 
     tr.ran = true;
     if (stats) {
@@ -769,13 +781,29 @@ int32_t prom_timing_end(prom_ctx* ctx, int32_t max_runs, double* ms, int32_t* n_
     ctx->timing = false;
     const int32_t n = std::min(ctx->timed_runs, std::max(max_runs, 0));
     for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
+    int clock_khz = 0;
+    PROM_HIP(hipDeviceGetAttribute(&clock_khz, hipDeviceAttributeWallClockRate, ctx->device));
+    std::vector<unsigned long long> ts;
     for (int32_t r = 0; r < n; ++r) {
       hipEvent_t* e = &ctx->tev[4 * (size_t)r];
       float v[4];
-      // timed runs carry only the tau kernel's start/stop pair (no extra packets between kernels)
+      // timed runs carry one event pair: the ordering kernel's completion -> the tau kernel's
+      // completion (the tau kernel's run time plus its dispatch behind the ordering kernel)
       PROM_HIP(hipEventElapsedTime(&v[2], e[2], e[3]));
       ms[4 * r + 0] = ms[4 * r + 1] = ms[4 * r + 3] = std::nan("");
       ms[4 * r + 2] = v[2];
+      // and the tau kernel's own span on the device clock: first workgroup start -> last workgroup end
+      const int32_t nb = r < (int32_t)ctx->ts_blocks.size() ? ctx->ts_blocks[r] : 0;
+      if (nb > 0 && clock_khz > 0) {
+        ts.resize(2 * (size_t)nb);
+        PROM_HIP(hipMemcpy(ts.data(), ctx->tsbuf[r].p, sizeof(unsigned long long) * ts.size(), hipMemcpyDeviceToHost));
+        unsigned long long lo = ~0ull, hi = 0;
+        for (int32_t b = 0; b < nb; ++b) {
+          lo = std::min(lo, ts[2 * (size_t)b]);
+          hi = std::max(hi, ts[2 * (size_t)b + 1]);
+        }
+        if (hi >= lo) ms[4 * r + 3] = (double)(hi - lo) / (double)clock_khz;
+      }
     }
     *n_runs = ctx->timed_runs;
     ctx->timed_runs = 0;

@@ -228,6 +228,11 @@ struct TransitDev {
   SigTabs4 sigtab_m{};                      // t[0]: the effective absorber's normalisation (ncoef, nscale)
   DevBuf sigma_max_m;                       // [1] sum_s chi_s sigma_max_s
   int32_t taup_resident = 0;                // k_tau_p wavefronts resident at once (set at the first run)
+  // timed runs: k_tau_p stamps each workgroup's first and last device-clock tick into ts_out[2 b],
+  // ts_out[2 b + 1] when it has at most ts_cap workgroups; ts_blocks reports the count (0: no stamps)
+  unsigned long long* ts_out = nullptr;
+  int32_t ts_cap = 0;
+  int32_t ts_blocks = 0;
   DevBuf molslot;                           // [n_mol] MolSlotDev
   DevBuf mol_ip;                            // [n_mol][n_orb][n_pr][n_x] int32 P bracket (-1: out of table)
   DevBuf mol_wp;                            // [n_mol][n_orb][n_pr][n_x] P weight
@@ -264,6 +269,8 @@ struct prom_ctx {
   prom::DevBuf scratch[6];
   bool timing = false;
   std::vector<hipEvent_t> tev;   // pool, 4 per timed run
+  std::vector<prom::DevBuf> tsbuf;     // pool, one per timed run: tau-kernel workgroup clock stamps
+  std::vector<int32_t> ts_blocks;      // per timed run: stamped workgroups (0: none)
   int32_t timed_runs = 0;
   int32_t timing_stride = 1;     // prom_timing_stride: events on every k-th run of a timing window
   int64_t window_runs = 0;       // runs since prom_timing_begin

@@ -1146,6 +1146,11 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   __shared__ double pd_[NW][2];
   __shared__ double pm_[NW][K + 2];
   __shared__ int32_t pg_[NW];
+  __shared__ int32_t sHc[2];                     // step 7: heavy units staged in LDS, their global base
+  // step 7 reads the tail moments at every tile's window end: with one effective species they are
+  // also kept in LDS (rows 0 .. G) when they fit, instead of a dependent HBM read per tile
+  constexpr int MOMC = NS == 1 ? 4096 : 1;
+  __shared__ double sMom[MOMC];
   const int32_t o = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int32_t* fl = flags + (int64_t)o * n_pr;
@@ -1156,6 +1161,15 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   for (int s = 0; s < NS; ++s) cs[s] = tabv.t[s].ncoef;
 
   PROM_TS(o * 16 + 0);
+  constexpr int TQP = 4;   // tiles per thread whose Q range is loaded now, for step 7
+  float2 tqv[TQP];
+#pragma unroll
+  for (int k = 0; k < TQP; ++k) {
+    const int32_t tl = tid + k * kWBlock;
+    tqv[k] = (tq && tl < n_tiles) ? tq[tl] : make_float2(0.0f, 0.0f);
+  }
+  bool mcache = false;
+  if (tid == 0) sHc[0] = 0;   // (barriers of steps 1-6 order it before step 7)
   for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }
   // ---- 1. load, classify, keys, combined scan/reduction
   double fs = 0.0, ts = 0.0;
@@ -1420,6 +1434,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       gtot += pg_[w];
     }
     G = gtot;
+    mcache = window && NS == 1 && (G + 1) * K <= MOMC;
     PROM_TS(o * 16 + 3);
     // ---- 6. records, envelopes, moments (group heads), in the sorted order
     double* mo = mrecs + (int64_t)o * n_pr * ST;
@@ -1472,12 +1487,19 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           atomicAdd(&hB[env_slot(Bg)], 1);
           atomicAdd(&hA[env_slot(Ag)], 1);
 #pragma unroll
-          for (int m = 0; m < K; ++m) mm[(int64_t)gi * K + m] = M.c[m] * msum[m];
+          for (int m = 0; m < K; ++m) {
+            const double v = M.c[m] * msum[m];
+            mm[(int64_t)gi * K + m] = v;
+            if (mcache) sMom[gi * K + m] = v;
+          }
         }
       }
     }
     if (window) {
-      if (tid < K) mm[(int64_t)G * K + tid] = 0.0;
+      if (tid < K) {
+        mm[(int64_t)G * K + tid] = 0.0;
+        if (mcache) sMom[G * K + tid] = 0.0;
+      }
       __syncthreads();
       PROM_TS(o * 16 + 4);
       // tab_t[v] = #{g : B_g >= X_v} = sum of hB over slots >= v + 1 (and likewise tab_h from hA):
@@ -1521,11 +1543,13 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     //         tiles whose window holds more than kHeavy records go to the heavy-unit list (one global
     //         counter, zeroed by k_columns8; any order)
     __syncthreads();   // moments (step 6) visible to the whole workgroup
+    PROM_TS(o * 16 + 5);
     const bool wtab = sorted && window;
     const int32_t pfl = (sorted ? 1 : 0) | (nnf ? 4 : 0);
     constexpr int TRS = 2 + K;
-    for (int32_t tl = tid; tl < n_tiles; tl += kWBlock) {
-      const float2 q = tq[tl];
+    constexpr int HCAP = (int)(sizeof(skey) / sizeof(int4));
+    int4* hbuf = reinterpret_cast<int4*>(skey);
+    auto tile_window = [&](int32_t tl, float2 q) {
       int32_t h = 0, t = sorted ? G : nact;
       if (wtab && q.x >= 0.0f) {
         const int vt = env_floor((float)tail_eps<NS>() / q.y * (1.0f - 0x1p-20f));
@@ -1541,15 +1565,31 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         r[0] = __builtin_bit_cast(double, make_int2(h, t));
         r[1] = __builtin_bit_cast(double, make_int2(fl, 0));
         if (fl & 2) {
-          const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
+          const double* mp = mcache ? sMom + t * K : wmom + ((int64_t)o * (n_pr + 1) + t) * K;
 #pragma unroll
           for (int k = 0; k < K; ++k) r[2 + k] = mp[k];
         }
         if (!nnf && t - h > kHeavy) {
-          const int32_t k = atomicAdd(hcnt, 1);
-          hlist[k] = make_int4(tl, h, t, fl | (o << 8));
+          // staged in LDS over the sort keys (free after step 6); one global append per workgroup
+          const int4 e = make_int4(tl, h, t, fl | (o << 8));
+          const int32_t k = atomicAdd(&sHc[0], 1);
+          if (k < HCAP) hbuf[k] = e;
+          else hlist[atomicAdd(hcnt, 1)] = e;
         }
       }
+    };
+#pragma unroll
+    for (int k = 0; k < TQP; ++k) {
+      const int32_t tl = tid + k * kWBlock;
+      if (tl < n_tiles) tile_window(tl, tqv[k]);
+    }
+    for (int32_t tl = tid + TQP * kWBlock; tl < n_tiles; tl += kWBlock) tile_window(tl, tq[tl]);
+    if (trec) {
+      __syncthreads();
+      const int32_t nh = sHc[0] < HCAP ? sHc[0] : HCAP;
+      if (tid == 0) sHc[1] = nh > 0 ? atomicAdd(hcnt, nh) : 0;
+      __syncthreads();
+      for (int32_t i = tid; i < nh; i += kWBlock) hlist[sHc[1] + i] = hbuf[i];
     }
   }
   if (tid == 0) {
@@ -2145,6 +2185,7 @@ __device__ __forceinline__ void tau_phase(const double (&sg)[LPL][NS], const Sig
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      #pragma unroll 4
       for (int32_t r = 0; r < nr; ++r) {
         const double F = buf[r * ST];
         double Nr[NS];
@@ -2241,6 +2282,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
                                                                    const int32_t* __restrict__ hcnt,
                                                                    int32_t n_heavy, const uint8_t* __restrict__ zfl,
                                                                    unsigned long long* __restrict__ evals,
+                                                                   unsigned long long* __restrict__ tstamp,
                                                                    double* __restrict__ R) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
@@ -2262,6 +2304,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int32_t gw = blockIdx.x * kTP + wid;
   double* sr = srec[wid];
+  // timed runs: the workgroup's first device-clock tick (the kernel's duration is the span over all)
+  if (tstamp && threadIdx.x == 0) tstamp[2 * blockIdx.x] = wall_clock64();
   if (gw < n_heavy) {
     // ---- heavy wavefronts: items e = gw, gw + n_heavy, ... over the 2 U halves of the U listed units;
     //      the first unit is read with the count
@@ -2357,6 +2401,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
       if (n[p] >= 0) {
         const double* buf = sr + off[p];
         double acc[2] = {0.0, 0.0};
+        #pragma unroll 4
         for (int32_t r = 0; r < n[p]; ++r) {
           const double F = buf[r * ST];
           double Nr[NS];
@@ -2415,6 +2460,10 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
           if (live[j]) R[(int64_t)o * n_wav + (int64_t)tile * kTW + 64 * j + lane] = (acc[j] + tfv[p] * fs) / fs;
       }
     }
+  }
+  if (tstamp) {
+    __syncthreads();
+    if (threadIdx.x == 0) tstamp[2 * blockIdx.x + 1] = wall_clock64();
   }
 #ifdef PROM_TRACE
   {
@@ -2844,6 +2893,12 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // no separate event packets between the kernels
   hipEvent_t ev0 = (ev && stage_events) ? ev[0] : nullptr;
   hipEvent_t ev1 = (ev && stage_events) ? ev[1] : nullptr;
+  // timed runs (no stage events): the tau kernel's interval opens at the ordering kernel's completion
+  // (its stop event), not at the tau packet's own start, which the command processor stamps before the
+  // packet's barrier on the ordering kernel resolves -- so it matches rocprofv3's dispatch durations
+  const bool tau_fast = !(tr.n_mol > 0) && tr.exp_mode && wpath && tr.window;
+  hipEvent_t ev_ord = ev ? (stage_events ? ev1 : (tau_fast ? ev[2] : nullptr)) : nullptr;
+  hipEvent_t ev_tau0 = (ev && stage_events) ? ev[2] : nullptr;
   // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
   if (cols8) {
@@ -2935,7 +2990,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   const int32_t n_wtiles = (int32_t)((tr.n_wav + kTW - 1) / kTW);
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
-  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev1, 0,                \
+  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev_ord, 0,             \
                      rs.flags.as<int32_t>(),                                                              \
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
                      tr.window ? 1 : 0, tabs4, rs.recs.as<double>(),                                     \
@@ -3020,7 +3075,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   } else if (tr.exp_mode && wpath && tr.window) {
 #define PROM_TAUW(NSV, PMV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_tau_w<NSV, UV>), dim3((unsigned)((tr.n_wav + kTW - 1) / kTW), (unsigned)((tr.n_orb + kTP - 1) / kTP)), \
-                     dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0,                  \
+                     dim3(kBlock), 0, s, ev_tau0, ev ? ev[3] : nullptr, 0,                              \
                      tabs4, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                           \
                      tr.n_orb, tr.n_wav, rs.wenv.as<int32_t>(), rs.wmom.as<double>(), rs.sig.as<double>(),  \
                      rs.win.as<int2>(), n_wtiles, msp ? rs.zfl.as<uint8_t>() : nullptr,                     \
@@ -3053,14 +3108,16 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       n_heavy = (n_heavy + kTP - 1) / kTP * kTP;
       const unsigned blocks = (unsigned)((n_heavy + n_static + kTP - 1) / kTP);
       *variant = 30 + (na <= 4 ? na : 0);
+      unsigned long long* tsp = (tr.ts_out && (int64_t)blocks <= tr.ts_cap) ? tr.ts_out : nullptr;
+      tr.ts_blocks = tsp ? (int32_t)blocks : 0;
 #define PROM_TAUP(NSV)                                                                                  \
   hipExtLaunchKernelGGL((k_tau_p<NSV>), dim3(blocks), dim3(kBlock), 0, s,                                 \
-                        ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, tabs4, rs.sig.as<double>(),        \
+                        ev_tau0, ev ? ev[3] : nullptr, 0, tabs4, rs.sig.as<double>(),                     \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
                         rs.wmom.as<double>(), rs.trec.as<double>(), n_wtiles, rs.hlist.as<int4>(),      \
                         (int32_t)(tr.n_orb * n_wtiles), rs.hcnt.as<int32_t>(), (int32_t)n_heavy,        \
                         msp ? rs.zfl.as<uint8_t>() : nullptr,                                            \
-                        tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
+                        tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tsp, R)
       switch (na) {
         case 1: PROM_TAUP(1); break;
         case 2: PROM_TAUP(2); break;

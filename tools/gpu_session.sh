@@ -26,6 +26,8 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py ;;
     benchfast) step bench 600 python bench.py --no-cpu-baseline ;;
     traffic) step traffic 700 bash tools/bench_traffic.sh ${TAG:-r01c} ;;
+    trace) step trace 300 python tools/trace_kernels.py C2 ;;
+    prof1) PROM_PIPELINE=1 step rocprof1 600 rocprofv3 --kernel-trace --stats -d $OUT/prof1 -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
   esac
 done
