@@ -181,7 +181,9 @@ def main():
     # dominant kernel: k_tau_p (planned windowed tau/exp/disk-sum; k_tau_w when the planned path does
     # not apply); mean launch duration from the start/stop events carried on its own dispatch packets
     # over the timed runs
-    tau_kernel = "k_tau_p" if st.get("tau_kernel_variant", 0) // 10 == 3 else "k_tau_w"
+    # (molecular species: the fused molecular kernel k_tau_mol)
+    tau_kernel = ("k_tau_mol" if getattr(prob, "n_molecules", 0) else
+                  "k_tau_p" if st.get("tau_kernel_variant", 0) // 10 == 3 else "k_tau_w")
     # k_tau_p: its span on the device clock (first workgroup start -> last workgroup end), which is what
     # rocprofv3's dispatch durations measure; the HIP event pair (ordering kernel done -> tau kernel
     # done) also holds the tau kernel's dispatch behind the ordering kernel and is reported beside it

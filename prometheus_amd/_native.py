@@ -363,6 +363,7 @@ class TransitInputs:
         self.struct = s
         self.keepalive = keep
         self.n_atoms = n_atoms
+        self.n_molecules = sum(1 for sc in scenarios for c in sc["constituents"] if c.get("is_molecule", False))
 
 
 _default_device = int(os.environ.get("PROMETHEUS_DEVICE", "0"))
