@@ -198,7 +198,12 @@ def main():
     evals = st["exp_evals"]
     tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, n_atoms)
     achieved_gbs = tau_bytes / (tau_ms * 1e-3) / 1e9
-    flops = evals * flops_per_eval(n_atoms)
+    flops_unit = flops_per_eval(n_atoms)
+    if tau_kernel == "k_tau_mol":
+        # SURVEY.md 8(d) molecular count: per chord-wavelength, n_x x (P lerp + 10^v + FMA) = 6 n_x flops,
+        # on top of the atomic exp evaluation
+        flops_unit += 6 * len(host["x"])
+    flops = evals * flops_unit
     traffic = latest_profile_traffic("prom::" + tau_kernel)
     # end-to-end (host prep + H2D + run + D2H) for reference, one call
     t_e2e = time.perf_counter()
@@ -228,7 +233,7 @@ def main():
                      "tau_ms_source": tau_clock, "tau_ms_hip_events": tau_ms_events,
                      "tau_ms_sampled_runs": int(len(ms_runs)),
                      "exp_evals": evals, "chord_lambda_evals": cle,
-                     "valu": {"flops": flops, "flops_per_exp_eval": flops_per_eval(n_atoms),
+                     "valu": {"flops": flops, "flops_per_exp_eval": flops_unit,
                               "achieved_tflops": flops / (tau_ms * 1e-3) / 1e12,
                               "peak_tflops": FP64_VALU_PEAK_TFLOPS}},
         "stage_ms_single_run": {"columns_order": st["ms_density"], "tau": st["ms_tau"], "total": st["ms_total"]},
