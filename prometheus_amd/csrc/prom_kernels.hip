@@ -2576,9 +2576,11 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
     const int32_t* ipl = act_ip + (int64_t)o * n_pr;
     double acc = 0.0;
     const double scale = exact ? 1.0 : kMinus2048OverLn2;
+    int32_t ip_next = n_act > 0 ? ipl[0] : 0;
     for (int32_t ci = 0; ci < n_act; ++ci) {
       const double* r = rec + (int64_t)ci * ST;
-      const int32_t ip = ipl[ci];
+      const int32_t ip = ip_next;
+      if (ci + 1 < n_act) ip_next = ipl[ci + 1];   // the next chord's index is in flight meanwhile
       double tau = 0.0;
 #pragma unroll
       for (int s = 0; s < NSA; ++s) tau = tau + r[1 + s] * sg[s];
@@ -2588,6 +2590,8 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
         const int64_t base = ((int64_t)m * nc + (int64_t)o * n_pr + ip) * n_x;
         const double* um = ul + (int64_t)m * max_np * kBlock + threadIdx.x;
         double sm = 0.0;
+        // (uniform per wavefront: scalar loads, batched by the unroll)
+#pragma unroll 10
         for (int32_t ix = 0; ix < n_x; ++ix) {
           const int32_t pi = mip[base + ix];
           if (pi < 0) continue;
