@@ -75,6 +75,14 @@ int32_t prom_voigt_sigma(prom_ctx* ctx, int64_t n, const double* x, int32_t n_li
 int32_t prom_table_lookup(prom_ctx* ctx, int32_t table_id, int64_t n_targets, const double* targets,
                           double* out);
 
+/* Release a table's device memory; its id is reused by a later upload.  The reference drops its
+ * interp1d objects with the constituent (gasProperties.py:694-715, :34-51 builds one per call); a
+ * transit problem set on this context that reads the table is invalidated (prom_transit_run then
+ * fails with PROM_E_STATE until prom_transit_set is called again). */
+int32_t prom_table_free(prom_ctx* ctx, int32_t table_id);
+/* Live tables on the context (atomic, molecular) and the device bytes they hold. */
+int32_t prom_table_count(prom_ctx* ctx, int32_t* n_atomic, int32_t* n_molecular, int64_t* device_bytes);
+
 /* ---- molecular tables (MolecularConstituent, gasProperties.py:765-818) ----------------------
  * Axes in the reference's units after its conversions: P [dyn cm^-2] (= p[Pa] * 10), T [K],
  * wavelength [cm] (= 1/bin_edges reversed, increasing); log_sigma[n_p][n_t][n_w] = log10(xsec + offset)
@@ -87,6 +95,8 @@ int32_t prom_molecular_upload(prom_ctx* ctx, int32_t n_p, const double* P, int32
 int32_t prom_molecular_sigma(prom_ctx* ctx, int32_t table_id, int64_t n_chords, int32_t n_x,
                              const double* P, double T, int64_t n_wav, const double* wavelength,
                              double* sigma_out);
+/* Release a molecular table (see prom_table_free). */
+int32_t prom_molecular_free(prom_ctx* ctx, int32_t table_id);
 
 /* ---- density scenarios (calculateNumberDensity, gasProperties.py:143-516) ------------------- */
 enum prom_density_kind {

@@ -93,6 +93,9 @@ SIGNATURES = {
     "prom_voigt_sigma": (C.c_int32, [C.c_void_p, C.c_int64, _dp, C.c_int32, _dp, _dp, _dp, C.c_double,
                                      C.c_double, _dp]),
     "prom_table_lookup": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int64, _dp, _dp]),
+    "prom_table_free": (C.c_int32, [C.c_void_p, C.c_int32]),
+    "prom_table_count": (C.c_int32, [C.c_void_p, _ip, _ip, C.POINTER(C.c_int64)]),
+    "prom_molecular_free": (C.c_int32, [C.c_void_p, C.c_int32]),
     "prom_molecular_upload": (C.c_int32, [C.c_void_p, C.c_int32, _dp, C.c_int32, _dp, C.c_int64, _dp, _dp,
                                           C.c_double, _ip]),
     "prom_molecular_sigma": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, _dp, C.c_double,
@@ -168,6 +171,9 @@ class Device:
         self.h = h
         self.device = int(device)
         self._keep = []
+        # tables whose host objects were collected: freed at the next table or problem upload (a
+        # finalizer may run while another thread is inside a call on this context)
+        self._pending_free: list = []
 
     def close(self):
         if getattr(self, "h", None):
@@ -189,7 +195,27 @@ class Device:
         self._check(self.lib.prom_synchronize(self.h), "prom_synchronize")
 
     # ---- tables -----------------------------------------------------------------------
+    def release_later(self, molecular: bool, table_id: int) -> None:
+        """Queue a table for prom_table_free / prom_molecular_free (safe from finalizers)."""
+        self._pending_free.append((bool(molecular), int(table_id)))
+
+    def _drain_frees(self) -> None:
+        while self._pending_free:
+            mol, tid = self._pending_free.pop()
+            self.table_free(tid, molecular=mol)
+
+    def table_free(self, table_id: int, molecular: bool = False) -> None:
+        fn = self.lib.prom_molecular_free if molecular else self.lib.prom_table_free
+        self._check(fn(self.h, int(table_id)), "prom_molecular_free" if molecular else "prom_table_free")
+
+    def table_count(self):
+        """(live atomic tables, live molecular tables, device bytes they hold)."""
+        a, m, b = C.c_int32(0), C.c_int32(0), C.c_int64(0)
+        self._check(self.lib.prom_table_count(self.h, C.byref(a), C.byref(m), C.byref(b)), "prom_table_count")
+        return int(a.value), int(m.value), int(b.value)
+
     def table_upload(self, x, y, offset: float) -> int:
+        self._drain_frees()
         x, y = _f64(x), _f64(y)
         tid = C.c_int32(-1)
         self._check(self.lib.prom_table_upload(self.h, len(x), _d(x), _d(y), float(offset), C.byref(tid)),
@@ -197,6 +223,7 @@ class Device:
         return int(tid.value)
 
     def table_build_voigt(self, x, line_w, line_g, line_coef, sigma_v, c_light, offset, want_host=True):
+        self._drain_frees()
         x, lw, lg, lc = _f64(x), _f64(line_w), _f64(line_g), _f64(line_coef)
         out = np.empty_like(x) if want_host else None
         tid = C.c_int32(-1)
@@ -222,6 +249,7 @@ class Device:
 
     # ---- molecular ----------------------------------------------------------------------
     def molecular_upload(self, P, T, W, V, offset) -> int:
+        self._drain_frees()
         P, T, W, V = _f64(P), _f64(T), _f64(W), _f64(V)
         assert V.shape == (len(P), len(T), len(W))
         tid = C.c_int32(-1)
@@ -253,6 +281,7 @@ class Device:
 
     # ---- transit ------------------------------------------------------------------------
     def transit_set(self, prob: "TransitInputs"):
+        self._drain_frees()
         self._keep = prob.keepalive
         self._check(self.lib.prom_transit_set(self.h, C.byref(prob.struct)), "prom_transit_set")
         self._shape = (prob.struct.n_orb, prob.struct.n_wav)

@@ -50,6 +50,25 @@ prom::DensityDev to_dev(const prom_density_model& m) {
 
 bool valid_kind(int32_t k) { return k >= PROM_DENSITY_BAROMETRIC && k <= PROM_DENSITY_TABULATED; }
 
+// Table slots: an upload takes the lowest free slot (freed ids are reused), so a loop that builds and
+// drops tables keeps the context's device memory flat.
+template <class T>
+int32_t store_table(std::vector<T>& v, T&& t) {
+  t.live = true;
+  for (size_t i = 0; i < v.size(); ++i)
+    if (!v[i].live) {
+      v[i] = std::move(t);
+      return (int32_t)i;
+    }
+  v.push_back(std::move(t));
+  return (int32_t)v.size() - 1;
+}
+
+template <class T>
+bool table_ok(const std::vector<T>& v, int32_t id) {
+  return id >= 0 && id < (int32_t)v.size() && v[id].live;
+}
+
 }  // namespace
 
 extern "C" {
@@ -161,8 +180,7 @@ int32_t prom_table_upload(prom_ctx* ctx, int64_t n, const double* x, const doubl
     t.ymax = m;
     build_directory(ctx, t, x, n);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
-    ctx->tables.push_back(std::move(t));
-    *table_id = (int32_t)ctx->tables.size() - 1;
+    *table_id = store_table(ctx->tables, std::move(t));
   });
 }
 
@@ -199,8 +217,7 @@ int32_t prom_table_build_voigt(prom_ctx* ctx, int64_t n, const double* x, int32_
       download(log_sigma_out, t.y, n, ctx->stream);
       PROM_HIP(hipStreamSynchronize(ctx->stream));
     }
-    ctx->tables.push_back(std::move(t));
-    *table_id = (int32_t)ctx->tables.size() - 1;
+    *table_id = store_table(ctx->tables, std::move(t));
   });
 }
 
@@ -222,7 +239,7 @@ int32_t prom_voigt_sigma(prom_ctx* ctx, int64_t n, const double* x, int32_t n_li
 int32_t prom_table_lookup(prom_ctx* ctx, int32_t table_id, int64_t n_targets, const double* targets,
                           double* out) {
   return guarded(ctx, [&] {
-    PROM_REQUIRE(table_id >= 0 && table_id < (int32_t)ctx->tables.size(), "prom_table_lookup: unknown table");
+    PROM_REQUIRE(table_ok(ctx->tables, table_id), "prom_table_lookup: unknown table");
     PROM_REQUIRE(n_targets >= 0 && (n_targets == 0 || (targets && out)), "prom_table_lookup: bad arguments");
     const prom::AtomTable& t = ctx->tables[table_id];
     upload(ctx->scratch[0], targets, n_targets, ctx->stream);
@@ -231,6 +248,56 @@ int32_t prom_table_lookup(prom_ctx* ctx, int32_t table_id, int64_t n_targets, co
                               ctx->scratch[0].as<double>(), n_targets, ctx->scratch[1].as<double>());
     download(out, ctx->scratch[1], n_targets, ctx->stream);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+// A freed table's memory goes back to the device; a transit problem that reads it is invalidated.
+static void free_table(prom_ctx* ctx, bool molecular, int32_t id) {
+  for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));   // runs in flight may read it
+  prom::TransitDev& tr = ctx->tr;
+  bool used = !molecular && tr.star && tr.star_table_id == id;
+  for (const auto& t : tr.terms)
+    if ((t.is_molecule != 0) == molecular && t.table == id) used = true;
+  if (used) {
+    drop_graphs(tr);
+    tr.ready = false;
+    tr.ran = false;
+  }
+  if (molecular) ctx->mtables[id] = prom::MolTable{};
+  else ctx->tables[id] = prom::AtomTable{};
+}
+
+int32_t prom_table_free(prom_ctx* ctx, int32_t table_id) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(table_ok(ctx->tables, table_id), "prom_table_free: unknown table");
+    free_table(ctx, false, table_id);
+  });
+}
+
+int32_t prom_molecular_free(prom_ctx* ctx, int32_t table_id) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(table_ok(ctx->mtables, table_id), "prom_molecular_free: unknown table");
+    free_table(ctx, true, table_id);
+  });
+}
+
+int32_t prom_table_count(prom_ctx* ctx, int32_t* n_atomic, int32_t* n_molecular, int64_t* device_bytes) {
+  return guarded(ctx, [&] {
+    int32_t a = 0, m = 0;
+    int64_t b = 0;
+    for (const auto& t : ctx->tables)
+      if (t.live) {
+        ++a;
+        b += (int64_t)(t.x.cap + t.y.cap + t.dir.cap);
+      }
+    for (const auto& t : ctx->mtables)
+      if (t.live) {
+        ++m;
+        b += (int64_t)(t.P.cap + t.T.cap + t.W.cap + t.V.cap);
+      }
+    if (n_atomic) *n_atomic = a;
+    if (n_molecular) *n_molecular = m;
+    if (device_bytes) *device_bytes = b;
   });
 }
 
@@ -255,8 +322,7 @@ int32_t prom_molecular_upload(prom_ctx* ctx, int32_t n_p, const double* P, int32
     for (int64_t i = 0; i < nv; ++i) m = std::max(m, log_sigma[i]);
     t.vmax = m;
     PROM_HIP(hipStreamSynchronize(ctx->stream));
-    ctx->mtables.push_back(std::move(t));
-    *table_id = (int32_t)ctx->mtables.size() - 1;
+    *table_id = store_table(ctx->mtables, std::move(t));
   });
 }
 
@@ -264,7 +330,7 @@ int32_t prom_molecular_sigma(prom_ctx* ctx, int32_t table_id, int64_t n_chords, 
                              const double* P, double T, int64_t n_wav, const double* wavelength,
                              double* sigma_out) {
   return guarded(ctx, [&] {
-    PROM_REQUIRE(table_id >= 0 && table_id < (int32_t)ctx->mtables.size(), "prom_molecular_sigma: unknown table");
+    PROM_REQUIRE(table_ok(ctx->mtables, table_id), "prom_molecular_sigma: unknown table");
     PROM_REQUIRE(n_chords >= 0 && n_x >= 0 && n_wav >= 0, "prom_molecular_sigma: bad sizes");
     const int64_t tot = n_chords * n_x * n_wav;
     upload(ctx->scratch[0], P, n_chords * n_x, ctx->stream);
@@ -377,7 +443,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         t.table = C.table_id;
         t.chi = C.chi;
         if (t.is_molecule) {
-          PROM_REQUIRE(C.table_id >= 0 && C.table_id < (int32_t)ctx->mtables.size(), "transit: unknown molecular table id");
+          PROM_REQUIRE(table_ok(ctx->mtables, C.table_id), "transit: unknown molecular table id");
           t.slot = n_mol++;
           const prom::MolTable& mt = ctx->mtables[C.table_id];
           prom::MolSlotDev md{};
@@ -390,7 +456,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
           md.scenario = sc;
           tr.mslots.push_back(md);
         } else {
-          PROM_REQUIRE(C.table_id >= 0 && C.table_id < (int32_t)ctx->tables.size(), "transit: unknown table id");
+          PROM_REQUIRE(table_ok(ctx->tables, C.table_id), "transit: unknown table id");
           t.slot = n_atoms++;
           const prom::AtomTable& tb = ctx->tables[C.table_id];
           tr.atom_sigma_max.push_back((std::pow(10.0, tb.ymax) - tb.offset) * (1.0 + 1e-9));
@@ -435,9 +501,22 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
           }
           nref[sc] = m;
         } else {
-          nref[sc] = std::fabs(S.density.p[0]);
+          // p[0] bounds the built-in profile only where it decays away from its body: a growing power
+          // law (q < 0), a negative scale height, a hydrostatic J_0 below J(R) or a negative n_0 would
+          // make the normalised columns exceed 1 and the windows' envelopes under-estimate tau
+          const double* p = S.density.p;
+          bool bounded = p[0] >= 0.0 && std::isfinite(p[0]);
+          if (S.density.kind == PROM_DENSITY_BAROMETRIC) bounded = bounded && p[2] > 0.0;
+          if (S.density.kind == PROM_DENSITY_POWERLAW) bounded = bounded && p[2] >= 0.0 && p[1] > 0.0;
+          if (S.density.kind == PROM_DENSITY_HYDROSTATIC)
+            bounded = bounded && p[4] >= 0.0 && p[1] > 0.0 && p[3] != 0.0 &&
+                      p[4] >= p[2] / (p[3] * p[1]) * (1.0 - 1e-12);
+          if (!bounded) tr.window = false;
+          nref[sc] = std::fabs(p[0]) * (1.0 + 1e-9);
         }
       }
+      for (const auto& t : tr.terms)   // negative mixing ratios give negative columns: no envelopes
+        if (!t.is_molecule && !(t.chi >= 0.0)) tr.window = false;
       std::vector<prom::SigTabDev> st;
       for (const auto& t : tr.terms) {
         if (t.is_molecule) continue;
@@ -492,12 +571,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       for (size_t i = 0; i < st.size() && i < 4; ++i) tr.sigtab_v.t[i] = st[i];
     }
     tr.star = pb->has_star != 0;
+    tr.star_table_id = tr.star ? pb->star_table : -1;
     if (tr.star) {
       // stellar spectrum: chord arrays, the F_star table and, per wavelength tile of the tau kernel, the
       // slice of table nodes its targets lambda / s_c can reach: s in [s_min, s_max] and IEEE division
       // is monotone, so fl(lambda / s) lies in [fl(lambda_min / s_max), fl(lambda_max / s_min)]
       PROM_REQUIRE(pb->chord_rho && pb->chord_clv && pb->chord_star_shift, "transit: stellar chord arrays missing");
-      PROM_REQUIRE(pb->star_table >= 0 && pb->star_table < (int32_t)ctx->tables.size(), "transit: unknown star table id");
+      PROM_REQUIRE(table_ok(ctx->tables, pb->star_table), "transit: unknown star table id");
       PROM_REQUIRE(n_mol == 0 && n_atoms <= 8,
                    "transit: the stellar-spectrum path takes <= 8 atomic constituents and no molecules");
       const prom::AtomTable& sb = ctx->tables[pb->star_table];
@@ -569,8 +649,11 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     // work buffers
     const int64_t nc = n_orb * tr.n_pr;
     tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
+    // pipelining needs every per-run buffer in the slot: the generic column path (k_ntot + k_columns:
+    // n_x > 64, > 8 terms or > 4 scenarios) keeps n(c, x) in the shared tr.ntot, so it runs one slot
+    const bool cols8 = n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4;
     const bool fast = tr.exp_mode && n_mol == 0 && n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && tr.window &&
-                      !tr.star;
+                      !tr.star && cols8;
     tr.depth = fast ? ctx->pipeline : 1;
     for (int si = 0; si < tr.depth; ++si) {
     prom::RunSlot& rs = tr.slot[si];

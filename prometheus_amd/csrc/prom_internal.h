@@ -37,6 +37,14 @@ struct DevBuf {
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p; cap = o.cap;
+      o.p = nullptr; o.cap = 0;
+    }
+    return *this;
+  }
   ~DevBuf() { release(); }
   void ensure(size_t bytes) {
     if (bytes <= cap) return;
@@ -139,6 +147,7 @@ struct SigTabs4 {
 };
 
 struct AtomTable {
+  bool live = false;     // slot in use (prom_table_free releases it for reuse)
   DevBuf x, y;
   int64_t n = 0;
   double offset = 0.0;
@@ -152,6 +161,7 @@ struct AtomTable {
 };
 
 struct MolTable {
+  bool live = false;
   DevBuf P, T, W, V;
   int32_t n_p = 0, n_t = 0;
   int64_t n_w = 0;
@@ -239,6 +249,7 @@ struct TransitDev {
   DevBuf mol_na;                            // [n_mol][n_orb][n_pr][n_x] n_abs = n chi
   std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
+  int32_t star_table_id = -1;               // prom_transit_problem.star_table (invalidation on free)
   // stellar spectrum (prom_transit_problem.has_star)
   bool star = false;
   bool star_uniform = false;                // every chord's stellar shift equal (no rotation)

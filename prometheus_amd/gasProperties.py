@@ -23,6 +23,7 @@ from __future__ import annotations
 import math
 import os
 import threading
+import weakref
 from copy import deepcopy
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -53,9 +54,19 @@ def _device(dev=None):
     return _native.get_device(_native.default_device() if dev is None else dev)
 
 
+def _release_tables(ids: Dict[int, int], molecular: bool) -> None:
+    """Finalizer of a table object: its device copies are freed at the context's next upload."""
+    for d, tid in list(ids.items()):
+        dev = _native._contexts.get(d)   # never create a context from a finalizer
+        if dev is not None:
+            dev.release_later(molecular, tid)
+    ids.clear()
+
+
 class LookupTable:
     """Host copy of a log10-sigma table (the reference keeps an interp1d with .x/.y) plus its
-    device-resident copies, one per GPU, uploaded on first use."""
+    device-resident copies, one per GPU, uploaded on first use and freed when the object is
+    collected."""
 
     def __init__(self, x: np.ndarray, y: np.ndarray, offset: float, ids: Optional[Dict[int, int]] = None):
         self.x = x
@@ -63,6 +74,12 @@ class LookupTable:
         self.offset = offset
         self._ids: Dict[int, int] = dict(ids or {})
         self._lock = threading.Lock()
+        weakref.finalize(self, _release_tables, self._ids, False)
+
+    def __deepcopy__(self, memo):
+        # a copy owns no device ids (it uploads its own on first use); sharing them would leave it
+        # reading a table freed when this object is collected
+        return LookupTable(deepcopy(self.x, memo), deepcopy(self.y, memo), self.offset)
 
     def table_id(self, dev: "_native.Device") -> int:
         with self._lock:
@@ -78,8 +95,11 @@ def n_interp_log(x_targets, x_grid, y_grid_log, offset):
     dev = _device()
     with dev.lock:
         tid = dev.table_upload(x_grid, y_grid_log, offset)
-        t = np.asarray(x_targets, dtype=np.float64)
-        return dev.table_lookup(tid, t.ravel()).reshape(t.shape)
+        try:
+            t = np.asarray(x_targets, dtype=np.float64)
+            return dev.table_lookup(tid, t.ravel()).reshape(t.shape)
+        finally:
+            dev.table_free(tid)
 
 
 # ============================================================================== density scenarios
@@ -357,6 +377,10 @@ class MolecularTable:
         self.grid = (P, T, W)
         self._ids: Dict[int, int] = {}
         self._lock = threading.Lock()
+        weakref.finalize(self, _release_tables, self._ids, True)
+
+    def __deepcopy__(self, memo):
+        return MolecularTable(*(deepcopy(a, memo) for a in (self.P, self.T, self.W, self.V)), self.offset)
 
     def table_id(self, dev) -> int:
         with self._lock:
@@ -616,7 +640,7 @@ class Transit:
         orb = self.spatialGrid.constructOrbphaseAxis()
         if shifts is None:
             shifts = lc.planet_shifts(self.planet, orb)
-        bounds = lc.band_bounds(shifts, line_centers or (lc.NA_D2, lc.NA_D1),
+        bounds = lc.band_bounds(shifts, (lc.NA_D2, lc.NA_D1) if line_centers is None else line_centers,
                                 lc.BANDWIDTH if bandwidth is None else bandwidth)
         R, acc = self._integrate(max_memory_gb, devices, cull_tau, options, bounds, want_R=return_spectrum)
         return (acc.lightcurve(), R) if return_spectrum else acc.lightcurve()

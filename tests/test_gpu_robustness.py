@@ -1,0 +1,166 @@
+"""GPU robustness: paths the golden-vector tests do not reach -- table lifetime, pipelined runs of every
+column path, phases with more active chords than the sorted-window limit, the multi-chunk memory
+budget and density profiles whose n_0 does not bound them.  Each result is checked against the CPU
+oracle (tolerance 1e-10 relative, the north star) or bitwise against the product's own reference run.
+"""
+import gc
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import prom_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+R_TOL = 1e-10
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.abs(a - b) / np.maximum(np.abs(b), 1e-300)
+    r[(a == b)] = 0.0
+    return float(np.max(r)) if r.size else 0.0
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from prometheus_amd import _native
+    return _native.get_device(0)
+
+
+def _oracle_R(cfg, wav):
+    scen, dop, grids = O.from_setup(cfg)
+    return O.transit_depth(scen, dop, grids, wav, O.build_tables(scen, grids))
+
+
+def test_table_free_keeps_memory_flat(dev):
+    """Building and dropping lookup tables (a retrieval loop rebuilding its atmosphere, n_interp_log
+    per call) leaves the context's table count and device bytes flat: ids are freed and reused."""
+    from prometheus_amd import gasProperties as gp
+    x = np.linspace(5.8e-5, 5.9e-5, 20000)
+    y = -20. + np.sin(x * 1e7)
+    gc.collect()
+    with dev.lock:
+        dev._drain_frees()
+        base = dev.table_count()
+    for i in range(30):
+        t = gp.LookupTable(x, y + i, 1e-50)
+        with dev.lock:
+            tid = t.table_id(dev)
+            assert dev.table_lookup(tid, x[:5]).shape == (5,)
+        del t
+        gc.collect()
+        out = gp.n_interp_log(x[:7], x, y, 1e-50)
+        assert rel(out, 10 ** np.interp(x[:7], x, y) - 1e-50) < 1e-13
+    with dev.lock:
+        dev._drain_frees()
+        after = dev.table_count()
+    assert after[0] <= base[0] + 1 and after[2] <= base[2] + 3 * 8 * 20000 + 8 * (4 * 20000 + 1)
+
+
+def test_freed_table_invalidates_problem(dev):
+    """A transit problem that reads a freed table cannot run (PROM_E_STATE), instead of reading freed
+    device memory; setting it again works."""
+    from prometheus_amd import _native
+    d = np.load(os.path.join(G, "transit_C1.npz"))
+    from prometheus_amd import setupfile
+    tr = setupfile.build_transit(json.loads(str(d["config"])))
+    host = tr._host_inputs()
+    with dev.lock:
+        dev.transit_set(tr._problem(dev, host, 0, len(tr.wavelength), 0.0))
+        dev.transit_run()
+        con = tr.atmosphere.densityDistributionList[0].constituents[0]
+        tid = con.lookupFunction.table_id(dev)
+        dev.table_free(tid)
+        con.lookupFunction._ids.pop(dev.device)
+        with pytest.raises(_native.NativeError, match="STATE|prom_transit_set"):
+            dev.transit_run()
+    R = tr.sumOverChords(devices=[0])   # re-uploads the table and sets the problem again
+    assert rel(R, d["R"]) < R_TOL
+
+
+@pytest.mark.parametrize("x_steps", [30, 80])
+def test_pipelined_runs_bitwise(dev, x_steps):
+    """Eight back-to-back runs without synchronisation (the pipelined fast path rotates slots and
+    streams; the generic column path of n_x > 64 runs on one slot): the last run's R is bitwise the
+    R of a single synchronised run."""
+    from prometheus_amd import configs, setupfile
+    cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
+                          res_low=5e-9, res_high=1e-10)
+    cfg["Grids"]["x_steps"] = x_steps
+    tr = setupfile.build_transit(cfg)
+    R1 = tr.sumOverChords(devices=[0])
+    host = tr._host_inputs()
+    with dev.lock:
+        dev.transit_set(tr._problem(dev, host, 0, len(tr.wavelength), 0.0))
+        for _ in range(8):
+            dev.transit_run()
+        R8 = dev.transit_result()
+    assert np.array_equal(R1, R8)
+    assert rel(R1, _oracle_R(cfg, tr.wavelength)) < R_TOL
+
+
+def test_more_active_chords_than_window_limit(dev):
+    """100 x 50 = 5,000 chords per phase, nearly all active (power law q = 6): more than the sorted
+    window limit (4,096), so the phases take the unsorted compaction and the heavy tau units; checked
+    against the oracle."""
+    from prometheus_amd import configs, setupfile
+    cfg = configs.reduced(configs.get("C3"), phi_steps=100, rho_steps=50, orbphase_steps=2,
+                          lower_w=5886e-8, upper_w=5900e-8, res_low=2e-9, res_high=2e-10)
+    cfg["Scenarios"]["powerLaw"]["P_0"] = 1e-1
+    tr = setupfile.build_transit(cfg)
+    R = tr.sumOverChords(devices=[0])
+    st = tr.last_stats[-1]
+    print("active %d of %d chord-phases, records %d" % (st["active_chords"], 2 * 5000, st["tau_records"]))
+    assert st["active_chords"] > 2 * 4096
+    assert st["tau_records"] == st["active_chords"]   # unsorted phases: no merging
+    assert rel(R, _oracle_R(cfg, tr.wavelength)) < R_TOL
+
+
+def test_multi_chunk_memory_budget(dev):
+    """A tiny max_memory_gb processes each shard in several 4,096-wavelength chunks (the analogue of
+    memoryHandler.py:55-66's batching): R and the band light curve are bitwise the one-chunk results."""
+    from prometheus_amd import setupfile
+    d = np.load(os.path.join(G, "transit_C2r.npz"))
+    tr = setupfile.build_transit(json.loads(str(d["config"])))
+    R1 = tr.sumOverChords(devices=[0])
+    n1 = len(tr.last_stats)
+    Rc = tr.sumOverChords(devices=[0], max_memory_gb=1e-9)
+    nc = len(tr.last_stats)
+    assert n1 == 1 and nc >= 2 and nc == -(-len(tr.wavelength) // 4096)
+    assert np.array_equal(R1, Rc)
+    lc1 = tr.bandLightcurve(devices=[0])
+    lcc = tr.bandLightcurve(devices=[0], max_memory_gb=1e-9)
+    assert rel(lcc, lc1) < 1e-14
+    assert rel(Rc, d["R"]) < R_TOL
+
+
+@pytest.mark.parametrize("q", [-0.5, 1.5])
+def test_unbounded_density_profile_disables_windows(dev, q):
+    """A power law growing outwards (q < 0) is not bounded by n_0: windows are switched off (variant
+    1x) and R still matches the oracle; q >= 0 keeps them (variant 2x/3x)."""
+    from prometheus_amd import configs, setupfile
+    cfg = configs.reduced(configs.get("C3"), orbphase_steps=2, lower_w=5886e-8, upper_w=5900e-8,
+                          res_low=5e-9, res_high=5e-10)
+    cfg["Scenarios"]["powerLaw"]["q_esc"] = q
+    cfg["Scenarios"]["powerLaw"]["P_0"] = 1e-6
+    tr = setupfile.build_transit(cfg)
+    R = tr.sumOverChords(devices=[0])
+    st = tr.last_stats[-1]
+    print("q", q, "variant", st["tau_kernel_variant"])
+    assert (st["tau_kernel_variant"] // 10 == 1) == (q < 0)
+    assert rel(R, _oracle_R(cfg, tr.wavelength)) < R_TOL
+
+
+def test_band_lightcurve_array_centres(dev):
+    """bandLightcurve accepts a numpy array of line centres (no truth-value ambiguity)."""
+    from prometheus_amd import setupfile, lightcurve as lc
+    d = np.load(os.path.join(G, "transit_C2r.npz"))
+    tr = setupfile.build_transit(json.loads(str(d["config"])))
+    a = tr.bandLightcurve(devices=[0])
+    b = tr.bandLightcurve(line_centers=np.array([lc.NA_D2, lc.NA_D1]), devices=[0])
+    assert np.array_equal(a, b)
