@@ -7,13 +7,15 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = ["csrc/prom_api.hip", "csrc/prom_kernels.hip"]
-HEADERS = ["csrc/prom_internal.h", "csrc/faddeeva.h", "csrc/exp2_table.h", "csrc/exp2_table_body.h",
-           "../include/prom_hip.h"]
+SOURCES = ["csrc/prom_api.hip", "csrc/prom_transit.hip", "csrc/prom_fn.hip", "csrc/prom_mol.hip",
+           "csrc/prom_rm.hip"]
+HEADERS = ["csrc/prom_internal.h", "csrc/prom_device.h", "csrc/faddeeva.h", "csrc/exp2_table.h",
+           "csrc/exp2_table_body.h", "../include/prom_hip.h"]
 OUT = os.path.join(HERE, "libprom_hip.so")
 ARCH = os.environ.get("PROM_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "--offload-arch=" + ARCH, "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=" + ARCH, "-ffp-contract=off", "-fPIC", "-Wall",
          "-Wno-unused-function"]
+OBJDIR = os.path.join(HERE, "build")
 
 
 def hipcc() -> str:
@@ -30,10 +32,25 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(os.path.join(HERE, f)) <= t for f in SOURCES + HEADERS + ["build.py"])
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, extra=()) -> str:
+    """One object per translation unit, compiled in parallel, then linked into the shared library."""
+    if not force and up_to_date() and not extra:
         return OUT
-    cmd = [hipcc()] + FLAGS + ["-o", OUT + ".tmp"] + [os.path.join(HERE, s) for s in SOURCES]
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(OBJDIR, exist_ok=True)
+    cc = hipcc()
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+        cmd = [cc] + FLAGS + list(extra) + ["-c", os.path.join(HERE, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True, cwd=HERE)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True, cwd=HERE)

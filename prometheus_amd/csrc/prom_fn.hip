@@ -1,0 +1,193 @@
+// Function-level kernels: n_interp_log / getSigmaAbs (gasProperties.py:34-51, :727-735), the Voigt
+// tables (:672-715), density plugins (:143-516), the molecular lookup (:789-818), reductions and the
+// light-curve band statistics (mainRetrieval.py:76-93).
+#include "prom_device.h"
+
+namespace prom {
+
+// ------------------------------------------------------------------ function-level kernels
+__global__ void k_table_lookup(const double* __restrict__ xp, const double* __restrict__ fp, int64_t n,
+                               double offset, const double* __restrict__ t, int64_t nt,
+                               double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nt;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    out[i] = pow(10.0, np_interp(t[i], xp, fp, n)) - offset;
+  }
+}
+
+void launch_table_lookup(hipStream_t s, const double* x, const double* y, int64_t n, double offset,
+                         const double* targets, int64_t nt, double* out) {
+  if (nt == 0) return;
+  hipLaunchKernelGGL(k_table_lookup, dim3(grid_for(nt)), dim3(kBlock), 0, s, x, y, n, offset, targets,
+                     nt, out);
+  PROM_HIP(hipGetLastError());
+}
+
+__global__ void k_voigt(const double* __restrict__ x, int64_t n, const double* __restrict__ lw,
+                        const double* __restrict__ lg, const double* __restrict__ lc, int32_t nl,
+                        double sigma_v, double c_light, double offset, int log_table,
+                        double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double cx = c_light / x[i];
+    double s = 0.0;
+    for (int32_t l = 0; l < nl; ++l) {
+      const double lam0 = lw[l];
+      const double prof = voigt_profile(cx - c_light / lam0, sigma_v / lam0, lg[l]);
+      s += lc[l] * prof;
+    }
+    out[i] = log_table ? log10(s + offset) : s;
+  }
+}
+
+void launch_voigt(hipStream_t s, const double* x, int64_t n, const double* lw, const double* lg,
+                  const double* lc, int32_t nl, double sigma_v, double c_light, double offset,
+                  int log_table, double* out) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_voigt, dim3(grid_for(n, 128)), dim3(128), 0, s, x, n, lw, lg, lc, nl, sigma_v,
+                     c_light, offset, log_table, out);
+  PROM_HIP(hipGetLastError());
+}
+
+__global__ void k_density(DensityDev m, const double* __restrict__ x, int32_t n_x,
+                          const double* __restrict__ y, const double* __restrict__ z,
+                          const double* __restrict__ bx, const double* __restrict__ by, int64_t n_chords,
+                          double* __restrict__ out) {
+  const int64_t tot = n_chords * n_x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i / n_x;
+    const int32_t ix = (int32_t)(i - c * n_x);
+    out[i] = density_at(m, x[ix], y[c], z[c], bx[c], by[c]);
+  }
+}
+
+void launch_density(hipStream_t s, const DensityDev& m, const double* x, int32_t n_x, const double* y,
+                    const double* z, const double* bx, const double* by, int64_t n_chords,
+                    double* out) {
+  if (n_chords * n_x == 0) return;
+  hipLaunchKernelGGL(k_density, dim3(grid_for(n_chords * n_x)), dim3(kBlock), 0, s, m, x, n_x, y, z, bx,
+                     by, n_chords, out);
+  PROM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ molecular lookup (rgi_bracket, mol_value: prom_device.h)
+__global__ void k_mol_sigma(const double* __restrict__ Pg, int32_t n_p, const double* __restrict__ Tg,
+                            int32_t n_t, const double* __restrict__ Wg, int64_t n_w,
+                            const double* __restrict__ V, double offset, int64_t n_chords, int32_t n_x,
+                            const double* __restrict__ P, double T, int64_t n_wav,
+                            const double* __restrict__ wav, double* __restrict__ out) {
+  const int64_t tot = n_chords * n_x * n_wav;
+  const double fill = log10(offset);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = i % n_wav;
+    const int64_t cx = i / n_wav;
+    const int64_t c = cx / n_x;
+    double p = P[cx];
+    p = p < 1e-4 ? 1e-4 : p;
+    int64_t ip, it, iw;
+    double tp, tt, tw;
+    double v = fill;
+    if (rgi_bracket(Pg, n_p, p, &ip, &tp) && rgi_bracket(Tg, n_t, T, &it, &tt) &&
+        rgi_bracket(Wg, n_w, wav[c * n_wav + w], &iw, &tw))
+      v = mol_value(V, n_t, n_w, ip, tp, it, tt, iw, tw);
+    out[i] = pow(10.0, v) - offset;
+  }
+}
+
+void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, int32_t n_x,
+                            const double* P, double T, int64_t n_wav, const double* wav, double* out) {
+  const int64_t tot = n_chords * n_x * n_wav;
+  if (tot == 0) return;
+  hipLaunchKernelGGL(k_mol_sigma, dim3(grid_for(tot)), dim3(kBlock), 0, s, t.P.as<double>(), t.n_p,
+                     t.T.as<double>(), t.n_t, t.W.as<double>(), t.n_w, t.V.as<double>(), t.offset,
+                     n_chords, n_x, P, T, n_wav, wav, out);
+  PROM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ reductions
+__global__ void k_max(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
+  __shared__ double sm[kBlock];
+  double m = -INFINITY;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double a = v[i];
+    m = (a > m || a != a) ? a : m;
+  }
+  sm[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = kBlock / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      const double a = sm[threadIdx.x + s];
+      if (a > sm[threadIdx.x] || a != a) sm[threadIdx.x] = a;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
+}
+
+// max (NaN-propagating) of a device array; scratch_dev must hold 1024 doubles
+double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev) {
+  const unsigned g = grid_for(n, kBlock, 1024);
+  hipLaunchKernelGGL(k_max, dim3(g), dim3(kBlock), 0, s, v, n, scratch_dev);
+  PROM_HIP(hipGetLastError());
+  std::vector<double> h(g);
+  PROM_HIP(hipMemcpyAsync(h.data(), scratch_dev, sizeof(double) * g, hipMemcpyDeviceToHost, s));
+  PROM_HIP(hipStreamSynchronize(s));
+  double m = -INFINITY;
+  for (double a : h) m = (a > m || a != a) ? a : m;
+  return m;
+}
+
+
+// ---- light-curve band statistics (mainRetrieval.py:76-93) -------------------------------------------
+// One workgroup per phase: strided partial sums / counts / maxima, then a fixed-order LDS tree, so the
+// result does not depend on scheduling.  The max propagates NaN (numpy.max).
+__global__ void __launch_bounds__(kBlock) k_band_stats(const double* __restrict__ R, const double* __restrict__ wav,
+                                                       int64_t n_wav, int32_t n_bands,
+                                                       const double* __restrict__ bounds, double* __restrict__ sum,
+                                                       int64_t* __restrict__ count, double* __restrict__ mx) {
+  __shared__ double ss[kBlock], sm[kBlock];
+  __shared__ int64_t sc[kBlock];
+  const int32_t o = blockIdx.x;
+  const double* b = bounds + (int64_t)o * n_bands * 2;
+  const double* r = R + (int64_t)o * n_wav;
+  double acc = 0.0, m = -__builtin_inf();
+  int64_t cnt = 0;
+  for (int64_t w = threadIdx.x; w < n_wav; w += kBlock) {
+    const double v = r[w], l = wav[w];
+    m = (v > m || v != v || m != m) ? (m != m ? m : v) : m;
+    bool sel = false;
+    for (int32_t k = 0; k < n_bands; ++k) sel = sel || (l >= b[2 * k] && l <= b[2 * k + 1]);
+    if (sel) {
+      acc += v;
+      ++cnt;
+    }
+  }
+  ss[threadIdx.x] = acc;
+  sm[threadIdx.x] = m;
+  sc[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int h = kBlock / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      ss[threadIdx.x] += ss[threadIdx.x + h];
+      sc[threadIdx.x] += sc[threadIdx.x + h];
+      const double a = sm[threadIdx.x], c = sm[threadIdx.x + h];
+      sm[threadIdx.x] = (a != a || c != c) ? __builtin_nan("") : (c > a ? c : a);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sum[o] = ss[0];
+    count[o] = sc[0];
+    mx[o] = sm[0];
+  }
+}
+
+void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,
+                       int32_t n_bands, const double* bounds, double* sum, int64_t* count, double* mx) {
+  hipLaunchKernelGGL(k_band_stats, dim3(n_orb), dim3(kBlock), 0, s, R, wav, n_wav, n_bands, bounds, sum, count, mx);
+  PROM_HIP(hipGetLastError());
+}
+
+}  // namespace prom

@@ -303,6 +303,9 @@ void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, 
 // tau pair (the fast path carries them on the tau kernel's dispatch packet)
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events);
+// the fused tau kernels of the molecular and stellar-spectrum paths (prom_mol.hip, prom_rm.hip)
+void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
+void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
 // per phase: sum / count of R over the band-selected wavelengths, max of R over all (prom_transit_band_stats)
 void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,

@@ -1,0 +1,170 @@
+// Molecular fused tau kernel (gasProperties.py:924-954 with MolecularConstituent.getSigmaAbs :789-818).
+#include "prom_device.h"
+
+namespace prom {
+
+// ---- molecular fused kernel -------------------------------------------------------------------
+// tau(c, w) = sum_atomic N_s sigma_s(w) + sum_mol dx * sum_x n_abs(c,x) sigma_m(P(c,x), T, lambda'_w)
+// (gasProperties.py:924-954).  Per thread (phase o, wavelength w) and molecular slot, the (T, lambda)
+// part of the trilinear RegularGridInterpolator weights is fixed: u_i = sum_{T,lambda corners} w V[i][.][.]
+// is formed once for every P node i into LDS; each (chord, sample) then costs one P interpolation
+// (uniform bracket from k_mol_prep), 10^v and an FMA.  Out-of-table samples (P, T or lambda) take the
+// fill value, i.e. sigma = 0, as in the reference.
+constexpr double kLog2Ten2048 = 0x1.a934f0979a371p+12;   // 2048 log2(10)
+
+template <int NSA, int EXPK>
+__global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const SigTabDev* __restrict__ tabs,
+                                                    const MolSlotDev* __restrict__ ms, int32_t n_mol,
+                                                    int32_t max_np, const double* __restrict__ wav,
+                                                    const double* __restrict__ recs,
+                                                    const int32_t* __restrict__ act_ip,
+                                                    const double* __restrict__ fout,
+                                                    const int32_t* __restrict__ counts,
+                                                    const double* __restrict__ tfrac,
+                                                    const double* __restrict__ fsum, int32_t n_pr,
+                                                    int32_t n_orb, int32_t phases_per_group, int64_t n_wav,
+                                                    int32_t n_x, double delta_x,
+                                                    const int32_t* __restrict__ mip,
+                                                    const double* __restrict__ mwp,
+                                                    const double* __restrict__ mna, double* __restrict__ R) {
+  extern __shared__ double lds[];   // [2048] exp table | [n_mol][max_np][kBlock] u
+  double* etab = lds;
+  double* ul = lds + PROM_EXP2_TABLE_N;
+  if (EXPK) fill_exp_table(etab);
+  __syncthreads();
+  const int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  const bool live = w < n_wav;
+  const double lam = wav[live ? w : n_wav - 1];
+  const int32_t o0 = blockIdx.y * phases_per_group;
+  const int32_t o1 = min(n_orb, o0 + phases_per_group);
+  constexpr int ST = 1 + NSA;
+  constexpr int NR = NSA > 0 ? NSA : 1;
+  double sg[NR], shv[NR];
+#pragma unroll
+  for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); sg[s] = 0.0; }
+  int64_t whint[4] = {-1, -1, -1, -1};
+  const int64_t nc = (int64_t)n_orb * n_pr;
+  for (int32_t o = o0; o < o1; ++o) {
+    const bool exact = !EXPK || counts[o * kCnt + 3] != 0;
+    const int32_t n_act = counts[o * kCnt + 0];
+    const double* __restrict__ rec = recs + (int64_t)o * n_pr * ST;
+#pragma unroll
+    for (int s = 0; s < NSA; ++s) {
+      const double sh = tabv.t[s].shift[o];
+      if (!(sh == shv[s])) {
+        sg[s] = sigma_of(sh * lam, tabv.t[s]);
+        shv[s] = sh;
+      }
+    }
+    uint32_t inb = 0;   // bit m: molecular slot m has (T, lambda') inside its table
+    for (int32_t m = 0; m < n_mol; ++m) {
+      const MolSlotDev d = ms[m];
+      int64_t it, iw;
+      double tt, tw;
+      const double lw = d.shift[o] * lam;
+      bool ok = rgi_bracket(d.T, d.n_t, d.temp, &it, &tt);
+      if (ok) {
+        // gallop the wavelength bracket from the previous phase's
+        ok = lw >= d.W[0] && lw <= d.W[d.n_w - 1];
+        if (ok) {
+          int64_t h = m < 4 ? whint[m] : -1;
+          int64_t lo = 0, hi = d.n_w - 1;
+          if (h >= 0 && h <= d.n_w - 2 && d.W[h] < lw && lw <= d.W[h + 1]) { lo = h; hi = h + 1; }
+          // scipy: i = searchsorted(g, v, 'left') - 1 clipped to [0, n-2]
+          while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (d.W[mid] < lw) lo = mid; else hi = mid;
+          }
+          iw = lo;
+          if (lw <= d.W[0]) iw = 0;
+          tw = (lw - d.W[iw]) / (d.W[iw + 1] - d.W[iw]);
+          if (m < 4) whint[m] = iw;
+        }
+      }
+      if (ok) {
+        inb |= 1u << m;
+        const double w00 = (1.0 - tt) * (1.0 - tw), w01 = (1.0 - tt) * tw;
+        const double w10 = tt * (1.0 - tw), w11 = tt * tw;
+        for (int32_t i = 0; i < d.n_p; ++i) {
+          const double* v0 = d.V + ((int64_t)i * d.n_t + it) * d.n_w + iw;
+          const double* v1 = v0 + d.n_w;
+          double u = 0.0;
+          u = u + v0[0] * w00;
+          u = u + v0[1] * w01;
+          u = u + v1[0] * w10;
+          u = u + v1[1] * w11;
+          ul[((int64_t)m * max_np + i) * kBlock + threadIdx.x] = u;
+        }
+      }
+    }
+    const int32_t* ipl = act_ip + (int64_t)o * n_pr;
+    double acc = 0.0;
+    const double scale = exact ? 1.0 : kMinus2048OverLn2;
+    int32_t ip_next = n_act > 0 ? ipl[0] : 0;
+    for (int32_t ci = 0; ci < n_act; ++ci) {
+      const double* r = rec + (int64_t)ci * ST;
+      const int32_t ip = ip_next;
+      if (ci + 1 < n_act) ip_next = ipl[ci + 1];   // the next chord's index is in flight meanwhile
+      double tau = 0.0;
+#pragma unroll
+      for (int s = 0; s < NSA; ++s) tau = tau + r[1 + s] * sg[s];
+      for (int32_t m = 0; m < n_mol; ++m) {
+        if (!((inb >> m) & 1u)) continue;
+        const MolSlotDev d = ms[m];
+        const int64_t base = ((int64_t)m * nc + (int64_t)o * n_pr + ip) * n_x;
+        const double* um = ul + (int64_t)m * max_np * kBlock + threadIdx.x;
+        double sm = 0.0;
+        // (uniform per wavefront: scalar loads, batched by the unroll)
+#pragma unroll 10
+        for (int32_t ix = 0; ix < n_x; ++ix) {
+          const int32_t pi = mip[base + ix];
+          if (pi < 0) continue;
+          const double tp = mwp[base + ix];
+          const double v = (1.0 - tp) * um[(int64_t)pi * kBlock] + tp * um[(int64_t)(pi + 1) * kBlock];
+          // 10^v: the LDS-table 2^(y/2048) with y = v 2048 log2(10) in table mode (relative error
+          // ~ |v| 2.3 2^-53 from the argument product, ~1e-14 at the table's floor), ocml otherwise
+          const double p10 = (EXPK && !exact) ? acc_exp2k(0.0, 1.0, v * kLog2Ten2048, etab) : exp10(v);
+          sm = __builtin_fma(mna[base + ix], p10 - d.offset, sm);
+        }
+        tau = tau + sm * delta_x;
+      }
+      if (!exact) acc = acc_exp2k(acc, r[0], tau * scale, etab);
+      else acc = acc + fout[ip] * exp(-tau);
+    }
+    if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
+  }
+}
+
+void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg) {
+  const SigTabDev* tabs = tr.sigtab.as<SigTabDev>();
+  const double* wav = tr.wav.as<double>();
+  const double* recs = rs.recs.as<double>();
+  const int32_t* aip = rs.act_ip.as<int32_t>();
+  const double* fo = tr.cfout.as<double>();
+  const int32_t* counts = rs.counts.as<int32_t>();
+  const double* tf = rs.tsum.as<double>();
+  const double* fs = rs.fsum.as<double>();
+  double* R = rs.R.as<double>();
+    PROM_REQUIRE(na <= 4, "transit: at most 4 atomic constituents next to molecular ones");
+    int32_t max_np = 0;
+    for (const auto& m : tr.mslots) max_np = std::max(max_np, m.n_p);
+    const size_t lds = PROM_EXP2_TABLE_N * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
+    PROM_REQUIRE(lds <= 160 * 1024, "transit: molecular tables too large for the LDS staging (n_mol * n_p)");
+#define PROM_TAUM(NSV, EK)                                                                                  \
+  hipLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
+                     max_np, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x,         \
+                     tr.delta_x, tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(), R)
+#define PROM_TAUM_NS(EK)                \
+  switch (na) {                         \
+    case 0: PROM_TAUM(0, EK); break;    \
+    case 1: PROM_TAUM(1, EK); break;    \
+    case 2: PROM_TAUM(2, EK); break;    \
+    case 3: PROM_TAUM(3, EK); break;    \
+    default: PROM_TAUM(4, EK);          \
+  }
+    if (tr.exp_mode) { PROM_TAUM_NS(1) } else { PROM_TAUM_NS(0) }
+#undef PROM_TAUM_NS
+#undef PROM_TAUM
+}
+
+}  // namespace prom

@@ -16,429 +16,9 @@
 //                 order, merging of chords with equal (2^-40) column densities
 //     k_tau<NS>   per (phase, wavelength): sigma_s = 10^interp(shift_o * lambda_w) - offset for each
 //                 species, then tau over the active chords, exp(-tau), disk sum, ratio
-#include <hip/hip_ext.h>
-
-#include "exp2_table.h"
-#include "faddeeva.h"
-#include "prom_internal.h"
+#include "prom_device.h"
 
 namespace prom {
-
-constexpr int kBlock = 256;
-constexpr int kTW = 128;   // k_tau_w: wavelengths per workgroup (one window tile)
-constexpr int kTP = 4;     // k_tau_w: phases per workgroup (one per wavefront)
-constexpr int kHeavy = 8;  // k_tau_p: windows longer than this go to the heavy wavefronts
-
-// Optional in-kernel timing (build with -DPROM_TRACE, tools/trace_kernels.py): wall-clock stamps
-// (100 MHz) of workgroup 0's steps and per-wavefront cycle counters in a device array.
-#ifdef PROM_TRACE
-__device__ unsigned long long g_trace[1 << 20];
-#define PROM_TS(slot)                                                   \
-  do {                                                                  \
-    __syncthreads();                                                    \
-    if (threadIdx.x == 0) g_trace[(slot)] = wall_clock64();             \
-  } while (0)
-#define PROM_ACC(slot, v)                                               \
-  do {                                                                  \
-    if ((threadIdx.x & 63) == 0) g_trace[(slot)] += (unsigned long long)(v); \
-  } while (0)
-#else
-#define PROM_TS(slot) do {} while (0)
-#define PROM_ACC(slot, v) do {} while (0)
-#endif
-#ifdef PROM_TRACE
-#define PROM_CLK(var) const long long var = clock64()
-#else
-#define PROM_CLK(var) do {} while (0)
-#endif
-
-__constant__ double kExp2TableDev[PROM_EXP2_TABLE_N] = {
-#define PROM_EXP2_TABLE_BODY
-#include "exp2_table_body.h"
-};
-
-static inline unsigned grid_for(int64_t n, int block = kBlock, int64_t cap = 1 << 20) {
-  int64_t g = (n + block - 1) / block;
-  if (g < 1) g = 1;
-  if (g > cap) g = cap;
-  return (unsigned)g;
-}
-
-// numpy.interp (numpy/_core/src/multiarray/compiled_base.c arr_interp) for one target.
-__device__ __forceinline__ double np_interp(double t, const double* __restrict__ xp,
-                                            const double* __restrict__ fp, int64_t n) {
-  if (t != t) return t;
-  if (n == 1) return (t < xp[0]) ? fp[0] : fp[0];
-  if (t < xp[0]) return fp[0];
-  if (t > xp[n - 1]) return fp[n - 1];
-  if (t == xp[n - 1]) return fp[n - 1];
-  int64_t lo = 0, hi = n - 1;  // xp[lo] <= t < xp[hi]
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (xp[mid] <= t) lo = mid; else hi = mid;
-  }
-  if (xp[lo] == t) return fp[lo];
-  const double slope = (fp[lo + 1] - fp[lo]) / (xp[lo + 1] - xp[lo]);
-  double r = slope * (t - xp[lo]) + fp[lo];
-  if (r != r) {
-    r = slope * (t - xp[lo + 1]) + fp[lo + 1];
-    if (r != r && fp[lo] == fp[lo + 1]) r = fp[lo];
-  }
-  return r;
-}
-
-// np_interp for one table of a transit problem, then 10^v - offset.  The bracket (numpy's: the largest
-// j <= n-2 with xp[j] <= t) comes from the bucket directory: dir[j] - 1 is the last node at or before
-// the bucket's start, and a window of 4 nodes (x and f fetched together) holds the bracket unless the
-// bucket is crowded or rounding moved j, in which case a gallop + bisection finds it.
-__device__ __forceinline__ double sigma_of(double t, const SigTabDev& tb) {
-  const double* __restrict__ xp = tb.x;
-  const double* __restrict__ fp = tb.y;
-  const int64_t n = tb.n;
-  double v;
-  if (t != t) v = t;
-  else if (n == 1 || !(t >= xp[0])) v = fp[0];
-  else if (t >= xp[n - 1]) v = fp[n - 1];
-  else {
-    const double fj = (t - tb.dir_x0) * tb.dir_inv_h;
-    const int32_t j = fj < 0.0 ? 0 : (fj >= (double)(tb.n_dir - 1) ? tb.n_dir - 1 : (int32_t)fj);
-    int64_t lo = tb.dir[j] - 1;
-    lo = lo < 0 ? 0 : (lo > n - 2 ? n - 2 : lo);
-    const int64_t l1 = lo + 1, l2 = lo + 2 < n ? lo + 2 : n - 1, l3 = lo + 3 < n ? lo + 3 : n - 1;
-    const double x0 = xp[lo], x1 = xp[l1], x2 = xp[l2], x3 = xp[l3];
-    const double f0 = fp[lo], f1 = fp[l1], f2 = fp[l2], f3 = fp[l3];
-    double xa, xb, fa, fb;
-    int64_t k = -1;
-    if (x0 <= t) {
-      if (t < x1) { k = lo; xa = x0; xb = x1; fa = f0; fb = f1; }
-      else if (t < x2) { k = l1; xa = x1; xb = x2; fa = f1; fb = f2; }
-      else if (t < x3) { k = l2; xa = x2; xb = x3; fa = f2; fb = f3; }
-    }
-    if (k < 0) {
-      int64_t a = lo, b = l3;   // invariant after the gallop: xp[a] <= t < xp[b]
-      for (int64_t st = 1; a > 0 && xp[a] > t; st <<= 1) { b = a; a = a - st > 0 ? a - st : 0; }
-      for (int64_t st = 1; b < n - 1 && xp[b] <= t; st <<= 1) { a = b; b = b + st < n - 1 ? b + st : n - 1; }
-      while (b - a > 1) {
-        const int64_t mid = (a + b) >> 1;
-        if (xp[mid] <= t) a = mid; else b = mid;
-      }
-      k = a;
-      xa = xp[a]; xb = xp[a + 1]; fa = fp[a]; fb = fp[a + 1];
-    }
-    if (xa == t) v = fa;
-    else {
-      const double slope = (fb - fa) / (xb - xa);
-      v = slope * (t - xa) + fa;
-      if (v != v) {
-        v = slope * (t - xb) + fb;
-        if (v != v && fa == fb) v = fa;
-      }
-    }
-  }
-  return exp10(v) - tb.offset;
-}
-
-// ---- wavefront scans on DPP row shifts + cross-row readlanes (no LDS traffic, no bpermute) ----
-template <int CTRL>
-__device__ __forceinline__ double dpp_mov(double v) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
-  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-template <int CTRL>
-__device__ __forceinline__ int32_t dpp_mov(int32_t v) {
-  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
-}
-__device__ __forceinline__ double lane_read(double v, int l) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ int32_t lane_read(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
-
-// inclusive prefix over lanes 0..63 (op applied as op(earlier, later))
-template <typename T, typename Op>
-__device__ __forceinline__ T wave_prefix(T v, Op op) {
-  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
-  T t = dpp_mov<0x111>(v);
-  if (rl >= 1) v = op(t, v);
-  t = dpp_mov<0x112>(v);
-  if (rl >= 2) v = op(t, v);
-  t = dpp_mov<0x114>(v);
-  if (rl >= 4) v = op(t, v);
-  t = dpp_mov<0x118>(v);
-  if (rl >= 8) v = op(t, v);
-  const T r0 = lane_read(v, 15), r1 = lane_read(v, 31), r2 = lane_read(v, 47);
-  const T c01 = op(r0, r1), c012 = op(c01, r2);
-  if (row == 1) v = op(r0, v);
-  else if (row == 2) v = op(c01, v);
-  else if (row == 3) v = op(c012, v);
-  return v;
-}
-// inclusive suffix over lanes 63..0 (op applied as op(earlier, later))
-template <typename T, typename Op>
-__device__ __forceinline__ T wave_suffix(T v, Op op) {
-  const int lane = threadIdx.x & 63, rl = lane & 15, row = lane >> 4;
-  T t = dpp_mov<0x101>(v);
-  if (rl <= 14) v = op(v, t);
-  t = dpp_mov<0x102>(v);
-  if (rl <= 13) v = op(v, t);
-  t = dpp_mov<0x104>(v);
-  if (rl <= 11) v = op(v, t);
-  t = dpp_mov<0x108>(v);
-  if (rl <= 7) v = op(v, t);
-  const T r1 = lane_read(v, 16), r2 = lane_read(v, 32), r3 = lane_read(v, 48);
-  const T c23 = op(r2, r3), c123 = op(r1, c23);
-  if (row == 2) v = op(v, r3);
-  else if (row == 1) v = op(v, c23);
-  else if (row == 0) v = op(v, c123);
-  return v;
-}
-
-// numpy.heaviside(d, 1.0)
-__device__ __forceinline__ double heaviside1(double d) { return d < 0.0 ? 0.0 : (d >= 0.0 ? 1.0 : d); }
-
-// One density sample, in the reference's evaluation order (see prom_density_kind in prom_hip.h).
-__device__ __forceinline__ double density_at(const DensityDev& m, double xv, double y, double z,
-                                             double bx, double by) {
-  const double dx = xv - bx, dy = y - by;
-  switch (m.kind) {
-    case PROM_DENSITY_BAROMETRIC: {
-      const double r = sqrt((dx * dx + dy * dy) + z * z);
-      return (m.p[0] * exp((m.p[1] - r) / m.p[2])) * heaviside1(r - m.p[1]);
-    }
-    case PROM_DENSITY_HYDROSTATIC: {
-      const double r = sqrt((dx * dx + dy * dy) + z * z);
-      const double jeans = m.p[2] / (m.p[3] * r) * heaviside1(r - m.p[1]);
-      return m.p[0] * exp(jeans - m.p[4]);
-    }
-    case PROM_DENSITY_POWERLAW: {
-      const double r = sqrt((dx * dx + dy * dy) + z * z);
-      return (m.p[0] * pow(m.p[1] / r, m.p[2])) * heaviside1(r - m.p[1]);
-    }
-    case PROM_DENSITY_TORUS: {
-      const double a = sqrt(dx * dx + dy * dy);
-      const double ta = (a - m.p[1]) / m.p[2];
-      const double tz = z / m.p[3];
-      return m.p[0] * (exp(-(ta * ta)) * exp(-(tz * tz)));
-    }
-    default:
-      return __builtin_nan("");
-  }
-}
-
-// numpy pairwise_sum of (a[i] * chi) for i < n (numpy/_core/src/umath/loops_utils.h.src),
-// then the reduction identity: 0.0 + result.
-__device__ __forceinline__ double pw_leaf(const double* __restrict__ a, int64_t n, double chi) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int64_t i = 0; i < n; ++i) r += a[i] * chi;
-    return r;
-  }
-  double r0 = a[0] * chi, r1 = a[1] * chi, r2 = a[2] * chi, r3 = a[3] * chi;
-  double r4 = a[4] * chi, r5 = a[5] * chi, r6 = a[6] * chi, r7 = a[7] * chi;
-  int64_t i = 8;
-  const int64_t lim = n - (n % 8);
-  for (; i < lim; i += 8) {
-    r0 += a[i + 0] * chi; r1 += a[i + 1] * chi; r2 += a[i + 2] * chi; r3 += a[i + 3] * chi;
-    r4 += a[i + 4] * chi; r5 += a[i + 5] * chi; r6 += a[i + 6] * chi; r7 += a[i + 7] * chi;
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += a[i] * chi;
-  return res;
-}
-
-__device__ double pairwise_sum_chi(const double* __restrict__ a, int64_t n, double chi) {
-  if (n <= 128) return 0.0 + pw_leaf(a, n, chi);
-  struct Frame { int64_t off, n; int stage; double left; };
-  Frame st[48];
-  int sp = 0;
-  st[0] = {0, n, 0, 0.0};
-  double ret = 0.0;
-  while (sp >= 0) {
-    Frame& f = st[sp];
-    if (f.n <= 128) { ret = pw_leaf(a + f.off, f.n, chi); --sp; continue; }
-    int64_t n2 = f.n / 2;
-    n2 -= n2 % 8;
-    if (f.stage == 0) { f.stage = 1; st[++sp] = {f.off, n2, 0, 0.0}; }
-    else if (f.stage == 1) { f.left = ret; f.stage = 2; st[++sp] = {f.off + n2, f.n - n2, 0, 0.0}; }
-    else { ret = f.left + ret; --sp; }
-  }
-  return 0.0 + ret;
-}
-
-// ------------------------------------------------------------------ function-level kernels
-__global__ void k_table_lookup(const double* __restrict__ xp, const double* __restrict__ fp, int64_t n,
-                               double offset, const double* __restrict__ t, int64_t nt,
-                               double* __restrict__ out) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nt;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    out[i] = pow(10.0, np_interp(t[i], xp, fp, n)) - offset;
-  }
-}
-
-void launch_table_lookup(hipStream_t s, const double* x, const double* y, int64_t n, double offset,
-                         const double* targets, int64_t nt, double* out) {
-  if (nt == 0) return;
-  hipLaunchKernelGGL(k_table_lookup, dim3(grid_for(nt)), dim3(kBlock), 0, s, x, y, n, offset, targets,
-                     nt, out);
-  PROM_HIP(hipGetLastError());
-}
-
-__global__ void k_voigt(const double* __restrict__ x, int64_t n, const double* __restrict__ lw,
-                        const double* __restrict__ lg, const double* __restrict__ lc, int32_t nl,
-                        double sigma_v, double c_light, double offset, int log_table,
-                        double* __restrict__ out) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const double cx = c_light / x[i];
-    double s = 0.0;
-    for (int32_t l = 0; l < nl; ++l) {
-      const double lam0 = lw[l];
-      const double prof = voigt_profile(cx - c_light / lam0, sigma_v / lam0, lg[l]);
-      s += lc[l] * prof;
-    }
-    out[i] = log_table ? log10(s + offset) : s;
-  }
-}
-
-void launch_voigt(hipStream_t s, const double* x, int64_t n, const double* lw, const double* lg,
-                  const double* lc, int32_t nl, double sigma_v, double c_light, double offset,
-                  int log_table, double* out) {
-  if (n == 0) return;
-  hipLaunchKernelGGL(k_voigt, dim3(grid_for(n, 128)), dim3(128), 0, s, x, n, lw, lg, lc, nl, sigma_v,
-                     c_light, offset, log_table, out);
-  PROM_HIP(hipGetLastError());
-}
-
-__global__ void k_density(DensityDev m, const double* __restrict__ x, int32_t n_x,
-                          const double* __restrict__ y, const double* __restrict__ z,
-                          const double* __restrict__ bx, const double* __restrict__ by, int64_t n_chords,
-                          double* __restrict__ out) {
-  const int64_t tot = n_chords * n_x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = i / n_x;
-    const int32_t ix = (int32_t)(i - c * n_x);
-    out[i] = density_at(m, x[ix], y[c], z[c], bx[c], by[c]);
-  }
-}
-
-void launch_density(hipStream_t s, const DensityDev& m, const double* x, int32_t n_x, const double* y,
-                    const double* z, const double* bx, const double* by, int64_t n_chords,
-                    double* out) {
-  if (n_chords * n_x == 0) return;
-  hipLaunchKernelGGL(k_density, dim3(grid_for(n_chords * n_x)), dim3(kBlock), 0, s, m, x, n_x, y, z, bx,
-                     by, n_chords, out);
-  PROM_HIP(hipGetLastError());
-}
-
-// ------------------------------------------------------------------ molecular lookup
-// Bracketing index of a sorted axis for RegularGridInterpolator (scipy _find_indices):
-// i = searchsorted(g, v) - 1 clipped to [0, n-2]; t = (v - g[i]) / (g[i+1] - g[i]).
-// Returns false when v is outside [g[0], g[n-1]] (fill value).
-__device__ __forceinline__ bool rgi_bracket(const double* __restrict__ g, int64_t n, double v, int64_t* i,
-                                            double* t) {
-  if (!(v >= g[0] && v <= g[n - 1])) return false;
-  int64_t lo = 0, hi = n;  // first index with g[idx] >= v  (searchsorted left)
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (g[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  int64_t k = lo - 1;
-  if (k < 0) k = 0;
-  if (k > n - 2) k = n - 2;
-  *i = k;
-  *t = (v - g[k]) / (g[k + 1] - g[k]);
-  return true;
-}
-
-// Trilinear value at (P, T, w), scipy's hypercube order: corners (dP, dT, dw) lexicographic,
-// weight = ((1 * wP) * wT) * ww, value = ((0 + v000 w) + v001 w) + ...
-__device__ __forceinline__ double mol_value(const double* __restrict__ V, int32_t n_t, int64_t n_w,
-                                            int64_t ip, double tp, int64_t it, double tt, int64_t iw,
-                                            double tw) {
-  double value = 0.0;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int dp = (c >> 2) & 1, dt = (c >> 1) & 1, dw = c & 1;
-    const double wp = dp ? tp : 1.0 - tp;
-    const double wt = dt ? tt : 1.0 - tt;
-    const double ww = dw ? tw : 1.0 - tw;
-    const double weight = ((1.0 * wp) * wt) * ww;
-    value = value + V[((ip + dp) * n_t + (it + dt)) * n_w + (iw + dw)] * weight;
-  }
-  return value;
-}
-
-__global__ void k_mol_sigma(const double* __restrict__ Pg, int32_t n_p, const double* __restrict__ Tg,
-                            int32_t n_t, const double* __restrict__ Wg, int64_t n_w,
-                            const double* __restrict__ V, double offset, int64_t n_chords, int32_t n_x,
-                            const double* __restrict__ P, double T, int64_t n_wav,
-                            const double* __restrict__ wav, double* __restrict__ out) {
-  const int64_t tot = n_chords * n_x * n_wav;
-  const double fill = log10(offset);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t w = i % n_wav;
-    const int64_t cx = i / n_wav;
-    const int64_t c = cx / n_x;
-    double p = P[cx];
-    p = p < 1e-4 ? 1e-4 : p;
-    int64_t ip, it, iw;
-    double tp, tt, tw;
-    double v = fill;
-    if (rgi_bracket(Pg, n_p, p, &ip, &tp) && rgi_bracket(Tg, n_t, T, &it, &tt) &&
-        rgi_bracket(Wg, n_w, wav[c * n_wav + w], &iw, &tw))
-      v = mol_value(V, n_t, n_w, ip, tp, it, tt, iw, tw);
-    out[i] = pow(10.0, v) - offset;
-  }
-}
-
-void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, int32_t n_x,
-                            const double* P, double T, int64_t n_wav, const double* wav, double* out) {
-  const int64_t tot = n_chords * n_x * n_wav;
-  if (tot == 0) return;
-  hipLaunchKernelGGL(k_mol_sigma, dim3(grid_for(tot)), dim3(kBlock), 0, s, t.P.as<double>(), t.n_p,
-                     t.T.as<double>(), t.n_t, t.W.as<double>(), t.n_w, t.V.as<double>(), t.offset,
-                     n_chords, n_x, P, T, n_wav, wav, out);
-  PROM_HIP(hipGetLastError());
-}
-
-// ------------------------------------------------------------------ reductions
-__global__ void k_max(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
-  __shared__ double sm[kBlock];
-  double m = -INFINITY;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const double a = v[i];
-    m = (a > m || a != a) ? a : m;
-  }
-  sm[threadIdx.x] = m;
-  __syncthreads();
-  for (int s = kBlock / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      const double a = sm[threadIdx.x + s];
-      if (a > sm[threadIdx.x] || a != a) sm[threadIdx.x] = a;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
-}
-
-// max (NaN-propagating) of a device array; scratch_dev must hold 1024 doubles
-double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev) {
-  const unsigned g = grid_for(n, kBlock, 1024);
-  hipLaunchKernelGGL(k_max, dim3(g), dim3(kBlock), 0, s, v, n, scratch_dev);
-  PROM_HIP(hipGetLastError());
-  std::vector<double> h(g);
-  PROM_HIP(hipMemcpyAsync(h.data(), scratch_dev, sizeof(double) * g, hipMemcpyDeviceToHost, s));
-  PROM_HIP(hipStreamSynchronize(s));
-  double m = -INFINITY;
-  for (double a : h) m = (a > m || a != a) ? a : m;
-  return m;
-}
 
 // ------------------------------------------------------------------ transit pipeline
 __global__ void k_ntot(DensityDev m, int32_t sc, const double* __restrict__ x, int32_t n_x,
@@ -921,176 +501,6 @@ __global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restric
   }
 }
 
-// ---- windowed integration: per-phase record order, envelopes, threshold tables, tail moments ----
-// For one phase and one wavelength, tau_i = sum_s N_si sigma_s.  With n_si = c_s N_si (c_s = 1 /
-// (chi_s n_ref L): n_ref bounds the scenario's density, L = n_x dx, so n <= 1; SigTabDev::ncoef) and
-// q_s = sigma_s / c_s, every record i satisfies
-//     a_i Q <= tau_i <= b_i Q,   a_i = min_s n_si,  b_i = max_s n_si,  Q = sum_s q_s
-// (sigma_s >= 0 up to the 1e-50 table offset's rounding, which the bounds absorb).
-// Records are ordered by b descending (ties: chord index), equal-column chords merged, and two
-// envelopes kept: B_i = max_{j >= i} b_j and A_i = min_{j <= i} a_j (both non-increasing in i).
-// For a wavefront whose wavelengths have Q in [Q_lo, Q_hi]:
-//   * records j >= t with B_t Q_hi < eps have tau_j < eps: their sum of F e^-tau is the cubic Taylor
-//     polynomial sum_e q^e M_e(t), with suffix moments M_e(t) = c_e sum_{j >= t} F_j prod_s n_sj^e_s
-//     (|e| <= 3, c_e = (-1)^|e| / prod e_s!); truncation error <= eps^4/24 per unit weight;
-//   * records j < h with A_h Q_lo >= tau_sat have tau_j >= tau_sat: skipped, error <= e^-tau_sat each;
-//   * records h <= j < t are integrated exactly (table exp).
-// eps = 2^-10, tau_sat = 40: |dR| <= 2^-40/24 + e^-40 < 4e-14 (merging adds <= 2^-40/e).
-// t and h come from per-phase tables indexed by the threshold's binade and top three mantissa bits
-// (X_v = the double with bits v << 49): tab_t[v] = #{i : B_i >= X_v}, tab_h[v] = #{i : A_i >= X_v};
-// the tau kernel picks the conservative neighbour (X_v <= eps/Q_hi for t, X_v > tau_sat/Q_lo for h).
-constexpr int kWBlock = 512;
-constexpr int kWPer = kWinMax / kWBlock;           // sorted positions per thread
-constexpr int kEnvVmax = 8184;                     // bits(1.0) >> 49
-constexpr int kEnvVmin = kEnvVmax - kEnvN + 1;     // X_vmin = 2^-(kEnvN / 8)
-// Tail of the window (records with tau < eps at every wavelength of the wavefront): the Taylor
-// polynomial of degree D in q_s over suffix moments, truncation <= eps^(D+1)/(D+1)! per unit weight.
-// One effective species (NS == 1, e.g. merged species): D = 7, eps = 2^-4 (5.8e-15); otherwise
-// D = 3, eps = 2^-10 (3.5e-14) -- (NS+D choose D) moments per record either way stays small.
-template <int NS> struct TailDeg { static constexpr int D = NS == 1 ? 7 : 3; };
-template <int NS> __host__ __device__ constexpr double tail_eps() { return NS == 1 ? 0x1p-4 : 0x1p-10; }
-
-// histogram slot of a non-negative envelope value: 1 + (table index of its 1/8-octave bucket), 0 below
-// the table, kEnvN + 1 above it.  v >= X_e  <=>  (bits(v) >> 49) >= kEnvVmin + e.
-__device__ __forceinline__ int32_t env_slot(double v) {
-  const int64_t b = (int64_t)(__builtin_bit_cast(unsigned long long, v) >> 49) - kEnvVmin;
-  return b < 0 ? 0 : (b >= kEnvN ? kEnvN + 1 : (int32_t)b + 1);
-}
-constexpr double kTauSat = 40.0;
-
-// Table index of a positive float threshold: the largest v with X_v = double(bits v << 49) <= x;
-// below the table for zero/denormal x, above it for +inf.
-__device__ __forceinline__ int env_floor(float x) {
-  if (!(x >= 1.17549435e-38f)) return -(1 << 28);
-  if (!(x <= 3.40282347e+38f)) return 1 << 28;
-  return (int)(__builtin_bit_cast(uint32_t, x) >> 20) + 7168;
-}
-
-
-__host__ __device__ constexpr int binom_c(int n, int k) {
-  int r = 1;
-  for (int i = 1; i <= k; ++i) r = r * (n - k + i) / i;
-  return r;
-}
-
-// Monomials of total degree <= D in NS variables, by degree then lexicographically; c[k] = (-1)^j / prod e_s!
-template <int NS>
-struct Monos {
-  static constexpr int D = TailDeg<NS>::D;
-  static constexpr int K = binom_c(NS + D, D);
-  int e[K][NS];
-  double c[K];
-  constexpr Monos() : e{}, c{} {
-    int total = 1;
-    for (int s = 0; s < NS; ++s) total *= D + 1;
-    int k = 0;
-    for (int j = 0; j <= D; ++j)
-      for (int idx = 0; idx < total; ++idx) {
-        int d[NS] = {};
-        int r = idx, sum = 0;
-        for (int s = NS - 1; s >= 0; --s) { d[s] = r % (D + 1); r /= D + 1; sum += d[s]; }
-        if (sum != j) continue;
-        double f = 1.0;
-        for (int s = 0; s < NS; ++s) {
-          e[k][s] = d[s];
-          for (int m = 2; m <= d[s]; ++m) f *= m;
-        }
-        c[k] = ((j & 1) ? -1.0 : 1.0) / f;
-        ++k;
-      }
-  }
-};
-
-// p[s][j] = v_s^j, formed as ((v v) v) ...
-template <int NS>
-__device__ __forceinline__ void tail_pows(const double (&v)[NS], double (&p)[NS][TailDeg<NS>::D + 1]) {
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    p[s][0] = 1.0;
-    p[s][1] = v[s];
-#pragma unroll
-    for (int j = 2; j <= TailDeg<NS>::D; ++j) p[s][j] = p[s][j - 1] * v[s];
-  }
-}
-
-// prod_s p[s][e_s] for monomial k
-template <int NS>
-__device__ __forceinline__ double mono_eval(const Monos<NS>& M, int k, const double (&p)[NS][TailDeg<NS>::D + 1]) {
-  double r = 1.0;
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-    if (M.e[k][s]) r *= p[s][M.e[k][s]];
-  return r;
-}
-
-// The tail sum_k mm[k] q^e_k (mm already carries c[k]): Horner for one species, monomials otherwise.
-// Every tau kernel evaluates it through this function, so they agree bit for bit.
-template <int NS>
-__device__ __forceinline__ double tail_eval(const double (&mm)[Monos<NS>::K], const double (&q)[NS]) {
-  constexpr Monos<NS> M{};
-  constexpr int K = Monos<NS>::K;
-  if constexpr (NS == 1) {
-    double tl = mm[K - 1];
-#pragma unroll
-    for (int k = K - 2; k >= 0; --k) tl = __builtin_fma(tl, q[0], mm[k]);
-    return tl;
-  } else {
-    double p[NS][TailDeg<NS>::D + 1];
-    tail_pows<NS>(q, p);
-    double tl = 0.0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) tl = __builtin_fma(mm[k], mono_eval<NS>(M, k, p), tl);
-    return tl;
-  }
-}
-
-struct OpAdd { template <typename T> __device__ T operator()(T a, T b) const { return a + b; } };
-struct OpMax { __device__ double operator()(double a, double b) const { return a > b ? a : b; } };
-struct OpMin { __device__ double operator()(double a, double b) const { return a < b ? a : b; } };
-
-// Exclusive scans over the kWBlock threads of a workgroup (8 waves); wsum: NW slots of LDS.
-// *total (optional) receives the fold over all threads.
-template <typename T, typename Op>
-__device__ __forceinline__ T wg_excl_prefix(T v, Op op, T id, T* wsum, T* total = nullptr) {
-  constexpr int NW = kWBlock / 64;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  T inc = v;
-  for (int off = 1; off < 64; off <<= 1) {
-    const T u = __shfl_up(inc, off, 64);
-    if (lane >= off) inc = op(inc, u);
-  }
-  T exc = __shfl_up(inc, 1, 64);
-  if (lane == 0) exc = id;
-  __syncthreads();
-  if (lane == 63) wsum[wid] = inc;
-  __syncthreads();
-  T carry = id, all = id;
-  for (int w = 0; w < NW; ++w) {
-    if (w < wid) carry = op(carry, wsum[w]);
-    all = op(all, wsum[w]);
-  }
-  if (total) *total = all;
-  return op(carry, exc);
-}
-
-template <typename T, typename Op>
-__device__ __forceinline__ T wg_excl_suffix(T v, Op op, T id, T* wsum) {
-  constexpr int NW = kWBlock / 64;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  T inc = v;
-  for (int off = 1; off < 64; off <<= 1) {
-    const T u = __shfl_down(inc, off, 64);
-    if (lane + off < 64) inc = op(inc, u);
-  }
-  T exc = __shfl_down(inc, 1, 64);
-  if (lane == 63) exc = id;
-  __syncthreads();
-  if (lane == 0) wsum[wid] = inc;
-  __syncthreads();
-  T carry = id;
-  for (int w = NW - 1; w > wid; --w) carry = op(carry, wsum[w]);
-  return op(carry, exc);
-}
 
 // One workgroup per phase, few dependent steps (2 global round trips, ~8 workgroup barriers for
 // phases with <= 1024 active chords):
@@ -1605,84 +1015,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     counts[o * kCnt + 7] = 0;
   }
   PROM_TS(o * 16 + 8);
-}
-
-// tau of one chord in the exact (non-finite column) path.  With merged species (zf != nullptr) the
-// single column is N = dx sum_x n and Y = sum_s chi_s sigma_s: the reference's sum_s (N chi_s) sigma_s is
-// NaN for an infinite N wherever some chi_s sigma_s is not > 0 (zf[w]), which N Y alone would miss.
-__device__ __forceinline__ double exact_tau_merged(double N, double Y, const uint8_t* __restrict__ zf, int64_t w) {
-  double tau = N * Y;
-  if (zf && !__builtin_isfinite(N) && zf[w]) tau = __builtin_nan("");
-  return tau;
-}
-
-// ---- fast exp: acc + F * 2^(y/2048) with a 2048-entry table in LDS --------------------------------
-// y = -tau * 2048/ln2.  k = rint(y), d = y - k in [-1/2, 1/2],
-//   2^(y/2048) = 2^(k >> 11) * T[k & 2047] * exp(d ln2/2048),
-// exp(d c) = 1 + d (c + d (c^2/2 + d c^3/6)) with c = ln2/2048: truncation (c/2)^4/24 = 3.5e-17.
-// Finite y only (non-finite column densities take the exact path); y below -2^31 saturates the
-// integer conversion and ldexp flushes the term to 0, which is exp's own answer there.
-constexpr double kExpC1 = 0.0003384507717577858;     // ln2 / 2048
-constexpr double kExpC2 = 5.727446245172041e-08;     // c^2 / 2
-constexpr double kExpC3 = 6.461528672932366e-12;     // c^3 / 6
-constexpr double kMinus2048OverLn2 = -2954.639443740597;
-
-__device__ __forceinline__ double acc_exp2k(double acc, double F, double y, const double* __restrict__ tab) {
-  const double k = __builtin_rint(y);
-  const int ki = (int)k;
-  const double d = y - k;
-  double t = __builtin_fma(d, kExpC3, kExpC2);
-  t = __builtin_fma(d, t, kExpC1);
-  const double e = __builtin_fma(d, t, 1.0);
-  const double S = __builtin_amdgcn_ldexp(tab[ki & (PROM_EXP2_TABLE_N - 1)], ki >> 11);
-  return __builtin_fma(F * S, e, acc);
-}
-
-// acc + F * exp(-tau) with y = -tau * 256 / ln2 given: 2^(y/256) = 2^(k >> 8) T[k & 255] exp(d ln2/256),
-// k = rint(y), d = y - k in [-1/2, 1/2], degree-5 Taylor polynomial (truncation (ln2/512)^6/720 = 9e-21
-// relative), T[i] = 2^(i/256) = the 2048-entry table at 8i (LDS, 2 KB).  y below -2^31 saturates the
-// integer conversion and ldexp returns 0, exp's own answer there.  About 12 FP64 operations.
-constexpr double kE256C1 = 0x1.62e42fefa39efp-9;   // (ln2/256)^1 / 1!
-constexpr double kE256C2 = 0x1.ebfbdff82c58fp-19;  // (ln2/256)^2 / 2!
-constexpr double kE256C3 = 0x1.c6b08d704a0c0p-29;  // (ln2/256)^3 / 3!
-constexpr double kE256C4 = 0x1.3b2ab6fba4e77p-39;  // (ln2/256)^4 / 4!
-constexpr double kE256C5 = 0x1.5d87fe78a6731p-50;  // (ln2/256)^5 / 5!
-constexpr double kM256Ln2 = -0x1.71547652b82fep+8; // -256 / ln2
-
-__device__ __forceinline__ double acc_exp256(double acc, double F, double y, const double* __restrict__ tab) {
-  const double k = __builtin_rint(y);
-  const int ki = (int)k;
-  const double d = y - k;
-  double p = __builtin_fma(d, kE256C5, kE256C4);
-  p = __builtin_fma(d, p, kE256C3);
-  p = __builtin_fma(d, p, kE256C2);
-  p = __builtin_fma(d, p, kE256C1);
-  p = __builtin_fma(d, p, 1.0);
-  const double S = __builtin_amdgcn_ldexp(tab[ki & 255], ki >> 8);
-  return __builtin_fma(F * S, p, acc);
-}
-
-// acc + F * exp(-tau) with y = -tau * 1024 / ln2 given: 2^(y/1024) = 2^(k >> 10) T[k & 1023] exp(d ln2/1024),
-// k = rint(y), d in [-1/2, 1/2], cubic Taylor polynomial (truncation (ln2/2048)^4/24 = 5.5e-16 relative),
-// T[i] = 2^(i/1024) = the 2048-entry table at 2i (LDS, 8 KB).  About 10 FP64 operations.
-constexpr double kE1024C1 = 0x1.62e42fefa39efp-11;  // (ln2/1024)^1 / 1!
-constexpr double kE1024C2 = 0x1.ebfbdff82c58fp-23;  // (ln2/1024)^2 / 2!
-constexpr double kE1024C3 = 0x1.c6b08d704a0c0p-35;  // (ln2/1024)^3 / 3!
-constexpr double kM1024Ln2 = -0x1.71547652b82fep+10; // -1024 / ln2
-
-__device__ __forceinline__ double acc_exp1024(double acc, double F, double y, const double* __restrict__ tab) {
-  const double k = __builtin_rint(y);
-  const int ki = (int)k;
-  const double d = y - k;
-  double p = __builtin_fma(d, kE1024C3, kE1024C2);
-  p = __builtin_fma(d, p, kE1024C1);
-  p = __builtin_fma(d, p, 1.0);
-  const double S = __builtin_amdgcn_ldexp(tab[ki & 1023], ki >> 10);
-  return __builtin_fma(F * S, p, acc);
-}
-
-__device__ __forceinline__ void fill_exp_table(double* etab) {
-  for (int i = threadIdx.x; i < PROM_EXP2_TABLE_N; i += kBlock) etab[i] = kExp2TableDev[i];
 }
 
 // Fused sigma lookup -> tau -> exp(-tau) -> disk sum -> ratio.
@@ -2479,407 +1811,6 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
 #endif
 }
 
-// ---- molecular fused kernel -------------------------------------------------------------------
-// tau(c, w) = sum_atomic N_s sigma_s(w) + sum_mol dx * sum_x n_abs(c,x) sigma_m(P(c,x), T, lambda'_w)
-// (gasProperties.py:924-954).  Per thread (phase o, wavelength w) and molecular slot, the (T, lambda)
-// part of the trilinear RegularGridInterpolator weights is fixed: u_i = sum_{T,lambda corners} w V[i][.][.]
-// is formed once for every P node i into LDS; each (chord, sample) then costs one P interpolation
-// (uniform bracket from k_mol_prep), 10^v and an FMA.  Out-of-table samples (P, T or lambda) take the
-// fill value, i.e. sigma = 0, as in the reference.
-constexpr double kLog2Ten2048 = 0x1.a934f0979a371p+12;   // 2048 log2(10)
-
-template <int NSA, int EXPK>
-__global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const SigTabDev* __restrict__ tabs,
-                                                    const MolSlotDev* __restrict__ ms, int32_t n_mol,
-                                                    int32_t max_np, const double* __restrict__ wav,
-                                                    const double* __restrict__ recs,
-                                                    const int32_t* __restrict__ act_ip,
-                                                    const double* __restrict__ fout,
-                                                    const int32_t* __restrict__ counts,
-                                                    const double* __restrict__ tfrac,
-                                                    const double* __restrict__ fsum, int32_t n_pr,
-                                                    int32_t n_orb, int32_t phases_per_group, int64_t n_wav,
-                                                    int32_t n_x, double delta_x,
-                                                    const int32_t* __restrict__ mip,
-                                                    const double* __restrict__ mwp,
-                                                    const double* __restrict__ mna, double* __restrict__ R) {
-  extern __shared__ double lds[];   // [2048] exp table | [n_mol][max_np][kBlock] u
-  double* etab = lds;
-  double* ul = lds + PROM_EXP2_TABLE_N;
-  if (EXPK) fill_exp_table(etab);
-  __syncthreads();
-  const int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-  const bool live = w < n_wav;
-  const double lam = wav[live ? w : n_wav - 1];
-  const int32_t o0 = blockIdx.y * phases_per_group;
-  const int32_t o1 = min(n_orb, o0 + phases_per_group);
-  constexpr int ST = 1 + NSA;
-  constexpr int NR = NSA > 0 ? NSA : 1;
-  double sg[NR], shv[NR];
-#pragma unroll
-  for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); sg[s] = 0.0; }
-  int64_t whint[4] = {-1, -1, -1, -1};
-  const int64_t nc = (int64_t)n_orb * n_pr;
-  for (int32_t o = o0; o < o1; ++o) {
-    const bool exact = !EXPK || counts[o * kCnt + 3] != 0;
-    const int32_t n_act = counts[o * kCnt + 0];
-    const double* __restrict__ rec = recs + (int64_t)o * n_pr * ST;
-#pragma unroll
-    for (int s = 0; s < NSA; ++s) {
-      const double sh = tabv.t[s].shift[o];
-      if (!(sh == shv[s])) {
-        sg[s] = sigma_of(sh * lam, tabv.t[s]);
-        shv[s] = sh;
-      }
-    }
-    uint32_t inb = 0;   // bit m: molecular slot m has (T, lambda') inside its table
-    for (int32_t m = 0; m < n_mol; ++m) {
-      const MolSlotDev d = ms[m];
-      int64_t it, iw;
-      double tt, tw;
-      const double lw = d.shift[o] * lam;
-      bool ok = rgi_bracket(d.T, d.n_t, d.temp, &it, &tt);
-      if (ok) {
-        // gallop the wavelength bracket from the previous phase's
-        ok = lw >= d.W[0] && lw <= d.W[d.n_w - 1];
-        if (ok) {
-          int64_t h = m < 4 ? whint[m] : -1;
-          int64_t lo = 0, hi = d.n_w - 1;
-          if (h >= 0 && h <= d.n_w - 2 && d.W[h] < lw && lw <= d.W[h + 1]) { lo = h; hi = h + 1; }
-          // scipy: i = searchsorted(g, v, 'left') - 1 clipped to [0, n-2]
-          while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (d.W[mid] < lw) lo = mid; else hi = mid;
-          }
-          iw = lo;
-          if (lw <= d.W[0]) iw = 0;
-          tw = (lw - d.W[iw]) / (d.W[iw + 1] - d.W[iw]);
-          if (m < 4) whint[m] = iw;
-        }
-      }
-      if (ok) {
-        inb |= 1u << m;
-        const double w00 = (1.0 - tt) * (1.0 - tw), w01 = (1.0 - tt) * tw;
-        const double w10 = tt * (1.0 - tw), w11 = tt * tw;
-        for (int32_t i = 0; i < d.n_p; ++i) {
-          const double* v0 = d.V + ((int64_t)i * d.n_t + it) * d.n_w + iw;
-          const double* v1 = v0 + d.n_w;
-          double u = 0.0;
-          u = u + v0[0] * w00;
-          u = u + v0[1] * w01;
-          u = u + v1[0] * w10;
-          u = u + v1[1] * w11;
-          ul[((int64_t)m * max_np + i) * kBlock + threadIdx.x] = u;
-        }
-      }
-    }
-    const int32_t* ipl = act_ip + (int64_t)o * n_pr;
-    double acc = 0.0;
-    const double scale = exact ? 1.0 : kMinus2048OverLn2;
-    int32_t ip_next = n_act > 0 ? ipl[0] : 0;
-    for (int32_t ci = 0; ci < n_act; ++ci) {
-      const double* r = rec + (int64_t)ci * ST;
-      const int32_t ip = ip_next;
-      if (ci + 1 < n_act) ip_next = ipl[ci + 1];   // the next chord's index is in flight meanwhile
-      double tau = 0.0;
-#pragma unroll
-      for (int s = 0; s < NSA; ++s) tau = tau + r[1 + s] * sg[s];
-      for (int32_t m = 0; m < n_mol; ++m) {
-        if (!((inb >> m) & 1u)) continue;
-        const MolSlotDev d = ms[m];
-        const int64_t base = ((int64_t)m * nc + (int64_t)o * n_pr + ip) * n_x;
-        const double* um = ul + (int64_t)m * max_np * kBlock + threadIdx.x;
-        double sm = 0.0;
-        // (uniform per wavefront: scalar loads, batched by the unroll)
-#pragma unroll 10
-        for (int32_t ix = 0; ix < n_x; ++ix) {
-          const int32_t pi = mip[base + ix];
-          if (pi < 0) continue;
-          const double tp = mwp[base + ix];
-          const double v = (1.0 - tp) * um[(int64_t)pi * kBlock] + tp * um[(int64_t)(pi + 1) * kBlock];
-          // 10^v: the LDS-table 2^(y/2048) with y = v 2048 log2(10) in table mode (relative error
-          // ~ |v| 2.3 2^-53 from the argument product, ~1e-14 at the table's floor), ocml otherwise
-          const double p10 = (EXPK && !exact) ? acc_exp2k(0.0, 1.0, v * kLog2Ten2048, etab) : exp10(v);
-          sm = __builtin_fma(mna[base + ix], p10 - d.offset, sm);
-        }
-        tau = tau + sm * delta_x;
-      }
-      if (!exact) acc = acc_exp2k(acc, r[0], tau * scale, etab);
-      else acc = acc + fout[ip] * exp(-tau);
-    }
-    if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
-  }
-}
-
-// ---- stellar spectrum path (gasProperties.py:1180-1219 with Fstar_function set) ----------------------
-// F(c, w) = rho_c * (F_star(lambda_w / s_c) * clv_c) differs per chord AND wavelength (the Rossiter-
-// McLaughlin shift s_c moves the stellar lines across the disk), so neither the flat-star F_out
-// factorisation nor the windowed tail moments apply: every (chord, wavelength) flux is evaluated.
-// One thread per wavelength, kRmP phases per workgroup.  F is computed once per (chord, wavelength)
-// and shared by the workgroup's phases; chords transparent at every phase of the group add F to one
-// shared sum (exp(-tau) == 1 to the last ulp), the others are resolved per phase from a bit mask.
-// F_star(t) = 10^(f_k + slope_k (t - x_k)) is evaluated as 10^f_k * exp(ln10 slope_k (t - x_k)) on the
-// LDS copy of the star-table slice that the workgroup's targets t = lambda / s can reach (prom_api.hip
-// rm_slices), bracketed through a slice-local bucket directory; a tile whose slice exceeds kRmStarMax
-// nodes uses the global lookup (sigma_of).  With one shift for every chord (no rotation) F_star is
-// evaluated once per wavelength.
-constexpr int kRmP = 8;            // phases per workgroup
-constexpr int kRmChunk = 64;       // chords staged in LDS per sweep
-constexpr int kRmGroup = 4;        // chords whose F_star lookups are interleaved
-constexpr int kRmDir = 2 * kRmStarMax;   // slice-directory buckets (at most)
-constexpr double kLn10 = 2.302585092994045684;
-
-// exp(a) for the F_star interpolation factor (|a| <= ln10 |f_k+1 - f_k|): the 256-entry table scheme of
-// acc_exp256 (relative error ~ |a| 2^-53 from the argument scaling)
-__device__ __forceinline__ double exp_tab(double a, const double* __restrict__ tab) {
-  const double y = a * -kM256Ln2;
-  const double k = __builtin_rint(y);
-  const int ki = (int)k;
-  const double d = y - k;
-  double p = __builtin_fma(d, kE256C5, kE256C4);
-  p = __builtin_fma(d, p, kE256C3);
-  p = __builtin_fma(d, p, kE256C2);
-  p = __builtin_fma(d, p, kE256C1);
-  p = __builtin_fma(d, p, 1.0);
-  return __builtin_amdgcn_ldexp(tab[ki & 255], ki >> 8) * p;
-}
-
-template <int NSMAX, bool OCML, bool UNISTAR>
-__global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__ tabs, int32_t na,
-                                                   const SigTabDev star, const int32_t* __restrict__ slices,
-                                                   const double* __restrict__ wav, int64_t n_wav,
-                                                   const double* __restrict__ crho,
-                                                   const double* __restrict__ cclv,
-                                                   const double* __restrict__ cshift,
-                                                   const int32_t* __restrict__ flags,
-                                                   const double* __restrict__ ncol, int32_t n_pr,
-                                                   int32_t n_orb, int32_t* __restrict__ counts,
-                                                   double* __restrict__ R) {
-  __shared__ double sexp[256];
-  __shared__ double sx[kRmStarMax], sF[kRmStarMax], sc[kRmStarMax];
-  __shared__ int16_t sdir[kRmDir];
-  __shared__ double sRho[kRmChunk], sClv[kRmChunk], sSh[kRmChunk];
-  __shared__ double sN[kRmP * NSMAX * kRmChunk];
-  __shared__ int32_t sMask[kRmChunk];
-  __shared__ int32_t scnt[kRmP * 3];
-  sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
-  const int32_t o0 = blockIdx.y * kRmP;
-  const int32_t np = n_orb - o0 < kRmP ? n_orb - o0 : kRmP;
-  const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool live = w < n_wav;
-  const double lam = wav[live ? w : n_wav - 1];
-  // chord counts per phase (stats), by the first workgroup of each phase group
-  if (blockIdx.x == 0 && counts) {
-    if (threadIdx.x < kRmP * 3) scnt[threadIdx.x] = 0;
-    __syncthreads();
-    for (int p = 0; p < np; ++p)
-      for (int32_t i = threadIdx.x; i < n_pr; i += kBlock) {
-        const int32_t f = flags[(int64_t)(o0 + p) * n_pr + i];
-        atomicAdd(&scnt[p * 3 + (f < 0 ? 0 : (f > 2 ? 2 : f))], 1);
-      }
-    __syncthreads();
-    if (threadIdx.x < np) {
-      int32_t* cp = counts + (int64_t)(o0 + threadIdx.x) * kCnt;
-      cp[0] = scnt[threadIdx.x * 3];
-      cp[1] = scnt[threadIdx.x * 3 + 1];
-      cp[2] = scnt[threadIdx.x * 3 + 2];
-      for (int k = 3; k < kCnt; ++k) cp[k] = 0;
-    }
-  }
-  // star-table slice {lo, m, half}: nodes lo .. lo+m-1 as (x_k, 10^f_k, ln10 slope_k) + a directory of
-  // nb = 4 half buckets over [x_0, x_m-1]: sdir[j] = last node <= x_0 + j h
-  const int32_t* sl = slices + 3 * (int64_t)blockIdx.x;
-  const int64_t lo = sl[0];
-  const int32_t m = UNISTAR ? 0 : sl[1], half = sl[2];
-  const int32_t nb = 4 * half < kRmDir ? 4 * half : kRmDir;
-  double sx0 = 0.0, inv_h = 0.0;
-  if (m > 0) {
-    for (int i = threadIdx.x; i < m; i += kBlock) {
-      const double x0 = star.x[lo + i], f0 = star.y[lo + i];
-      sx[i] = x0;
-      sF[i] = exp10(f0);                       // star tables have offset 0 (prom_transit_set)
-      sc[i] = i + 1 < m ? ((star.y[lo + i + 1] - f0) / (star.x[lo + i + 1] - x0)) * kLn10 : 0.0;
-    }
-    sx0 = star.x[lo];
-    const double span = star.x[lo + m - 1] - sx0;
-    inv_h = span > 0.0 ? (double)nb / span : 0.0;
-    __syncthreads();
-    for (int j = threadIdx.x; j < nb; j += kBlock) {
-      const double b = sx0 + (double)j * (span / (double)nb);
-      int pos = 0;
-      for (int st = half; st > 0; st >>= 1) pos += (pos + st < m && sx[pos + st] <= b) ? st : 0;
-      sdir[j] = (int16_t)pos;
-    }
-  }
-  // sigma_s at each of this thread's phases (shift_o * lambda, as getLOSopticalDepth_Batch)
-  double sg[kRmP][NSMAX];
-#pragma unroll
-  for (int p = 0; p < kRmP; ++p)
-#pragma unroll
-    for (int s = 0; s < NSMAX; ++s)
-      sg[p][s] = (p < np && s < na) ? sigma_of(tabs[s].shift[o0 + p] * lam, tabs[s]) : 0.0;
-  double fstar_uni = 0.0;
-  if constexpr (UNISTAR) fstar_uni = sigma_of(lam / cshift[0], star);
-  double in[kRmP];
-#pragma unroll
-  for (int p = 0; p < kRmP; ++p) in[p] = 0.0;
-  double out = 0.0, tall = 0.0;
-  for (int32_t c0 = 0; c0 < n_pr; c0 += kRmChunk) {
-    const int nch = n_pr - c0 < kRmChunk ? n_pr - c0 : kRmChunk;
-    __syncthreads();
-    for (int i = threadIdx.x; i < nch; i += kBlock) {
-      sRho[i] = crho[c0 + i];
-      sClv[i] = cclv[c0 + i];
-      sSh[i] = cshift[c0 + i];
-      int32_t am = 0, bm = 0;
-      for (int p = 0; p < np; ++p) {
-        const int32_t f = flags[(int64_t)(o0 + p) * n_pr + c0 + i];
-        am |= (f == 0) << p;
-        bm |= (f == 2) << p;
-      }
-      sMask[i] = am | (bm << 8);
-    }
-    for (int i = threadIdx.x; i < na * np * nch; i += kBlock) {
-      const int sp = i / nch, c = i - sp * nch;     // sp = s * np + p
-      const int s = sp / np, p = sp - s * np;
-      sN[(p * NSMAX + s) * kRmChunk + c] = ncol[((int64_t)s * n_orb + o0 + p) * n_pr + c0 + c];
-    }
-    __syncthreads();
-    for (int cg = 0; cg < nch; cg += kRmGroup) {
-      // F_star for kRmGroup chords at once: their LDS chains (directory -> bracket steps -> node ->
-      // table exp) are independent, so interleaving them hides the LDS latency
-      double fsg[kRmGroup];
-      if constexpr (UNISTAR) {
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) fsg[u] = fstar_uni;
-      } else if (m > 0) {
-        double t[kRmGroup];
-        int k[kRmGroup];
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) {
-          t[u] = lam / sSh[cg + u < nch ? cg + u : nch - 1];
-          const double fj = (t[u] - sx0) * inv_h;
-          const int j = !(fj >= 1.0) ? 1 : (fj >= (double)nb ? nb : (int)fj);
-          k[u] = sdir[j - 1];
-        }
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int u = 0; u < kRmGroup; ++u) k[u] += (k[u] + 1 < m && sx[k[u] + 1] <= t[u]) ? 1 : 0;
-        const double xlast = sx[m - 1];
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) {
-          const double tu = t[u];
-          if (!(tu >= sx0) || tu >= xlast) {
-            // below the table (the slice starts at node 0) / at or beyond the table's last node
-            fsg[u] = tu != tu ? tu : (tu >= xlast ? sF[m - 1] : sF[0]);
-            continue;
-          }
-          int kk = k[u];
-          if (sx[kk + 1] <= tu) {                      // crowded bucket: bisect the rest of the slice
-            int a = kk + 1, b = m - 1;                 // sx[a] <= t < sx[b]
-            while (b - a > 1) {
-              const int mid = (a + b) >> 1;
-              if (sx[mid] <= tu) a = mid; else b = mid;
-            }
-            kk = a;
-          }
-          const double xk = sx[kk];
-          const double arg = sc[kk] * (tu - xk);
-          if (xk == tu) fsg[u] = sF[kk];
-          else if (__builtin_isfinite(arg)) fsg[u] = sF[kk] * exp_tab(arg, sexp);
-          else fsg[u] = sigma_of(tu, star);          // infinite slope (repeated node): np.interp's rules
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) fsg[u] = sigma_of(lam / sSh[cg + u < nch ? cg + u : nch - 1], star);
-      }
-#pragma unroll
-      for (int u = 0; u < kRmGroup; ++u) {
-        const int c = cg + u;
-        if (c >= nch) break;
-        const double fs = fsg[u];
-        const double Fc = sRho[c] * (fs * sClv[c]);
-        out += Fc;
-        const int32_t mk = __builtin_amdgcn_readfirstlane(sMask[c]);
-        if (mk == 0) {
-          tall += Fc;                                  // transparent at every phase of the group
-          continue;
-        }
-#pragma unroll
-        for (int p = 0; p < kRmP; ++p) {
-          if (p >= np) break;
-          if ((mk >> p) & 1) {
-            double tau = 0.0;
-#pragma unroll
-            for (int s = 0; s < NSMAX; ++s)
-              if (s < na) tau += sN[(p * NSMAX + s) * kRmChunk + c] * sg[p][s];
-            if (OCML || !(tau < 700.0 && tau > -700.0)) in[p] += Fc * exp(-tau);
-            else in[p] = acc_exp256(in[p], Fc, tau * kM256Ln2, sexp);
-          } else if (!((mk >> (p + 8)) & 1)) {
-            in[p] += Fc;                               // transparent at this phase
-          }
-        }
-      }
-    }
-  }
-  if (live) {
-#pragma unroll
-    for (int p = 0; p < kRmP; ++p)
-      if (p < np) R[(int64_t)(o0 + p) * n_wav + w] = (in[p] + tall) / out;
-  }
-}
-
-// ---- light-curve band statistics (mainRetrieval.py:76-93) -------------------------------------------
-// One workgroup per phase: strided partial sums / counts / maxima, then a fixed-order LDS tree, so the
-// result does not depend on scheduling.  The max propagates NaN (numpy.max).
-__global__ void __launch_bounds__(kBlock) k_band_stats(const double* __restrict__ R, const double* __restrict__ wav,
-                                                       int64_t n_wav, int32_t n_bands,
-                                                       const double* __restrict__ bounds, double* __restrict__ sum,
-                                                       int64_t* __restrict__ count, double* __restrict__ mx) {
-  __shared__ double ss[kBlock], sm[kBlock];
-  __shared__ int64_t sc[kBlock];
-  const int32_t o = blockIdx.x;
-  const double* b = bounds + (int64_t)o * n_bands * 2;
-  const double* r = R + (int64_t)o * n_wav;
-  double acc = 0.0, m = -__builtin_inf();
-  int64_t cnt = 0;
-  for (int64_t w = threadIdx.x; w < n_wav; w += kBlock) {
-    const double v = r[w], l = wav[w];
-    m = (v > m || v != v || m != m) ? (m != m ? m : v) : m;
-    bool sel = false;
-    for (int32_t k = 0; k < n_bands; ++k) sel = sel || (l >= b[2 * k] && l <= b[2 * k + 1]);
-    if (sel) {
-      acc += v;
-      ++cnt;
-    }
-  }
-  ss[threadIdx.x] = acc;
-  sm[threadIdx.x] = m;
-  sc[threadIdx.x] = cnt;
-  __syncthreads();
-  for (int h = kBlock / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) {
-      ss[threadIdx.x] += ss[threadIdx.x + h];
-      sc[threadIdx.x] += sc[threadIdx.x + h];
-      const double a = sm[threadIdx.x], c = sm[threadIdx.x + h];
-      sm[threadIdx.x] = (a != a || c != c) ? __builtin_nan("") : (c > a ? c : a);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    sum[o] = ss[0];
-    count[o] = sc[0];
-    mx[o] = sm[0];
-  }
-}
-
-void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,
-                       int32_t n_bands, const double* bounds, double* sum, int64_t* count, double* mx) {
-  hipLaunchKernelGGL(k_band_stats, dim3(n_orb), dim3(kBlock), 0, s, R, wav, n_wav, n_bands, bounds, sum, count, mx);
-  PROM_HIP(hipGetLastError());
-}
-
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;
@@ -2968,28 +1899,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   if (tr.star) {
     // 2'. stellar spectrum: one exact chord-order kernel over the flags / columns
     if (ev1) PROM_HIP(hipEventRecord(ev1, s));
-    const SigTabDev star = tr.star_tab;
-    const dim3 g((unsigned)((tr.n_wav + kBlock - 1) / kBlock), (unsigned)((tr.n_orb + kRmP - 1) / kRmP));
-#define PROM_RM(NSV, OC)                                                                                \
-  do {                                                                                                  \
-    if (tr.star_uniform) { PROM_RM2(NSV, OC, true); } else { PROM_RM2(NSV, OC, false); }                 \
-  } while (0)
-#define PROM_RM2(NSV, OC, UV)                                                                           \
-  hipExtLaunchKernelGGL((k_tau_rm<NSV, OC, UV>), g, dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, \
-                        tr.sigtab.as<SigTabDev>(), na, star, tr.rm_slices.as<int32_t>(), tr.wav.as<double>(), \
-                        tr.n_wav, tr.crho.as<double>(), tr.cclv.as<double>(), tr.cshift.as<double>(),     \
-                        rs.flags.as<int32_t>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb,                  \
-                        tr.count_evals ? rs.counts.as<int32_t>() : nullptr, rs.R.as<double>())
-#define PROM_RM_NS(OC)                       \
-  if (na <= 1) PROM_RM(1, OC);               \
-  else if (na == 2) PROM_RM(2, OC);          \
-  else if (na <= 4) PROM_RM(4, OC);          \
-  else PROM_RM(8, OC);
-    PROM_REQUIRE(tr.n_mol == 0 && na <= 8, "transit: the stellar-spectrum path takes <= 8 atomic constituents and no molecules");
-    if (tr.exp_mode) { PROM_RM_NS(false) } else { PROM_RM_NS(true) }
-#undef PROM_RM_NS
-#undef PROM_RM
-#undef PROM_RM2
+    launch_tau_rm(s, tr, rs, na, ev);
     *variant = 40 + (na <= 8 ? na : 0);
     PROM_HIP(hipGetLastError());
     return;
@@ -3061,26 +1971,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   const bool tau_w = !(tr.n_mol > 0) && tr.exp_mode && wpath && tr.window;
   if (ev && !tau_w) PROM_HIP(hipEventRecord(ev[2], s));
   if (tr.n_mol > 0) {
-    PROM_REQUIRE(na <= 4, "transit: at most 4 atomic constituents next to molecular ones");
-    int32_t max_np = 0;
-    for (const auto& m : tr.mslots) max_np = std::max(max_np, m.n_p);
-    const size_t lds = PROM_EXP2_TABLE_N * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
-    PROM_REQUIRE(lds <= 160 * 1024, "transit: molecular tables too large for the LDS staging (n_mol * n_p)");
-#define PROM_TAUM(NSV, EK)                                                                                  \
-  hipLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
-                     max_np, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x,         \
-                     tr.delta_x, tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(), R)
-#define PROM_TAUM_NS(EK)                \
-  switch (na) {                         \
-    case 0: PROM_TAUM(0, EK); break;    \
-    case 1: PROM_TAUM(1, EK); break;    \
-    case 2: PROM_TAUM(2, EK); break;    \
-    case 3: PROM_TAUM(3, EK); break;    \
-    default: PROM_TAUM(4, EK);          \
-  }
-    if (tr.exp_mode) { PROM_TAUM_NS(1) } else { PROM_TAUM_NS(0) }
-#undef PROM_TAUM_NS
-#undef PROM_TAUM
+    launch_tau_mol(s, tr, rs, na, g, ppg);
   } else if (tr.exp_mode && wpath && tr.window) {
 #define PROM_TAUW(NSV, PMV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_tau_w<NSV, UV>), dim3((unsigned)((tr.n_wav + kTW - 1) / kTW), (unsigned)((tr.n_orb + kTP - 1) / kTP)), \
@@ -3148,6 +2039,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 }
 
 }  // namespace prom
+
 
 #ifdef PROM_TRACE
 extern "C" int32_t prom_trace_read(unsigned long long* out, int32_t n, int32_t reset) {
