@@ -32,16 +32,17 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(os.path.join(HERE, f)) <= t for f in SOURCES + HEADERS + ["build.py"])
 
 
-def build(force: bool = False, verbose: bool = False, extra=()) -> str:
-    """One object per translation unit, compiled in parallel, then linked into the shared library."""
-    if not force and up_to_date() and not extra:
+def build(force: bool = False, verbose: bool = False, extra=(), out: str = OUT, objdir: str = OBJDIR) -> str:
+    """One object per translation unit, compiled in parallel, then linked into the shared library
+    (``extra``/``out``/``objdir``: variant builds such as the -DPROM_TRACE library of tools/trace_kernels.py)."""
+    if not force and out == OUT and up_to_date() and not extra:
         return OUT
     from concurrent.futures import ThreadPoolExecutor
-    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(objdir, exist_ok=True)
     cc = hipcc()
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+        obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
         cmd = [cc] + FLAGS + list(extra) + ["-c", os.path.join(HERE, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
@@ -50,12 +51,12 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> str:
 
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+    cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True, cwd=HERE)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -169,6 +169,7 @@ int32_t prom_table_upload(prom_ctx* ctx, int64_t n, const double* x, const doubl
                           double offset, int32_t* table_id) {
   return guarded(ctx, [&] {
     PROM_REQUIRE(n >= 1 && x && log_sigma && table_id, "prom_table_upload: bad arguments");
+    PROM_REQUIRE(n < ((int64_t)1 << 31), "prom_table_upload: more than 2^31 - 1 nodes");
     for (int64_t i = 1; i < n; ++i) PROM_REQUIRE(!(x[i] < x[i - 1]), "prom_table_upload: x must be non-decreasing");
     prom::AtomTable t;
     upload(t.x, x, n, ctx->stream);
@@ -200,6 +201,7 @@ int32_t prom_table_build_voigt(prom_ctx* ctx, int64_t n, const double* x, int32_
                                double offset, int32_t* table_id, double* log_sigma_out) {
   return guarded(ctx, [&] {
     PROM_REQUIRE(n >= 1 && table_id, "prom_table_build_voigt: bad arguments");
+    PROM_REQUIRE(n < ((int64_t)1 << 31), "prom_table_build_voigt: more than 2^31 - 1 nodes");
     for (int64_t i = 1; i < n; ++i) PROM_REQUIRE(!(x[i] < x[i - 1]), "prom_table_build_voigt: x must be non-decreasing");
     prom::AtomTable t;
     voigt_common(ctx, n, x, n_lines, line_wavelength, line_gamma, line_coef, t.x);
@@ -528,7 +530,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         const double inv = (c > 0.0 && std::isfinite(c)) ? bound : 0.0;
         st.push_back({tb.x.as<double>(), tb.y.as<double>(), tb.n, tb.offset,
                       tr.shift.as<double>() + (int64_t)t.scenario * n_orb, tb.dir.as<int32_t>(), tb.n_dir, 0,
-                      tb.dir_x0, tb.dir_inv_h, std::isfinite(c) ? c : 0.0, inv, t.chi});
+                      tb.dir_x0, tb.dir_inv_h, std::isfinite(c) ? c : 0.0, inv, t.chi, tb.hx.front(), tb.hx.back()});
       }
       // species merging: one scenario carries every atomic constituent (and there are >= 2 of them)
       int32_t sc0 = -1;
@@ -583,7 +585,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       const prom::AtomTable& sb = ctx->tables[pb->star_table];
       PROM_REQUIRE(sb.offset == 0.0, "transit: the star table must have offset 0 (n_interp_log(..., 0.0))");
       tr.star_tab = prom::SigTabDev{sb.x.as<double>(), sb.y.as<double>(), sb.n, sb.offset, nullptr,
-                                    sb.dir.as<int32_t>(), sb.n_dir, 0, sb.dir_x0, sb.dir_inv_h, 0.0, 0.0};
+                                    sb.dir.as<int32_t>(), sb.n_dir, 0, sb.dir_x0, sb.dir_inv_h, 0.0, 0.0, 0.0,
+                                    sb.hx.front(), sb.hx.back()};
       upload(tr.crho, pb->chord_rho, tr.n_pr, s);
       upload(tr.cclv, pb->chord_clv, tr.n_pr, s);
       upload(tr.cshift, pb->chord_star_shift, tr.n_pr, s);
@@ -675,16 +678,16 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
                        std::max(prom::n_tail_moments(n_atoms), prom::n_tail_moments(1)));   // merged species: 1
       }
       rs.evals.ensure(sizeof(unsigned long long) * 64);
-      rs.sig.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * tr.n_wav);
-      rs.zfl.ensure((size_t)tr.n_wav);
+      // resampled cross-sections: one row per phase when the Doppler factors differ between phases
+      const int64_t sig_rows = tr.uniform_shift ? 1 : n_orb;
+      rs.sig.ensure(sizeof(double) * sig_rows * std::max<int64_t>(n_atoms, 1) * tr.n_wav);
+      rs.zfl.ensure((size_t)(sig_rows * tr.n_wav));
       const int64_t n_wtiles = (tr.n_wav + 127) / 128;
-      rs.tq.ensure(sizeof(float) * 2 * n_wtiles);
-      rs.win.ensure(sizeof(int32_t) * 2 * n_orb * n_wtiles);
-      rs.hlist.ensure(sizeof(int32_t) * 4 * n_orb * n_wtiles);
+      rs.tq.ensure(sizeof(float) * 4 * sig_rows * n_wtiles);
+
+      rs.hlist.ensure(sizeof(int32_t) * 4 * 2 * n_orb * 2 * n_wtiles);   // small and big lists, <= 1 per half tile
       rs.hcnt.ensure(sizeof(int32_t) * 4);
-      if (n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && n_mol == 0)
-        rs.trec.ensure(sizeof(double) * n_orb * n_wtiles *
-                       (2 + std::max(prom::n_tail_moments(n_atoms), prom::n_tail_moments(1))));
+      rs.trec.ensure(sizeof(int32_t) * 4 * n_orb * n_wtiles);   // {h, t, flags, 0} per (phase, tile)
       tr.taup_resident = 0;
       rs.tsum.ensure(sizeof(double) * n_orb);
       rs.fsum.ensure(sizeof(double) * n_orb);

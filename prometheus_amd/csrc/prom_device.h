@@ -14,7 +14,8 @@ namespace prom {
 constexpr int kBlock = 256;
 constexpr int kTW = 128;   // k_tau_w: wavelengths per workgroup (one window tile)
 constexpr int kTP = 4;     // k_tau_w: phases per workgroup (one per wavefront)
-constexpr int kHeavy = 8;  // k_tau_p: windows longer than this go to the heavy wavefronts
+constexpr int kHeavy = 8;  // k_tau_p: tiles whose window is longer than this become heavy entries
+constexpr int kChunk = 64; // k_tau_p: records per chunk of a heavy entry (longer entries: one workgroup)
 
 // Optional in-kernel timing (build with -DPROM_TRACE, tools/trace_kernels.py): wall-clock stamps
 // (100 MHz) of workgroup 0's steps and per-wavefront cycle counters in a device array.
@@ -123,6 +124,54 @@ __device__ __forceinline__ double sigma_of(double t, const SigTabDev& tb) {
     }
   }
   return exp10(v) - tb.offset;
+}
+
+// sigma_of for NS tables at once (the species of one wavelength): every table's directory load goes
+// out first, then every table's 4-node window (x and f, 64 B per target: the resampling kernel is bound
+// by the vector L1's bytes, so numpy.interp's slope is divided here rather than fetched), so a thread
+// waits for two dependent round trips instead of 2 NS.  Same bracket rules and arithmetic as sigma_of, so
+// the results are identical bit for bit.
+template <int NS>
+__device__ __forceinline__ void sigma_multi(const SigTabs4& tabv, const double (&t)[NS], double (&v)[NS]) {
+  int32_t d[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const SigTabDev& tb = tabv.t[s];
+    const double fj = (t[s] - tb.dir_x0) * tb.dir_inv_h;
+    const int32_t j = fj >= 0.0 ? (fj >= (double)(tb.n_dir - 1) ? tb.n_dir - 1 : (int32_t)fj) : 0;
+    d[s] = tb.dir[j];
+  }
+  struct Win { double x0, x1, x2, x3, f0, f1, f2, f3; } u[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const SigTabDev& tb = tabv.t[s];
+    const int32_t n = (int32_t)tb.n;
+    int32_t l = d[s] - 1;
+    l = l > n - 2 ? n - 2 : l;
+    l = l < 0 ? 0 : l;   // (n == 1: 0)
+    const int32_t l1 = l + 1 < n ? l + 1 : n - 1, l2 = l + 2 < n ? l + 2 : n - 1, l3 = l + 3 < n ? l + 3 : n - 1;
+    u[s].x0 = tb.x[l]; u[s].x1 = tb.x[l1]; u[s].x2 = tb.x[l2]; u[s].x3 = tb.x[l3];
+    u[s].f0 = tb.y[l]; u[s].f1 = tb.y[l1]; u[s].f2 = tb.y[l2]; u[s].f3 = tb.y[l3];
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const SigTabDev& tb = tabv.t[s];
+    const double tt = t[s];
+    const bool found = tb.n >= 2 && tt >= tb.xfirst && tt < tb.xlast && u[s].x0 <= tt && tt < u[s].x3;
+    const bool c0 = tt < u[s].x1, c1 = tt < u[s].x2;
+    const double xa = c0 ? u[s].x0 : (c1 ? u[s].x1 : u[s].x2);
+    const double xb = c0 ? u[s].x1 : (c1 ? u[s].x2 : u[s].x3);
+    const double fa = c0 ? u[s].f0 : (c1 ? u[s].f1 : u[s].f2);
+    const double fb = c0 ? u[s].f1 : (c1 ? u[s].f2 : u[s].f3);
+    double r;
+    if (xa == tt) r = fa;
+    else {
+      const double slope = (fb - fa) / (xb - xa);
+      r = slope * (tt - xa) + fa;
+    }
+    if (found && r == r) v[s] = exp10(r) - tb.offset;
+    else v[s] = sigma_of(tt, tb);
+  }
 }
 
 // ---- wavefront scans on DPP row shifts + cross-row readlanes (no LDS traffic, no bpermute) ----

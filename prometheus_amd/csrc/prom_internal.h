@@ -115,6 +115,7 @@ struct SigTabDev {
   double ncoef;          // c_s: column normalisation of the windowed integration (n = c_s N <= 1)
   double nscale;         // 1 / c_s (0 when c_s == 0)
   double chi;            // the constituent's mixing ratio (species merging: Y = sum_s chi_s sigma_s)
+  double xfirst, xlast;  // x[0], x[n - 1] (range test without a dependent load)
 };
 
 // Per molecular slot of a transit problem.
@@ -185,15 +186,16 @@ struct RunSlot {
   DevBuf wenv;                              // [n_orb][2][kEnvN] int32 threshold -> record tables
   DevBuf wmom;                              // [n_orb][n_pr + 1][K] suffix tail moments
   DevBuf evals;                             // [64] uint64 exp-evaluation counters (stats runs)
-  DevBuf sig;                               // no orbital Doppler shift: sigma_s(lambda_w) [n_atoms][n_wav]
-  DevBuf zfl;                               // merged species: some chi_s sigma_s(lambda_w) not > 0 [n_wav] uint8
-  DevBuf tq;                                // no orbital Doppler shift: Q range per 128-lambda tile [n_tiles] float2
-  DevBuf win;                               // ... and each tile's tau window {h, t} per phase [n_orb][n_tiles] int2
-  DevBuf trec;                              // ... tile records {h, t}, {flags, 0}, tail moments at t
-                                            //     [n_orb][n_tiles][2 + K] (k_order, for k_tau_p)
-  DevBuf hlist;                             // ... (tile, phase) units with long windows
-                                            //     {tile, h, t, flags | phase << 8} [n_orb * n_tiles] int4
-  DevBuf hcnt;                              // ... their count (int32; zeroed by k_columns8)
+  DevBuf sig;                               // resampled sigma_s(shift lambda_w) [sig rows][n_atoms or 1][n_wav]
+                                            //     (one row, or one per phase with orbital Doppler shift)
+  DevBuf zfl;                               // merged species: some chi_s sigma_s not > 0 [sig rows][n_wav] uint8
+  DevBuf tq;                                // resampled path: Q ranges of the two halves of each 128-lambda
+                                            //     tile [sig rows][n_tiles] float4 (k_columns8)
+  DevBuf trec;                              // ... each tile's tau window and flags {h, t, flags, 0} per phase
+                                            //     [n_orb][n_tiles] int4 (k_order)
+  DevBuf hlist;                             // ... heavy entries {half tile, h, t, flags | phase << 8}: small
+                                            //     list [n_orb * 2 n_tiles], then big list [n_orb * 2 n_tiles] int4
+  DevBuf hcnt;                              // ... their counts (int32 small, big; zeroed by k_columns8)
   DevBuf R;                                 // [n_orb][n_wav]
 };
 

@@ -136,9 +136,10 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
                                  const double* __restrict__ moon_R, const double* __restrict__ sig_max,
                                  double cull, double* __restrict__ ncol, int32_t* __restrict__ flags,
                                  const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
-                                 double* __restrict__ sig, float2* __restrict__ tq, int32_t merge_sp,
-                                 double nscale_m, int32_t* __restrict__ hcnt, uint8_t* __restrict__ zfl) {
-  if (hcnt && blockIdx.x == 0 && threadIdx.x == 0) hcnt[0] = 0;   // k_order's heavy-unit counter
+                                 double* __restrict__ sig, float4* __restrict__ tq, int32_t merge_sp,
+                                 double nscale_m, int32_t* __restrict__ hcnt, uint8_t* __restrict__ zfl,
+                                 int32_t sig_rows) {
+  if (hcnt && blockIdx.x == 0 && threadIdx.x < 2) hcnt[threadIdx.x] = 0;   // k_order's heavy-entry counters
   // Eight lanes per chord; lane j holds samples j, j + 8, ..., j + 8 (SPL - 1).  That is numpy's
   // pairwise_sum layout (loops_utils.h.src) for 8 <= n_x < 128: lane j accumulates r[j] = a[j] +
   // a[j+8] + ... sequentially, the eight partial sums combine as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
@@ -146,17 +147,39 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
   PROM_CLK(tk0);
   constexpr int G = kBlock / 8;         // chords per workgroup
   if constexpr (NSIG > 0) {
-    // trailing workgroups: sigma_s(shift_s lambda_w) for problems without orbital Doppler shift
+    // trailing workgroups: sigma_s(shift_{s,o} lambda_w), once per wavelength (sig_rows == 1: no orbital
+    // Doppler shift) or once per (phase, wavelength) (sig_rows == n_orb): row r of sig is phase r's
+    // chord workgroups [0, cb), padding to cb8 (a multiple of 8), then the sigma workgroups
     const unsigned cb = (unsigned)(((int64_t)n_orb * n_pr + G - 1) / G);
-    if (blockIdx.x >= cb) {
-      // ... and each kTW-wavelength tile's range of Q = sum_s max(sigma_s / c_s, 0) (float, widened by
-      // 2^-20; {-1, 0} when Q is not finite), from which k_order picks the tile's tau window.  Lanes
-      // past n_wav take the last wavelength, as k_tau_w's do.
-      __shared__ float tqs[kBlock / 64][2];
-      __shared__ int32_t tqb[kBlock / 64];
-      const int64_t w = (int64_t)(blockIdx.x - cb) * kBlock + threadIdx.x;
+    const unsigned cb8 = (cb + 7u) & ~7u;
+    if (blockIdx.x >= cb && blockIdx.x < cb8) return;
+    if (blockIdx.x >= cb8) {
+      // ... and each 64-wavelength half tile's range of Q = sum_s max(sigma_s / c_s, 0) (float, widened by
+      // 2^-20; {-1, 0} when Q is not finite), from which k_order picks the tau windows.  Lanes past
+      // n_wav take the last wavelength, as the tau kernels' do.
+      // One thread per (row, wavelength): sigma_multi issues the directory loads of all species together,
+      // then their node windows.  XCD-aware order: workgroups are dealt to the 8 XCDs round robin, so
+      // workgroup b takes item (b % 8) * per + b / 8 of the (wavelength block, row) items, rows fastest:
+      // each XCD walks one contiguous wavelength range for all phases and its L2 keeps that range of the
+      // tables.
+      const int lane = threadIdx.x & 63;
+      const int64_t nwb = (n_wav + kBlock - 1) / kBlock;   // sigma workgroups per row
+      const int64_t nb = nwb * sig_rows;
+      const int64_t per = (nb + 7) / 8;
+      const int64_t bp = (int64_t)(blockIdx.x - cb8);
+      const int64_t item = (bp & 7) * per + (bp >> 3);
+      if (item >= nb) return;
+      const int64_t wb = item / sig_rows;
+      const int32_t orow = (int32_t)(item - wb * sig_rows);
+      const int64_t w = wb * kBlock + threadIdx.x;
       const bool live = w < n_wav;
       const double lam = wav[live ? w : n_wav - 1];
+      const int32_t nse = merge_sp ? 1 : NSIG;           // sigma arrays per row
+      double tg[NSIG], sv[NSIG];
+#pragma unroll
+      for (int s = 0; s < NSIG; ++s) tg[s] = tabv.t[s].shift[orow] * lam;
+      sigma_multi<NSIG>(tabv, tg, sv);
+      double* srow = sig + (int64_t)orow * nse * n_wav;
       double Q = 0.0;
       if (merge_sp) {
         // species merging: the effective absorber's cross-section Y = sum_s chi_s sigma_s
@@ -164,22 +187,21 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
         bool z = false;   // some chi_s sigma_s not > 0: an infinite column gives NaN there (inf * 0)
 #pragma unroll
         for (int s = 0; s < NSIG; ++s) {
-          const double v = tabv.t[s].chi * sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
+          const double v = tabv.t[s].chi * sv[s];
           z = z || !(v > 0.0);
           Y += v;
         }
         if (live) {
-          sig[w] = Y;
-          zfl[w] = z ? 1 : 0;
+          srow[w] = Y;
+          zfl[(int64_t)orow * n_wav + w] = z ? 1 : 0;
         }
         const double qs = Y * nscale_m;
         Q = qs > 0.0 ? qs : 0.0;
       } else {
 #pragma unroll
         for (int s = 0; s < NSIG; ++s) {
-          const double sv = sigma_of(tabv.t[s].shift[0] * lam, tabv.t[s]);
-          if (live) sig[(int64_t)s * n_wav + w] = sv;
-          const double qs = sv * tabv.t[s].nscale;
+          if (live) srow[(int64_t)s * n_wav + w] = sv[s];
+          const double qs = sv[s] * tabv.t[s].nscale;
           Q += qs > 0.0 ? qs : 0.0;
         }
       }
@@ -190,17 +212,11 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
         ql = fminf(ql, __shfl_xor(ql, off, 64));
       }
       const bool bad = __ballot(!(Q <= 1.0e100)) != 0ull;
-      const int wv = threadIdx.x >> 6;
-      if ((threadIdx.x & 63) == 0) { tqs[wv][0] = ql; tqs[wv][1] = qh; tqb[wv] = bad ? 1 : 0; }
-      __syncthreads();
-      static_assert(kBlock == 2 * kTW, "two window tiles per sigma workgroup");
-      if (threadIdx.x < 2) {
-        const int a = 2 * threadIdx.x;
-        const int64_t tl = 2 * (int64_t)(blockIdx.x - cb) + threadIdx.x;
-        if (tl * kTW < n_wav)
-          tq[tl] = (tqb[a] | tqb[a + 1]) ? make_float2(-1.0f, 0.0f)
-                                         : make_float2(fminf(tqs[a][0], tqs[a + 1][0]), fmaxf(tqs[a][1], tqs[a + 1][1]));
-      }
+      const int64_t n_halves = 2 * ((n_wav + kTW - 1) / kTW);
+      const int64_t hw = wb * (kBlock / 64) + (threadIdx.x >> 6);
+      if (lane == 0 && hw < n_halves)
+        reinterpret_cast<float2*>(tq)[(int64_t)orow * n_halves + hw] =
+            bad ? make_float2(-1.0f, 0.0f) : make_float2(ql, qh);
       return;
     }
   }
@@ -537,9 +553,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
                                                    double* __restrict__ fsum,
                                                    int32_t* __restrict__ wenv,
                                                    double* __restrict__ wmom,
-                                                   const float2* __restrict__ tq, int32_t n_tiles,
-                                                   int2* __restrict__ win, int4* __restrict__ hlist,
-                                                   int32_t* __restrict__ hcnt, double* __restrict__ trec) {
+                                                   const float4* __restrict__ tq, int32_t tq_rows,
+                                                   int32_t n_tiles, int64_t n_wav,
+                                                   int4* __restrict__ trec, int4* __restrict__ hlist, int64_t hcap,
+                                                   int32_t* __restrict__ hcnt) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
@@ -556,11 +573,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   __shared__ double pd_[NW][2];
   __shared__ double pm_[NW][K + 2];
   __shared__ int32_t pg_[NW];
-  __shared__ int32_t sHc[2];                     // step 7: heavy units staged in LDS, their global base
-  // step 7 reads the tail moments at every tile's window end: with one effective species they are
-  // also kept in LDS (rows 0 .. G) when they fit, instead of a dependent HBM read per tile
-  constexpr int MOMC = NS == 1 ? 4096 : 1;
-  __shared__ double sMom[MOMC];
+  __shared__ int32_t sHc[4];                     // step 7: heavy entries staged in LDS (small, big), global bases
   const int32_t o = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int32_t* fl = flags + (int64_t)o * n_pr;
@@ -572,14 +585,13 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
 
   PROM_TS(o * 16 + 0);
   constexpr int TQP = 4;   // tiles per thread whose Q range is loaded now, for step 7
-  float2 tqv[TQP];
+  float4 tqv[TQP];
 #pragma unroll
   for (int k = 0; k < TQP; ++k) {
     const int32_t tl = tid + k * kWBlock;
-    tqv[k] = (tq && tl < n_tiles) ? tq[tl] : make_float2(0.0f, 0.0f);
+    tqv[k] = (tq && tl < n_tiles) ? tq[(tq_rows > 1 ? (int64_t)o * n_tiles : 0) + tl] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
-  bool mcache = false;
-  if (tid == 0) sHc[0] = 0;   // (barriers of steps 1-6 order it before step 7)
+  if (tid < 2) sHc[tid] = 0;   // (barriers of steps 1-6 order it before step 7)
   for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }
   // ---- 1. load, classify, keys, combined scan/reduction
   double fs = 0.0, ts = 0.0;
@@ -723,20 +735,67 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       if (has1) skey[r1] = k1;
       __syncthreads();
     } else {
-      int32_t P = 1;
+      // merge sort in place (keys are unique): thread t owns positions [8t, 8t + 8); its eight keys are
+      // sorted in registers, then runs of L = 8, 16, .. P/2 merge pairwise: a key's position in the
+      // merged run is its index in its own run plus the number of smaller keys in the partner run (a
+      // branchless binary search in LDS, the eight keys interleaved); 9 passes of 2 barriers at P = 4096
+      constexpr int KP = kWinMax / kWBlock;
+      static_assert(KP == 8, "eight keys per thread");
+      int32_t P = 8;
       while (P < n) P <<= 1;
-      for (int32_t i = n + tid; i < P; i += kWBlock) skey[i] = ~0ull;
+      // padding keys: unique (the merge ranks assume it) and above every real key (<= 0xffc0... | pos)
+      for (int32_t i = n + tid; i < P; i += kWBlock) skey[i] = 0xffffffffffff0000ull | (unsigned)i;
       __syncthreads();
-      for (int32_t size = 2; size <= P; size <<= 1) {
-        for (int32_t st = size >> 1; st > 0; st >>= 1) {
-          for (int32_t t = tid; t < P / 2; t += kWBlock) {
-            const int32_t i = 2 * t - (t & (st - 1));
-            const int32_t jj = i + st;
-            const bool up = (i & size) == 0;
-            const unsigned long long a = skey[i], b = skey[jj];
-            if ((a > b) == up) { skey[i] = b; skey[jj] = a; }
+      const int32_t p0 = KP * tid;
+      const bool own = p0 < P;
+      unsigned long long k[KP];
+#pragma unroll
+      for (int q = 0; q < KP; ++q) k[q] = own ? skey[p0 + q] : ~0ull;
+      // Batcher's odd-even merge sort network for 8 keys (19 compare-exchanges)
+      auto cx = [&](int a, int b) {
+        const unsigned long long x = k[a], y = k[b];
+        k[a] = x < y ? x : y;
+        k[b] = x < y ? y : x;
+      };
+      cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
+      cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
+      cx(1, 2); cx(5, 6);
+      cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
+      cx(2, 4); cx(3, 5);
+      cx(1, 2); cx(3, 4); cx(5, 6);
+      __syncthreads();   // every chunk loaded before any sorted chunk is stored
+      if (own) {
+#pragma unroll
+        for (int q = 0; q < KP; ++q) skey[p0 + q] = k[q];
+      }
+      __syncthreads();
+      for (int32_t L = KP; L < P; L <<= 1) {
+        const int32_t base = p0 & ~(2 * L - 1);
+        const bool left = (p0 & L) == 0;
+        const int32_t ps = left ? base + L : base;           // partner run [ps, ps + L)
+        const int32_t idx = p0 - (left ? base : base + L);   // index of k[0] in its own run
+        int32_t lo[KP];
+#pragma unroll
+        for (int q = 0; q < KP; ++q) lo[q] = 0;
+        if (own) {
+          for (int32_t st = L >> 1; st > 0; st >>= 1) {
+#pragma unroll
+            for (int q = 0; q < KP; ++q)
+              if (skey[ps + lo[q] + st - 1] < k[q]) lo[q] += st;
           }
-          __syncthreads();
+#pragma unroll
+          for (int q = 0; q < KP; ++q)
+            if (lo[q] == L - 1 && skey[ps + L - 1] < k[q]) lo[q] = L;
+        }
+        __syncthreads();   // every search done before any key moves
+        if (own) {
+#pragma unroll
+          for (int q = 0; q < KP; ++q) skey[base + idx + q + lo[q]] = k[q];
+        }
+        __syncthreads();
+        if (own) {
+#pragma unroll
+          for (int q = 0; q < KP; ++q) k[q] = skey[p0 + q];
         }
       }
     }
@@ -844,7 +903,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       gtot += pg_[w];
     }
     G = gtot;
-    mcache = window && NS == 1 && (G + 1) * K <= MOMC;
     PROM_TS(o * 16 + 3);
     // ---- 6. records, envelopes, moments (group heads), in the sorted order
     double* mo = mrecs + (int64_t)o * n_pr * ST;
@@ -900,7 +958,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           for (int m = 0; m < K; ++m) {
             const double v = M.c[m] * msum[m];
             mm[(int64_t)gi * K + m] = v;
-            if (mcache) sMom[gi * K + m] = v;
           }
         }
       }
@@ -908,7 +965,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     if (window) {
       if (tid < K) {
         mm[(int64_t)G * K + tid] = 0.0;
-        if (mcache) sMom[G * K + tid] = 0.0;
       }
       __syncthreads();
       PROM_TS(o * 16 + 4);
@@ -947,44 +1003,57 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     }
   }
   if (tq) {
-    // ---- 7. tau window [h, t) of every wavelength tile for this phase (no orbital Doppler shift:
-    //         Q per tile from k_columns8), exactly as k_tau_w would pick it from the tables.  With
-    //         trec (the planned tau kernel): the tile record {h, t, flags, tail moments at t}, and the
-    //         tiles whose window holds more than kHeavy records go to the heavy-unit list (one global
-    //         counter, zeroed by k_columns8; any order)
+    // ---- 7. tau window [h, t) of every wavelength tile for this phase (Q ranges per half tile from
+    //         k_columns8: one row per phase with orbital Doppler shift, else one shared row), exactly as
+    //         k_tau_w would pick it from the tables for the tile's union Q range.  With trec (the planned
+    //         tau kernel): the tile record {h, t, flags, tail moments at t}; a tile whose window holds more
+    //         than kHeavy records instead becomes two heavy entries, one per live 64-wavelength half, each
+    //         with the window of its own Q range: halves of at most kChunk records go to the small list
+    //         (one wavefront each), longer ones to the big list (one workgroup each, chunks of kChunk).
+    //         Two global counters (zeroed by k_columns8); list order is free.
     __syncthreads();   // moments (step 6) visible to the whole workgroup
     PROM_TS(o * 16 + 5);
     const bool wtab = sorted && window;
     const int32_t pfl = (sorted ? 1 : 0) | (nnf ? 4 : 0);
-    constexpr int TRS = 2 + K;
-    constexpr int HCAP = (int)(sizeof(skey) / sizeof(int4));
-    int4* hbuf = reinterpret_cast<int4*>(skey);
-    auto tile_window = [&](int32_t tl, float2 q) {
-      int32_t h = 0, t = sorted ? G : nact;
-      if (wtab && q.x >= 0.0f) {
-        const int vt = env_floor((float)tail_eps<NS>() / q.y * (1.0f - 0x1p-20f));
-        const int vh = env_floor((float)kTauSat / q.x * (1.0f + 0x1p-20f));
+    constexpr int HCAP = (int)(sizeof(skey) / sizeof(int4)) / 2;   // staged entries per list
+    int4* hbuf = reinterpret_cast<int4*>(skey);                    // [0, HCAP) small, [HCAP, 2 HCAP) big
+    const float4* tqo = tq + (tq_rows > 1 ? (int64_t)o * n_tiles : 0);
+    const int32_t t_all = sorted ? G : nact;
+    auto window_of = [&](float ql, float qh, int32_t* hp, int32_t* tp) {
+      int32_t h = 0, t = t_all;
+      if (wtab && ql >= 0.0f) {
+        const int vt = env_floor((float)tail_eps<NS>() / qh * (1.0f - 0x1p-20f));
+        const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
         t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : hB[vt - kEnvVmin]);
         h = vh >= kEnvVmax ? 0 : hA[vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin];
       }
-      h = h < t ? h : t;
-      win[(int64_t)o * n_tiles + tl] = make_int2(h, t);
-      if (trec) {
-        const int32_t fl = pfl | ((wtab && t < G) ? 2 : 0);
-        double* r = trec + ((int64_t)o * n_tiles + tl) * TRS;
-        r[0] = __builtin_bit_cast(double, make_int2(h, t));
-        r[1] = __builtin_bit_cast(double, make_int2(fl, 0));
-        if (fl & 2) {
-          const double* mp = mcache ? sMom + t * K : wmom + ((int64_t)o * (n_pr + 1) + t) * K;
-#pragma unroll
-          for (int k = 0; k < K; ++k) r[2 + k] = mp[k];
-        }
+      *hp = h < t ? h : t;
+      *tp = t;
+    };
+    auto tile_window = [&](int32_t tl, float4 q) {
+      const bool live1 = (int64_t)tl * kTW + 64 < n_wav;   // the second half holds wavelengths
+      const bool bad = q.x < 0.0f || (live1 && q.z < 0.0f);
+      const float ql = bad ? -1.0f : (live1 ? fminf(q.x, q.z) : q.x);
+      const float qh = bad ? 0.0f : (live1 ? fmaxf(q.y, q.w) : q.y);
+      int32_t h, t;
+      window_of(ql, qh, &h, &t);
+      const int32_t fl = pfl | ((wtab && t < G) ? 2 : 0);
+      trec[(int64_t)o * n_tiles + tl] = make_int4(h, t, fl, 0);
+      if (hlist) {
         if (!nnf && t - h > kHeavy) {
-          // staged in LDS over the sort keys (free after step 6); one global append per workgroup
-          const int4 e = make_int4(tl, h, t, fl | (o << 8));
-          const int32_t k = atomicAdd(&sHc[0], 1);
-          if (k < HCAP) hbuf[k] = e;
-          else hlist[atomicAdd(hcnt, 1)] = e;
+          // staged in LDS over the sort keys (free after step 6); one global append per list and workgroup
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            if (hf == 1 && !live1) continue;
+            int32_t hh, tt;
+            window_of(hf ? q.z : q.x, hf ? q.w : q.y, &hh, &tt);
+            const int32_t ff = pfl | ((wtab && tt < G) ? 2 : 0);
+            const int4 e = make_int4(2 * tl + hf, hh, tt, ff | (o << 8));
+            const int big = tt - hh > kChunk ? 1 : 0;
+            const int32_t k = atomicAdd(&sHc[big], 1);
+            if (k < HCAP) hbuf[big * HCAP + k] = e;
+            else hlist[(int64_t)big * hcap + atomicAdd(&hcnt[big], 1)] = e;
+          }
         }
       }
     };
@@ -993,13 +1062,16 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       const int32_t tl = tid + k * kWBlock;
       if (tl < n_tiles) tile_window(tl, tqv[k]);
     }
-    for (int32_t tl = tid + TQP * kWBlock; tl < n_tiles; tl += kWBlock) tile_window(tl, tq[tl]);
-    if (trec) {
+    for (int32_t tl = tid + TQP * kWBlock; tl < n_tiles; tl += kWBlock) tile_window(tl, tqo[tl]);
+    if (hlist) {
       __syncthreads();
-      const int32_t nh = sHc[0] < HCAP ? sHc[0] : HCAP;
-      if (tid == 0) sHc[1] = nh > 0 ? atomicAdd(hcnt, nh) : 0;
+      const int32_t ns = sHc[0] < HCAP ? sHc[0] : HCAP;
+      const int32_t nb = sHc[1] < HCAP ? sHc[1] : HCAP;
+      if (tid == 0) sHc[2] = ns > 0 ? atomicAdd(&hcnt[0], ns) : 0;
+      if (tid == 64) sHc[3] = nb > 0 ? atomicAdd(&hcnt[1], nb) : 0;
       __syncthreads();
-      for (int32_t i = tid; i < nh; i += kWBlock) hlist[sHc[1] + i] = hbuf[i];
+      for (int32_t i = tid; i < ns; i += kWBlock) hlist[sHc[2] + i] = hbuf[i];
+      for (int32_t i = tid; i < nb; i += kWBlock) hlist[hcap + sHc[3] + i] = hbuf[HCAP + i];
     }
   }
   if (tid == 0) {
@@ -1241,8 +1313,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
                                                   const int32_t* __restrict__ wenv,
                                                   const double* __restrict__ wmom,
                                                   const double* __restrict__ sig,
-                                                  const int2* __restrict__ win, int32_t n_tiles,
-                                                  const uint8_t* __restrict__ zfl,
+                                                  const int4* __restrict__ trec, int32_t n_tiles,
+                                                  const uint8_t* __restrict__ zfl, int32_t sig_rows,
                                                   unsigned long long* __restrict__ evals,
                                                   double* __restrict__ R) {
   constexpr Monos<NS> M{};
@@ -1274,8 +1346,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
     live[j] = w < n_wav;
     lam[j] = wav[live[j] ? w : n_wav - 1];
   }
-  int2 hw = make_int2(0, 0);
-  if constexpr (UNI) hw = win[(int64_t)o * n_tiles + blockIdx.x];   // window chosen by k_order
+  int4 hw = make_int4(0, 0, 0, 0);
+  if constexpr (UNI) hw = trec[(int64_t)o * n_tiles + blockIdx.x];   // window chosen by k_order
   const int32_t* cp = counts + o * kCnt;
   const int32_t cA = cp[0], cG = cp[4];
   const int32_t cF = (cp[5] ? 1 : 0) | (cp[6] ? 2 : 0) | (cp[3] ? 4 : 0);
@@ -1283,7 +1355,11 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
   // ---- 2.-3. sigma
   double sg[kLPT][NS];
   if constexpr (UNI) {
-    // resampled by the trailing workgroups of k_columns8
+    // resampled by the trailing workgroups of k_columns8 (one row per phase with orbital Doppler shift)
+    if (sig_rows > 1) {
+      sig += (int64_t)o * NS * n_wav;
+      if (zfl) zfl += (int64_t)o * n_wav;
+    }
 #pragma unroll
     for (int j = 0; j < kLPT; ++j) {
       const int64_t w = tile + 64 * j + lane;
@@ -1470,29 +1546,74 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
 #endif
 }
 
-// ---- planned tau integration (no orbital Doppler shift) ------------------------------------------------
-// k_tau_w gives every (128-wavelength tile, phase) one wavefront: a run is ~1.6 rounds of resident
-// wavefronts and its end is set by the few windows at line cores (up to ~70 records, 30x the median)
-// that start in the second round.  k_tau_p instead:
-//   - static wavefronts, one per (tile, group of 4 phases): every phase whose window holds at most
-//     kHeavy records (nearly all) is integrated there; the records of the group's phases travel as one
-//     packed load;
-//   - heavy wavefronts, first in the grid: the (tile, phase) units with longer windows, which k_order
-//     lists per phase (hlist / hcnt), each split into two items of 64 wavelengths (one per lane).
-// Each (phase, wavelength) is integrated with k_tau_w's operations in k_tau_w's order, whichever
-// wavefront takes it, so R does not depend on the split.
+// ---- planned tau integration ---------------------------------------------------------------------------
+// k_tau_w gives every (128-wavelength tile, phase) one wavefront: the end of a run is set by the few
+// windows at line cores, which hold up to ~1,000 records (Doppler-shifted multi-line spectra) against a
+// median of zero.  k_tau_p instead takes k_order's plan:
+//   - big entries (a 64-wavelength half tile of one phase whose window holds more than kChunk records):
+//     one workgroup each; its four wavefronts take the entry's chunks of kChunk records round robin,
+//     each summing its chunks in order, and the four partial sums are added in wavefront order;
+//   - small entries (halves with at most kChunk records): one wavefront each;
+//   - static wavefronts, one per (tile, group of 4 phases): every phase whose tile window holds at most
+//     kHeavy records (nearly all wavelengths); the records of the group's phases travel as one packed load.
+// Every workgroup of the grid first takes its share of the big entries (round robin), then each
+// wavefront its share of the small entries, then its static unit, so long windows spread over the whole
+// chip.  The result of a (phase, wavelength) depends only on its tile's and half's windows, never on the
+// grid: R is identical for any sharding of the wavelength axis.
+// PH: sigma has one row per phase (orbital Doppler shift), else one row for all phases.
 
-// The integration of one phase at LPL wavelengths per lane: records [h, t) staged through this
-// wavefront's LDS slice `sr` in chunks of 64 (the first chunk `nx` already loaded), the tail polynomial
-// from the moments mm, the transparent sum tf -- k_tau_w's operations in k_tau_w's order.
+// Records [c, c + 64) for c = 64 first, 64 (first + step), ... < n of one entry, staged through this
+// wavefront's LDS slice `sr` (double buffered; `nx` holds the first chunk, already loaded), accumulated in
+// order into acc: acc += F e^{-tau} at LPL wavelengths per lane.
+template <int NS, int LPL>
+__device__ __forceinline__ void tau_records(const double (&sy)[LPL][NS], const double* __restrict__ src, int32_t n,
+                                            int32_t first, int32_t step, double (&nx)[1 + NS], int lane,
+                                            double* __restrict__ sr, const double* __restrict__ sexp,
+                                            double (&acc)[LPL]) {
+  constexpr int ST = 1 + NS;
+  const int32_t nel = n * ST;
+  int32_t it = 0;
+  for (int32_t c0 = 64 * first; c0 < n; c0 += 64 * step, ++it) {
+    const int32_t nr = (n - c0) < 64 ? (n - c0) : 64;
+    double* buf = sr + (it & 1) * 64 * ST;
+#pragma unroll
+    for (int c = 0; c < ST; ++c) buf[64 * c + lane] = nx[c];
+    const int32_t cn = c0 + 64 * step;
+    if (cn < n) {
+#pragma unroll
+      for (int c = 0; c < ST; ++c) {
+        const int32_t e = cn * ST + 64 * c + lane;
+        nx[c] = e < nel ? src[e] : 0.0;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    #pragma unroll 4
+    for (int32_t r = 0; r < nr; ++r) {
+      const double F = buf[r * ST];
+      double Nr[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) Nr[s] = buf[r * ST + 1 + s];
+#pragma unroll
+      for (int j = 0; j < LPL; ++j) {
+        double y = Nr[0] * sy[j][0];
+#pragma unroll
+        for (int s = 1; s < NS; ++s) y = __builtin_fma(Nr[s], sy[j][s], y);
+        acc[j] = acc_exp1024(acc[j], F, y, sexp);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// The integration of one phase at LPL wavelengths per lane: records [h, t) (all chunks, in order), the
+// tail polynomial from the moments mm, the transparent sum tf -- k_tau_w's operations in k_tau_w's order.
 template <int NS, int LPL>
 __device__ __forceinline__ void tau_phase(const double (&sg)[LPL][NS], const SigTabs4& tabv, const double* __restrict__ src,
                                           int32_t n, double (&nx)[1 + NS], bool tail, const double (&mm)[Monos<NS>::K], double tf,
                                           int lane, double* __restrict__ sr, const double* __restrict__ sexp,
                                           double (&acc)[LPL]) {
-  constexpr Monos<NS> M{};
-  constexpr int K = Monos<NS>::K;
-  constexpr int ST = 1 + NS;
 #pragma unroll
   for (int j = 0; j < LPL; ++j) acc[j] = 0.0;
   if (n > 0) {
@@ -1501,38 +1622,7 @@ __device__ __forceinline__ void tau_phase(const double (&sg)[LPL][NS], const Sig
     for (int j = 0; j < LPL; ++j)
 #pragma unroll
       for (int s = 0; s < NS; ++s) sy[j][s] = sg[j][s] * kM1024Ln2;
-    const int32_t nel = n * ST;
-    for (int32_t c0 = 0; c0 < n; c0 += 64) {
-      const int32_t nr = (n - c0) < 64 ? (n - c0) : 64;
-      double* buf = sr + ((c0 >> 6) & 1) * 64 * ST;
-#pragma unroll
-      for (int c = 0; c < ST; ++c) buf[64 * c + lane] = nx[c];
-      if (c0 + 64 < n) {
-#pragma unroll
-        for (int c = 0; c < ST; ++c) {
-          const int32_t e = (c0 + 64) * ST + 64 * c + lane;
-          nx[c] = e < nel ? src[e] : 0.0;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      #pragma unroll 4
-      for (int32_t r = 0; r < nr; ++r) {
-        const double F = buf[r * ST];
-        double Nr[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) Nr[s] = buf[r * ST + 1 + s];
-#pragma unroll
-        for (int j = 0; j < LPL; ++j) {
-          double y = Nr[0] * sy[j][0];
-#pragma unroll
-          for (int s = 1; s < NS; ++s) y = __builtin_fma(Nr[s], sy[j][s], y);
-          acc[j] = acc_exp1024(acc[j], F, y, sexp);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
+    tau_records<NS, LPL>(sy, src, n, 0, 1, nx, lane, sr, sexp, acc);
   }
   if (tail) {
 #pragma unroll
@@ -1557,48 +1647,34 @@ __device__ __forceinline__ void tau_count(unsigned long long* __restrict__ evals
   if (lane == 0) atomicAdd(&evals[gw & 63], (unsigned long long)n * (unsigned long long)nl);
 }
 
-
-// A heavy item: phase o, 64 wavelengths of a tile (half hf), one per lane, window [h, t) of any length.
-template <int NS>
-__device__ __forceinline__ void tau_heavy(int32_t tile, int32_t hf, int32_t o, int32_t h, int32_t t, int32_t fl,
-                                          const SigTabs4& tabv, const double* __restrict__ sig,
-                                          const double* __restrict__ recs, const double* __restrict__ mrecs,
-                                          const double* __restrict__ tfrac, int32_t n_pr, int64_t n_wav,
-                                          const double* __restrict__ wmom, unsigned long long* __restrict__ evals,
-                                          int lane, int gw, double* __restrict__ sr,
-                                          const double* __restrict__ sexp, double* __restrict__ R) {
-  constexpr int K = Monos<NS>::K;
+// One heavy entry {half tile, h, t, flags | phase << 8}: this lane's wavelength, its cross-sections (row of
+// the entry's phase when PH), the record source, the first chunk `first` preloaded into nx.
+template <int NS, bool PH>
+__device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const double* __restrict__ sig,
+                                            const double* __restrict__ recs, const double* __restrict__ mrecs,
+                                            int32_t n_pr, int64_t n_wav, int lane, int64_t* w, bool* live,
+                                            double (&sg)[1][NS], const double** src, double (&nx)[1 + NS]) {
   constexpr int ST = 1 + NS;
-  const int64_t w = (int64_t)tile * kTW + 64 * hf + lane;
-  bool live[1] = {w < n_wav};
-  double sg[1][NS];
+  const int32_t o = en.w >> 8;
+  *w = (int64_t)en.x * 64 + lane;
+  *live = *w < n_wav;
+  const double* so = sig + (PH ? (int64_t)o * NS * n_wav : 0);
 #pragma unroll
-  for (int s = 0; s < NS; ++s) sg[0][s] = sig[(int64_t)s * n_wav + (live[0] ? w : n_wav - 1)];
-  const double* src = ((fl & 1) ? mrecs : recs) + ((int64_t)o * n_pr + h) * ST;
-  const int32_t nel = (t - h) * ST;
-  double nx[ST];
+  for (int s = 0; s < NS; ++s) sg[0][s] = so[(int64_t)s * n_wav + (*live ? *w : n_wav - 1)];
+  *src = (((en.w & 1) ? mrecs : recs)) + ((int64_t)o * n_pr + en.y) * ST;
+  const int32_t nel = (en.z - en.y) * ST;
 #pragma unroll
   for (int c = 0; c < ST; ++c) {
-    const int32_t e = 64 * c + lane;
-    nx[c] = e < nel ? src[e] : 0.0;
+    const int32_t e = 64 * first * ST + 64 * c + lane;
+    nx[c] = e < nel ? (*src)[e] : 0.0;
   }
-  const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;   // t <= G <= n_pr: the row exists
-  double mm[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) mm[k] = mp[k];
-  const double tf = tfrac[o];
-  double acc[1];
-  tau_phase<NS, 1>(sg, tabv, src, t - h, nx, (fl & 2) != 0, mm, tf, lane, sr, sexp, acc);
-  tau_count<1>(evals, gw, lane, t - h, live);
-  if (live[0]) R[(int64_t)o * n_wav + w] = acc[0];
 }
 
-// Grid: n_heavy heavy wavefronts (blockIdx first), then one static wavefront per (tile, group of 4
-// phases).  Static wavefront: round trip 1 = its phases' tile records {h, t, flags, tail moments}
-// (k_order), sigma at its 128 wavelengths (2 per lane), the exp table; a second round trip only for
-// the packed records of non-empty light windows.  Heavy wavefront: the unit count and its first unit,
-// then records, sigma and moments.
-template <int NS>
+// Grid: max(static units / 4, resident workgroups) workgroups of 4 wavefronts.  Static unit sw (wavefront
+// blockIdx.x * 4 + wid < n_static): tile sw % n_tiles, phases 4 (sw / n_tiles) ...; round trip 1 = its
+// phases' tile records {h, t, flags, tail moments} (k_order), sigma at its 128 wavelengths (2 per lane), the
+// exp table; a second round trip only for the packed records of non-empty light windows.
+template <int NS, bool PH>
 __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs4 tabv, const double* __restrict__ sig,
                                                                    const double* __restrict__ recs,
                                                                    const double* __restrict__ mrecs,
@@ -1609,22 +1685,22 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
                                                                    const double* __restrict__ fsum, int32_t n_pr,
                                                                    int32_t n_orb, int64_t n_wav,
                                                                    const double* __restrict__ wmom,
-                                                                   const double* __restrict__ trec, int32_t n_tiles,
-                                                                   const int4* __restrict__ hlist, int32_t hcap,
+                                                                   const int4* __restrict__ trec, int32_t n_tiles,
+                                                                   const int4* __restrict__ hlist, int64_t hcap,
                                                                    const int32_t* __restrict__ hcnt,
-                                                                   int32_t n_heavy, const uint8_t* __restrict__ zfl,
+                                                                   int32_t n_static, const uint8_t* __restrict__ zfl,
                                                                    unsigned long long* __restrict__ evals,
                                                                    unsigned long long* __restrict__ tstamp,
                                                                    double* __restrict__ R) {
-  constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int ST = 1 + NS;
   constexpr int PQ = (4 * kHeavy * ST + 63) / 64;   // packed record loads per lane
-  constexpr int TRS = 2 + K;                        // tile record: {h, t}, {flags, 0}, K moments
-  constexpr int TV = (4 * TRS + 63) / 64;           // tile-record loads per lane (four records)
+  constexpr int MQ = (4 * K + 63) / 64;             // tail-moment loads per lane (four phases)
+  constexpr int SR = PH ? 4 : 1;                    // sigma rows a static wavefront loads
   static_assert(4 * kHeavy * ST <= 2 * 64 * ST, "a group's packed records fit the wavefront's LDS slice");
   __shared__ double srec[kTP][2 * 64 * ST];   // per wavefront: two chunks of 64 records
   __shared__ double sexp[1024];                // 2^(i/1024)
+  __shared__ double spart[kTP][64];            // big entries: the wavefronts' partial sums
 #ifdef PROM_TRACE
   const unsigned long long wt0 = wall_clock64();
   long long wrk = 0;
@@ -1638,62 +1714,114 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
   double* sr = srec[wid];
   // timed runs: the workgroup's first device-clock tick (the kernel's duration is the span over all)
   if (tstamp && threadIdx.x == 0) tstamp[2 * blockIdx.x] = wall_clock64();
-  if (gw < n_heavy) {
-    // ---- heavy wavefronts: items e = gw, gw + n_heavy, ... over the 2 U halves of the U listed units;
-    //      the first unit is read with the count
-    const int32_t U = hcnt[0];
-    int4 en = hlist[min(gw >> 1, hcap - 1)];
+  const int32_t nsmall = hcnt[0], nbig = hcnt[1];
+  // the static unit's loads go out with the first round trip
+  const int32_t sw = gw;
+  const int32_t tile = sw % n_tiles, o0 = (sw / n_tiles) * 4;
+  const bool has = sw < n_static && o0 < n_orb;
+  const int32_t np = has ? min(4, n_orb - o0) : 0;
+  // lane p < np: phase p's tile record {h, t, flags, 0}
+  const int4 tv = lane < np ? trec[(int64_t)(o0 + lane) * n_tiles + tile] : make_int4(0, 0, 0, 0);
+  bool live[2];
+  double sg[SR][2][NS];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
-    __syncthreads();
-    for (int32_t e = gw; e < 2 * U; e += n_heavy) {
-      if (e != gw) en = hlist[e >> 1];
-      const int32_t tile = __builtin_amdgcn_readfirstlane(en.x), h = __builtin_amdgcn_readfirstlane(en.y);
-      const int32_t t = __builtin_amdgcn_readfirstlane(en.z), w4 = __builtin_amdgcn_readfirstlane(en.w);
+  for (int j = 0; j < 2; ++j) {
+    const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
+    live[j] = w < n_wav;
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      const double* so = sig + (PH ? (int64_t)(o0 + r) * NS * n_wav : 0);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sg[r][j][s] = r < np ? so[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)] : 0.0;
+    }
+  }
+  double tfv[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) tfv[p] = p < np ? tfrac[o0 + p] : 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
+  __syncthreads();
+
+  // ---- big entries: one per workgroup at a time, chunks round robin over the four wavefronts
+  for (int32_t e = blockIdx.x; e < nbig; e += gridDim.x) {
+    const int4 en = hlist[hcap + e];
+    const int32_t h = __builtin_amdgcn_readfirstlane(en.y), t = __builtin_amdgcn_readfirstlane(en.z);
+    const int32_t f4 = __builtin_amdgcn_readfirstlane(en.w);
+    const int32_t o = f4 >> 8;
+    int64_t w;
+    bool lv;
+    double sgh[1][NS], nx[ST];
+    const double* src;
+    heavy_setup<NS, PH>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), wid, sig, recs, mrecs, n_pr,
+                        n_wav, lane, &w, &lv, sgh, &src, nx);
+    double mm[K];
+    if (wid == 0 && (f4 & 2)) {
+      const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;   // t <= G <= n_pr: the row exists
+#pragma unroll
+      for (int k = 0; k < K; ++k) mm[k] = mp[k];
+    }
+    double sy[1][NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) sy[0][s] = sgh[0][s] * kM1024Ln2;
+    double acc[1] = {0.0};
+    tau_records<NS, 1>(sy, src, t - h, wid, kTP, nx, lane, sr, sexp, acc);
+    int32_t nrec = 0;   // records of the chunks this wavefront took
+    for (int32_t c0 = 64 * wid; c0 < t - h; c0 += 64 * kTP) nrec += min(64, t - h - c0);
+    const bool lva[1] = {lv};
+    tau_count<1>(evals, gw, lane, nrec, lva);
 #ifdef PROM_TRACE
-      wrk += t - h;
+    wrk += nrec;
 #endif
-      tau_heavy<NS>(tile, e & 1, w4 >> 8, h, t, w4 & 255, tabv, sig, recs, mrecs, tfrac, n_pr, n_wav, wmom, evals,
-                    lane, e, sr, sexp, R);
-    }
-  } else {
-    // ---- static wavefront: tile, phases o0 .. o0 + np - 1
-    const int32_t sw = gw - n_heavy;
-    const int32_t tile = sw % n_tiles, o0 = (sw / n_tiles) * 4;
-    const bool has = o0 < n_orb;
-    const int32_t np = has ? min(4, n_orb - o0) : 0;
-    // element p TRS + i (lane e & 63 of tv[e >> 6]) holds double i of phase p's tile record
-    double tv[TV];
-#pragma unroll
-    for (int q = 0; q < TV; ++q) {
-      const int e = 64 * q + lane, p = e / TRS;
-      tv[q] = p < np ? trec[((int64_t)(o0 + p) * n_tiles + tile) * TRS + (e - p * TRS)] : 0.0;
-    }
-    bool live[2];
-    double sg[2][NS];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
-      live[j] = w < n_wav;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) sg[j][s] = sig[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)];
-    }
-    double tfv[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) tfv[p] = p < np ? tfrac[o0 + p] : 0.0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
+    spart[wid][lane] = acc[0];
     __syncthreads();
+    if (wid == 0) {
+      double r = ((spart[0][lane] + spart[1][lane]) + spart[2][lane]) + spart[3][lane];
+      if (f4 & 2) {
+        double qv[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) qv[s] = sgh[0][s] * tabv.t[s].nscale;
+        r += tail_eval<NS>(mm, qv);
+      }
+      r += tfrac[o];
+      if (lv) R[(int64_t)o * n_wav + w] = r;
+    }
+    __syncthreads();
+  }
+  // ---- small entries: one per wavefront
+  for (int32_t e = gw; e < nsmall; e += gridDim.x * kTP) {
+    const int4 en = hlist[e];
+    const int32_t h = __builtin_amdgcn_readfirstlane(en.y), t = __builtin_amdgcn_readfirstlane(en.z);
+    const int32_t f4 = __builtin_amdgcn_readfirstlane(en.w);
+    const int32_t o = f4 >> 8;
+    int64_t w;
+    bool lv;
+    double sgh[1][NS], nx[ST];
+    const double* src;
+    heavy_setup<NS, PH>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), 0, sig, recs, mrecs, n_pr,
+                        n_wav, lane, &w, &lv, sgh, &src, nx);
+    const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
+    double mm[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) mm[k] = mp[k];
+    double acc[1];
+    tau_phase<NS, 1>(sgh, tabv, src, t - h, nx, (f4 & 2) != 0, mm, tfrac[o], lane, sr, sexp, acc);
+    const bool lva[1] = {lv};
+    tau_count<1>(evals, gw, lane, t - h, lva);
+#ifdef PROM_TRACE
+    wrk += t - h;
+#endif
+    if (lv) R[(int64_t)o * n_wav + w] = acc[0];
+  }
+  // ---- static unit: tile, phases o0 .. o0 + np - 1
+  if (np > 0) {
     int32_t h[4], t[4], fl[4], n[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const int2 ht = __builtin_bit_cast(int2, lane_read(tv[(p * TRS) >> 6], (p * TRS) & 63));
-      const int2 ff = __builtin_bit_cast(int2, lane_read(tv[(p * TRS + 1) >> 6], (p * TRS + 1) & 63));
-      h[p] = p < np ? ht.x : 0;
-      t[p] = p < np ? ht.y : 0;
-      fl[p] = p < np ? ff.x : 0;
+      h[p] = p < np ? lane_read(tv.x, p) : 0;
+      t[p] = p < np ? lane_read(tv.y, p) : 0;
+      fl[p] = p < np ? lane_read(tv.z, p) : 0;
     }
-    // light phases (window <= kHeavy records, not exact): packed; heavy ones are another wavefront's
+    // light phases (window <= kHeavy records, not exact): packed; heavy ones are k_order's entries
     int32_t off[5];
     off[0] = 0;
 #pragma unroll
@@ -1716,29 +1844,39 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
         pre[q] = ((fp & 1) ? mrecs : recs)[((int64_t)(o0 + p) * n_pr + hp) * ST + (e - op)];
       }
     }
+    // element p K + k (lane e & 63 of mv[e >> 6]) holds tail moment k at phase p's window end
+    double mv[MQ];
+#pragma unroll
+    for (int q = 0; q < MQ; ++q) {
+      const int e = 64 * q + lane, p = e / K;
+      const int32_t fp = p == 0 ? fl[0] : (p == 1 ? fl[1] : (p == 2 ? fl[2] : fl[3]));
+      const int32_t tp = p == 0 ? t[0] : (p == 1 ? t[1] : (p == 2 ? t[2] : t[3]));
+      mv[q] = (p < np && (fp & 2)) ? wmom[((int64_t)(o0 + p) * (n_pr + 1) + tp) * K + (e - p * K)] : 0.0;
+    }
 #pragma unroll
     for (int q = 0; q < PQ; ++q) sr[64 * q + lane] = pre[q];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double sy[2][NS];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int s = 0; s < NS; ++s) sy[j][s] = sg[j][s] * kM1024Ln2;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       if (p >= np) continue;
       const int32_t o = o0 + p;
+      const int r = PH ? p : 0;
       if (n[p] >= 0) {
+        double sy[2][NS];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < NS; ++s) sy[j][s] = sg[r][j][s] * kM1024Ln2;
         const double* buf = sr + off[p];
         double acc[2] = {0.0, 0.0};
         #pragma unroll 4
-        for (int32_t r = 0; r < n[p]; ++r) {
-          const double F = buf[r * ST];
+        for (int32_t q = 0; q < n[p]; ++q) {
+          const double F = buf[q * ST];
           double Nr[NS];
 #pragma unroll
-          for (int s = 0; s < NS; ++s) Nr[s] = buf[r * ST + 1 + s];
+          for (int s = 0; s < NS; ++s) Nr[s] = buf[q * ST + 1 + s];
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             double y = Nr[0] * sy[j][0];
@@ -1750,12 +1888,12 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
         if (fl[p] & 2) {
           double mm[K];
 #pragma unroll
-          for (int k = 0; k < K; ++k) mm[k] = lane_read(tv[(p * TRS + 2 + k) >> 6], (p * TRS + 2 + k) & 63);
+          for (int k = 0; k < K; ++k) mm[k] = lane_read(mv[(p * K + k) >> 6], (p * K + k) & 63);
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             double qv[NS];
 #pragma unroll
-            for (int s = 0; s < NS; ++s) qv[s] = sg[j][s] * tabv.t[s].nscale;
+            for (int s = 0; s < NS; ++s) qv[s] = sg[r][j][s] * tabv.t[s].nscale;
             acc[j] += tail_eval<NS>(mm, qv);
           }
         }
@@ -1772,17 +1910,18 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
         // non-finite column densities: exact reference order over the chord-order records
         const double* rb = recs + (int64_t)o * n_pr * ST;
         const int32_t* ipl = act_ip + (int64_t)o * n_pr;
+        const uint8_t* zo = zfl ? zfl + (PH ? (int64_t)o * n_wav : 0) : nullptr;
         double acc[2] = {0.0, 0.0};
         for (int32_t i = 0; i < t[p]; ++i) {
-          const double* r = rb + (int64_t)i * ST;
+          const double* rr = rb + (int64_t)i * ST;
           const double F = fout[ipl[i]];
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            double tau = r[1] * sg[j][0];
+            double tau = rr[1] * sg[r][j][0];
 #pragma unroll
-            for (int s = 1; s < NS; ++s) tau = tau + r[1 + s] * sg[j][s];
-            if (NS == 1 && zfl)
-              tau = exact_tau_merged(r[1], sg[j][0], zfl, live[j] ? (int64_t)tile * kTW + 64 * j + lane : n_wav - 1);
+            for (int s = 1; s < NS; ++s) tau = tau + rr[1 + s] * sg[r][j][s];
+            if (NS == 1 && zo)
+              tau = exact_tau_merged(rr[1], sg[r][j][0], zo, live[j] ? (int64_t)tile * kTW + 64 * j + lane : n_wav - 1);
             acc[j] = acc[j] + F * exp(-tau);
           }
         }
@@ -1805,7 +1944,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
       g_trace[wl + 1] = wall_clock64();
       g_trace[wl + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)) |
                         ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32);
-      g_trace[wl + 3] = (unsigned long long)wrk | (gw < n_heavy ? (1ull << 62) : 0ull);
+      g_trace[wl + 3] = (unsigned long long)wrk;
     }
   }
 #endif
@@ -1815,11 +1954,12 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;
   const bool wpath = tr.exp_mode && tr.n_mol == 0 && tr.n_atoms >= 1 && tr.n_atoms <= kWinMaxSpecies;
-  // no orbital Doppler shift: sigma_s(lambda_w) is resampled once per wavelength by extra workgroups
-  // of the column kernel (they run beside the chord work) instead of once per phase group
+  // sigma_s(shift lambda_w) is resampled by extra workgroups of the column kernel (they run beside the
+  // chord work): once per wavelength without orbital Doppler shift, once per (phase, wavelength) with it
   const bool cols8 = tr.n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4;
-  const bool pre_sigma = cols8 && wpath && tr.window && tr.uniform_shift && !tr.star;
-  // species merging (TransitDev::species_merge_ok) on the no-Doppler fast path: downstream of the
+  const bool pre_sigma = cols8 && wpath && tr.window && !tr.star;
+  const int32_t sig_rows = tr.uniform_shift ? 1 : tr.n_orb;
+  // species merging (TransitDev::species_merge_ok) on the resampled fast path: downstream of the
   // column kernel there is one effective absorber
   const bool msp = pre_sigma && tr.species_merge_ok;
   const int32_t nsig = tr.n_atoms;                 // species the column kernel resamples
@@ -1842,18 +1982,22 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
   if (cols8) {
-    const unsigned sig_blocks = pre_sigma ? grid_for(tr.n_wav) : 0u;
+    // with resampling: chord workgroups padded to a multiple of 8, sigma workgroups rounded up to one
+    const unsigned chord_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
+    // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
+    const unsigned sig_blocks = pre_sigma ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
+    const unsigned col_blocks = pre_sigma ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
 #define PROM_COLS(SV, NSV)                                                                               \
   hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
-                     dim3((unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8)) + sig_blocks),                \
+                     dim3(col_blocks),                                                                    \
                      dim3(kBlock), 0, s, ev0, nullptr, 0, cargs, n_terms,                                 \
                      tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
                      tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
                      tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
                      tr.moon_R.as<double>(), smax, tr.cull_tau, rs.ncol.as<double>(),                       \
                      rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>(), \
-                     pre_sigma ? rs.tq.as<float2>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale,    \
-                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, rs.zfl.as<uint8_t>())
+                     pre_sigma ? rs.tq.as<float4>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale,    \
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, rs.zfl.as<uint8_t>(), sig_rows)
 #define PROM_COLS_L(NSV)                       \
   if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
   else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
@@ -1907,6 +2051,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // 2. per-phase compaction, ordering, merging of equal-column chords, window tables (and, without
   //    orbital Doppler shift, every tile's window)
   const int32_t n_wtiles = (int32_t)((tr.n_wav + kTW - 1) / kTW);
+  const int64_t hcap = (int64_t)tr.n_orb * 2 * n_wtiles;   // heavy entries per list: at most one per half tile
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
   hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev_ord, 0,             \
@@ -1915,10 +2060,9 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      tr.window ? 1 : 0, tabs4, rs.recs.as<double>(),                                     \
                      rs.act_ip.as<int32_t>(), rs.mrecs.as<double>(), rs.counts.as<int32_t>(),            \
                      rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>(), \
-                     pre_sigma ? rs.tq.as<float2>() : nullptr, n_wtiles, rs.win.as<int2>(),             \
-                     (pre_sigma && tr.plan) ? rs.hlist.as<int4>() : nullptr,                           \
-                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr,                         \
-                     (pre_sigma && tr.plan) ? rs.trec.as<double>() : nullptr)
+                     pre_sigma ? rs.tq.as<float4>() : nullptr, sig_rows, n_wtiles, tr.n_wav,            \
+                     rs.trec.as<int4>(), (pre_sigma && tr.plan) ? rs.hlist.as<int4>() : nullptr, hcap, \
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr)
     switch (na) {
       case 1: PROM_CHW(1); break;
       case 2: PROM_CHW(2); break;
@@ -1978,7 +2122,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      dim3(kBlock), 0, s, ev_tau0, ev ? ev[3] : nullptr, 0,                              \
                      tabs4, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                           \
                      tr.n_orb, tr.n_wav, rs.wenv.as<int32_t>(), rs.wmom.as<double>(), rs.sig.as<double>(),  \
-                     rs.win.as<int2>(), n_wtiles, msp ? rs.zfl.as<uint8_t>() : nullptr,                     \
+                     rs.trec.as<int4>(), n_wtiles, msp ? rs.zfl.as<uint8_t>() : nullptr, (UV) ? sig_rows : 1, \
                      tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, R)
 #define PROM_TAUW_NS(PMV, UV)            \
   switch (na) {                          \
@@ -1988,41 +2132,44 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     default: PROM_TAUW(4, PMV, UV); break; \
   }
     if (pre_sigma && tr.plan) {
-      // planned: heavy wavefronts over k_order's lists of long windows, static ones over (tile, 4 phases)
+      // planned: big and small heavy entries from k_order's lists over the whole grid, then one static
+      // wavefront per (tile, 4 phases)
+      const bool ph = sig_rows > 1;
       if (tr.taup_resident == 0) {
         int cus = 0, nb = 0;
         int dev = 0;
         PROM_HIP(hipGetDevice(&dev));
         PROM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+#define PROM_OCC(NSV)                                                                                        \
+  (ph ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, true>, kBlock, 0)                     \
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, false>, kBlock, 0))
         switch (na) {
-          case 1: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<1>, kBlock, 0)); break;
-          case 2: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<2>, kBlock, 0)); break;
-          case 3: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<3>, kBlock, 0)); break;
-          default: PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<4>, kBlock, 0)); break;
+          case 1: PROM_HIP(PROM_OCC(1)); break;
+          case 2: PROM_HIP(PROM_OCC(2)); break;
+          case 3: PROM_HIP(PROM_OCC(3)); break;
+          default: PROM_HIP(PROM_OCC(4)); break;
         }
-        tr.taup_resident = std::max(1, cus) * std::max(1, nb) * kTP;
+#undef PROM_OCC
+        tr.taup_resident = std::max(1, cus) * std::max(1, nb);   // workgroups resident at once
       }
       const int64_t n_static = (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
-      // heavy wavefronts: what the static ones leave of one resident round, at least a quarter of it
-      int64_t n_heavy = std::max<int64_t>(tr.taup_resident / 4, tr.taup_resident - n_static);
-      n_heavy = (n_heavy + kTP - 1) / kTP * kTP;
-      const unsigned blocks = (unsigned)((n_heavy + n_static + kTP - 1) / kTP);
+      const int64_t blocks = std::max<int64_t>((n_static + kTP - 1) / kTP, tr.taup_resident);
       *variant = 30 + (na <= 4 ? na : 0);
-      unsigned long long* tsp = (tr.ts_out && (int64_t)blocks <= tr.ts_cap) ? tr.ts_out : nullptr;
+      unsigned long long* tsp = (tr.ts_out && blocks <= tr.ts_cap) ? tr.ts_out : nullptr;
       tr.ts_blocks = tsp ? (int32_t)blocks : 0;
-#define PROM_TAUP(NSV)                                                                                  \
-  hipExtLaunchKernelGGL((k_tau_p<NSV>), dim3(blocks), dim3(kBlock), 0, s,                                 \
+#define PROM_TAUP(NSV, PHV)                                                                             \
+  hipExtLaunchKernelGGL((k_tau_p<NSV, PHV>), dim3((unsigned)blocks), dim3(kBlock), 0, s,                \
                         ev_tau0, ev ? ev[3] : nullptr, 0, tabs4, rs.sig.as<double>(),                     \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
-                        rs.wmom.as<double>(), rs.trec.as<double>(), n_wtiles, rs.hlist.as<int4>(),      \
-                        (int32_t)(tr.n_orb * n_wtiles), rs.hcnt.as<int32_t>(), (int32_t)n_heavy,        \
+                        rs.wmom.as<double>(), rs.trec.as<int4>(), n_wtiles, rs.hlist.as<int4>(),        \
+                        hcap, rs.hcnt.as<int32_t>(), (int32_t)n_static,                                 \
                         msp ? rs.zfl.as<uint8_t>() : nullptr,                                            \
                         tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tsp, R)
       switch (na) {
-        case 1: PROM_TAUP(1); break;
-        case 2: PROM_TAUP(2); break;
-        case 3: PROM_TAUP(3); break;
-        default: PROM_TAUP(4); break;
+        case 1: if (ph) { PROM_TAUP(1, true); } else { PROM_TAUP(1, false); } break;
+        case 2: if (ph) { PROM_TAUP(2, true); } else { PROM_TAUP(2, false); } break;
+        case 3: if (ph) { PROM_TAUP(3, true); } else { PROM_TAUP(3, false); } break;
+        default: if (ph) { PROM_TAUP(4, true); } else { PROM_TAUP(4, false); } break;
       }
 #undef PROM_TAUP
     } else if (pre_sigma) { PROM_TAUW_NS(8, true) } else { PROM_TAUW_NS(2, false) }

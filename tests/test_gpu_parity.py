@@ -312,14 +312,16 @@ def test_many_los_samples_generic_columns(dev):
     assert rel(R, Ro) < R_TOL
 
 
-@pytest.mark.parametrize("name", ["C1", "C2r", "exomoon", "C2"])
+@pytest.mark.parametrize("name", ["C1", "C2r", "C3r", "C4r", "exomoon", "C2", "C3"])
 def test_planned_tau_bitwise(dev, name, monkeypatch):
-    """The planned tau kernel (k_tau_p: static (tile, 4-phase) wavefronts + heavy-window wavefronts from
-    k_order's lists) computes every (phase, wavelength) with k_tau_w's operations in k_tau_w's order:
-    R is bitwise identical with the planned path off (PROM_TAU_PLAN=0), and the exp count is equal."""
+    """The planned tau kernel (k_tau_p: static (tile, 4-phase) wavefronts for light windows, heavy entries
+    per 64-wavelength half with their own windows, long ones split into 64-record chunks over a workgroup)
+    against k_tau_w (PROM_TAU_PLAN=0: one window per 128-wavelength tile, records summed in order).  Light
+    tiles are bitwise equal; heavy halves differ by at most the two windows' truncation bounds plus the
+    chunked summation's rounding, and never evaluate more exponentials."""
     from prometheus_amd import configs
-    if name == "C2":
-        cfg = configs.get("C2")
+    if name in ("C2", "C3"):
+        cfg = configs.get(name)
     else:
         cfg = json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
@@ -330,10 +332,10 @@ def test_planned_tau_bitwise(dev, name, monkeypatch):
     R_w = tr.sumOverChords(devices=[0])
     st_w = tr.last_stats[-1]
     print(name, "variants", st_p["tau_kernel_variant"], st_w["tau_kernel_variant"], "exp evals", st_p["exp_evals"])
-    if not cfg["Fundamentals"]["DopplerOrbitalMotion"]:
-        assert st_p["tau_kernel_variant"] // 10 == 3 and st_w["tau_kernel_variant"] // 10 == 2
-    assert np.array_equal(R_p, R_w)
-    assert st_p["exp_evals"] == st_w["exp_evals"]
+    assert st_p["tau_kernel_variant"] // 10 == 3 and st_w["tau_kernel_variant"] // 10 == 2
+    bound = 2 * (2.0 ** -40 / 24 + np.exp(-40.0)) + 1e-14
+    assert np.max(np.abs(R_p - R_w)) <= bound
+    assert st_p["exp_evals"] <= st_w["exp_evals"]
 
 
 @pytest.mark.parametrize("name", ["C2r", "C2"])

@@ -25,6 +25,7 @@ SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_SMEM SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT 
 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_LEVEL_WAVES SQ_INSTS_BRANCH
 FETCH_SIZE
 WRITE_SIZE
+TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum
 PASSES
 find $OUT -name "*counter_collection.csv" | head
 exit 0

@@ -17,10 +17,9 @@ import numpy as np  # noqa: E402
 from prometheus_amd import build  # noqa: E402
 
 out = os.path.join(REPO, "prometheus_amd", "libprom_hip_trace.so")
-cmd = [build.hipcc()] + build.FLAGS + ["-DPROM_TRACE", "-o", out] + [os.path.join(build.HERE, s) for s in build.SOURCES]
-srcs = [os.path.join(build.HERE, s) for s in build.SOURCES]
+srcs = [os.path.join(build.HERE, s) for s in build.SOURCES + build.HEADERS]
 if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(f) for f in srcs):
-    subprocess.run(cmd, check=True, cwd=build.HERE)
+    build.build(force=True, extra=["-DPROM_TRACE"], out=out, objdir=os.path.join(build.HERE, "build_trace"))
 os.environ["PROMETHEUS_AMD_LIB"] = out
 
 from prometheus_amd import _native, configs, gasProperties, setupfile  # noqa: E402
