@@ -3,17 +3,19 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu-baseline]
 
-N=1: the BASELINE.json configs[1] workload (C2: barometric Na + K, 190,205 wavelengths x 8
-orbital phases x 2,400 chords x 30 samples, WASP-49b).  One step = one pass of the hot path over
-the whole spectrum with all inputs resident in HBM: density + column densities + culling,
-sigma resample of every species at every phase, and the fused tau -> exp(-tau) -> disk-sum ->
-ratio kernel (prom_transit_run).
+N=1: the largest single-GPU configuration of BASELINE.json, configs[2] (C3: power-law atmosphere
+with Na I + Ca II + Mg I, orbital Doppler shift on, 351,222 wavelengths x 16 orbital phases x
+2,400 chords x 30 samples, WASP-49b).  One step = one pass of the hot path over the whole spectrum
+with all inputs resident in HBM: density + column densities + culling, sigma resample of every
+species at every phase's Doppler shift, chord ordering, and the fused tau -> exp(-tau) ->
+disk-sum -> ratio kernel (prom_transit_run).  --config C2 gives the configs[1] line.
 
-N>1 (launched by torch.distributed.run, one process per GPU): weak scaling by wavelength
-sharding.  The global spectrum is the C2 grid at N-times finer resolution (resolutionLow/N,
-resolutionHigh/N: ~N x 190k wavelengths); rank r integrates the contiguous shard r of it.  No
-collective touches the data path; torch.distributed is used only for the timing barrier and the
-max-over-ranks time.
+N>1 (launched by torch.distributed.run, one process per GPU), wavelength sharding, no collective on
+the data path (torch.distributed carries only the timing barrier and the max-over-ranks time):
+  --scaling weak (default): the global spectrum is the config's grid at N-times finer resolution
+      (resolutionLow/N, resolutionHigh/N: ~N x the wavelengths); rank r integrates shard r.
+  --scaling strong: the global spectrum is the config's grid as it stands (e.g. --config C4x10,
+      C5), split into N contiguous shards.
 
 Prints one JSON line (rank 0).
 """
@@ -42,7 +44,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="C2")
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--cpu-workers", type=int, default=None,
+                    help="processes of the multi-core CPU baseline leg (default: this process's CPU share, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-wavelengths", type=int, default=None,
                     help="oracle sample size (default: ~10 s of reference-speed CPU work per config)")
@@ -53,10 +58,10 @@ def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
 
-def global_config(name: str, world: int) -> dict:
+def global_config(name: str, world: int, scaling: str = "weak") -> dict:
     from prometheus_amd import configs
     cfg = configs.get(name)
-    if world > 1:
+    if world > 1 and scaling == "weak":
         g = cfg["Grids"]
         g["resolutionLow"] = g["resolutionLow"] / world
         g["resolutionHigh"] = g["resolutionHigh"] / world
@@ -81,10 +86,12 @@ def tau_bytes_per_launch(n_wav: int, n_orb: int, n_sigma: int) -> int:
     return 8 * n_orb * n_wav + 8 * n_wav * n_sigma
 
 
-def latest_profile_traffic(kernel: str = "prom::k_tau_p"):
-    """Measured HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC summary
-    (profiles/*traffic_all_kernels.json, tools/bench_traffic.sh), or None."""
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*traffic_all_kernels.json")), reverse=True):
+def latest_profile_traffic(kernel: str, config: str):
+    """Measured HBM bytes per launch of ``kernel`` on ``config`` from the newest committed rocprofv3 PMC
+    summary (profiles/r*_<config>_traffic.json, written by tools/bench_traffic.sh through
+    tools/traffic_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md "HBM"), or None."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_%s_traffic.json" % config)), reverse=True):
         try:
             with open(path) as fh:
                 d = json.load(fh)
@@ -100,29 +107,92 @@ def describe(cfg: dict) -> str:
     return "; ".join("%s: %s" % (k, "+".join(v.keys())) for k, v in cfg["Species"].items())
 
 
-def cpu_baseline(cfg: dict, n_sample: int):
-    """The oracle (numpy restatement of the reference dataflow, single process) on a bounded sample:
-    every phase and chord of the config, the first n_sample wavelengths of the grid."""
+_CPU = {}
+
+
+def _cpu_chunk(sel):
+    """One worker's share of the multi-core CPU leg (state inherited from the parent at fork)."""
+    from oracle import prom_oracle as O
+    scen, dop, grids, tabs = _CPU["state"]
+    t0 = time.perf_counter()
+    O.transit_depth(scen, dop, grids, sel, tabs)
+    return time.perf_counter() - t0
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))   # the GPU box grants 16 CPUs per GPU (nproc shows the whole host)
+
+
+def cpu_baseline(cfg: dict, n_sample: int, workers: int):
+    """The oracle (numpy restatement of the reference dataflow, gasProperties.py:1160-1258) on a bounded
+    sample of the same workload, two legs:
+      single: one process, the first n_sample wavelengths (what the reference itself does: it is
+              single-threaded);
+      multi:  `workers` forked processes over a wavelength-chunked sample of workers * n_sample
+              wavelengths (the reference's CPU multiprocessing plan, SURVEY.md 8d / BASELINE.md).
+    Every phase and chord is integrated.  Runs before this process touches the GPU, so the fork is clean.
+    Returns the multi-core leg as the baseline, with the single-core leg beside it."""
+    import multiprocessing as mp
     from oracle import prom_oracle as O
     mol = {"H2O": O.synthetic_molecular_table()} if "H2O" in str(cfg["Species"]) else None
     scen, dop, grids = O.from_setup(cfg, mol)
     tabs = O.build_tables(scen, grids)
     wav = O.simulation_wavelengths(grids, O.atomic_species(scen))
+    n_orb = int(grids["orbphase_steps"])
+    n_pr = int(grids["phi_steps"]) * int(grids["rho_steps"])
     sel = wav[:n_sample]
     t0 = time.perf_counter()
     O.transit_depth(scen, dop, grids, sel, tabs)
-    dt = time.perf_counter() - t0
-    pts = len(sel) * int(grids["orbphase_steps"])
-    return {"value": pts / dt, "unit": "spectrum points/s", "cores": 1, "kind": "port",
-            "sample": "%s: all %d phases x %d chords, first %d of %d wavelengths (%d points) in %.2f s, "
-                      "single-process numpy" % (cfg.get("_name", "config"), int(grids["orbphase_steps"]),
-                                                int(grids["phi_steps"]) * int(grids["rho_steps"]), len(sel),
-                                                len(wav), pts, dt)}
+    dt1 = time.perf_counter() - t0
+    single = len(sel) * n_orb / dt1
+    _CPU["state"] = (scen, dop, grids, tabs)
+    n_mc = min(len(wav), n_sample * workers)
+    chunks = [c for c in np.array_split(wav[:n_mc], workers) if len(c)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(len(chunks)) as pool:
+        pool.map(_cpu_chunk, [c[:1] for c in chunks])          # workers up (imports, first touch)
+        t0 = time.perf_counter()
+        pool.map(_cpu_chunk, chunks, chunksize=1)
+        dtm = time.perf_counter() - t0
+    multi = n_mc * n_orb / dtm
+    name = cfg.get("_name", "config")
+    return {"value": multi, "unit": "spectrum points/s", "cores": len(chunks), "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "single_core_value": single,
+            "sample": "%s: all %d phases x %d chords; multi-core leg: first %d of %d wavelengths (%d points) "
+                      "chunked over %d forked numpy processes in %.2f s; single-core leg: first %d wavelengths "
+                      "in %.2f s (%.3g points/s)" % (name, n_orb, n_pr, n_mc, len(wav), n_mc * n_orb,
+                                                     len(chunks), dtm, len(sel), dt1, single)}
+
+
+CPU_SAMPLE = {"C1": 219, "C2": 12288, "C3": 6144, "C4": 12288, "C4x10": 12288, "C5": 16}
 
 
 def main():
     args = parse()
     rank, local_rank, world = dist_env()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before anything touches the GPU: the multi-core leg forks worker processes
+        cfgc = global_config(args.config, 1)
+        cfgc["_name"] = args.config
+        cpu = cpu_baseline(cfgc, args.cpu_sample_wavelengths or CPU_SAMPLE.get(args.config, 4096),
+                           args.cpu_workers or cpu_share())
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
     dist = None
@@ -132,7 +202,7 @@ def main():
     from prometheus_amd import _native, setupfile, gasProperties, sharding  # noqa: F401
     _native.set_default_device(local_rank)
 
-    cfg = global_config(args.config, world)
+    cfg = global_config(args.config, world, args.scaling)
     cfg_name = args.config
     if any(sp not in ("NaI", "KI", "CaII", "MgI") for sc in cfg["Species"].values() for sp in sc):
         from prometheus_amd.configs import synthetic_molecular_table
@@ -204,7 +274,7 @@ def main():
         # on top of the atomic exp evaluation
         flops_unit += 6 * len(host["x"])
     flops = evals * flops_unit
-    traffic = latest_profile_traffic("prom::" + tau_kernel)
+    traffic = latest_profile_traffic("prom::" + tau_kernel, cfg_name)
     # end-to-end (host prep + H2D + run + D2H) for reference, one call
     t_e2e = time.perf_counter()
     R = tr.sumOverChords(devices=[local_rank]) if world == 1 else None
@@ -218,7 +288,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (WASP-49b catalogue system, NIST line list bundled from the reference)",
@@ -241,13 +311,10 @@ def main():
                    "blocked": st["blocked_chords"], "integrated_records": st["tau_records"]},
         "setup_s": setup_s,
         "end_to_end_s": e2e_s if R is not None else None,
+        "end_to_end_points_per_s": (n_wav_global * n_orb / e2e_s) if R is not None else None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cfgc = dict(cfg)
-        cfgc["_name"] = cfg_name
-        n_cpu = args.cpu_sample_wavelengths or {"C1": 219, "C2": 12288, "C3": 6144, "C4": 12288,
-                                                 "C5": 16}.get(cfg_name, 4096)
-        result["cpu_baseline"] = cpu_baseline(cfgc, n_cpu)
+    if cpu is not None:
+        result["cpu_baseline"] = cpu
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -90,6 +90,15 @@ def c4():
             "Grids": _grids(5880e-8, 7710e-8, 1e-10, 1e-11)}
 
 
+def c4x10():
+    """C4 at 10x finer resolution (resLow 0.001 A, resHigh 0.0001 A: ~1.8e6 wavelengths), the
+    strong-scaling variant of SURVEY.md 8d/8e."""
+    cfg = c4()
+    cfg["Grids"]["resolutionLow"] = 1e-11
+    cfg["Grids"]["resolutionHigh"] = 1e-12
+    return cfg
+
+
 def c5():
     """hydrostatic + synthetic H2O table, 1-2 micron at 1e-10 cm (1e6 points), 32 phases."""
     return {"Fundamentals": _fund(False),
@@ -112,7 +121,7 @@ def exomoon():
     return cfg
 
 
-PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C5": c5, "exomoon": exomoon}
+PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C5": c5, "exomoon": exomoon}
 
 
 def get(name: str) -> dict:

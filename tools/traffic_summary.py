@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Per-launch FETCH_SIZE / WRITE_SIZE of each kernel from tools/bench_traffic.sh output (kB -> bytes).
 gfx950 note (MI355X_MICROARCH.md, HBM): FETCH_SIZE reads exactly half the bytes of a wide (16 B/lane)
-coalesced stream; other access widths are uncalibrated.  We report the raw counter bytes
-(hbm_bytes_per_launch = (FETCH_SIZE + WRITE_SIZE) * 1024) and, separately, the read side doubled
-as an upper estimate."""
+coalesced stream; other access widths are uncalibrated.  hbm_bytes_per_launch applies that
+correction (2 * FETCH_SIZE + WRITE_SIZE, kB -> bytes); the raw counter sum is kept beside it as
+hbm_bytes_per_launch_raw."""
 import collections
 import csv
 import glob
@@ -28,6 +28,6 @@ for k, c in acc.items():
     fetch = sum(c["FETCH_SIZE"]) / max(1, len(c["FETCH_SIZE"])) * 1024.0
     write = sum(c["WRITE_SIZE"]) / max(1, len(c["WRITE_SIZE"])) * 1024.0
     out[short] = {"launches": max(len(c["FETCH_SIZE"]), len(c["WRITE_SIZE"])), "fetch_bytes": fetch,
-                  "write_bytes": write, "hbm_bytes_per_launch": fetch + write,
-                  "hbm_bytes_per_launch_read_doubled": 2 * fetch + write}
+                  "write_bytes": write, "hbm_bytes_per_launch": 2 * fetch + write,
+                  "hbm_bytes_per_launch_raw": fetch + write, "fetch_correction": 2.0}
 json.dump(out, sys.stdout, indent=1)
