@@ -571,6 +571,54 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       }
       tr.sigtab_v = prom::SigTabs4{};
       for (size_t i = 0; i < st.size() && i < 4; ++i) tr.sigtab_v.t[i] = st[i];
+      // sigma segments of the Doppler rows (k_columns8 sigma_rows_block): per 256-wavelength block and
+      // atomic slot, nodes [lo, hi] with X[lo] <= fl(s_min lambda_first) and fl(s_max lambda_last) < X[hi]
+      // (numpy's bracket j of a target: the largest j <= n-2 with X[j] <= t)
+      tr.sig_seg_ok = false;
+      if (!tr.uniform_shift && n_atoms >= 1 && n_atoms <= 4) {
+        const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
+        std::vector<int32_t> seg(2 * nb * n_atoms, 0);
+        int32_t ia = 0;
+        for (const auto& t : tr.terms) {
+          if (t.is_molecule) continue;
+          const prom::AtomTable& tb = ctx->tables[t.table];
+          const std::vector<double>& X = tb.hx;
+          const int64_t n = tb.n;
+          double smin = INFINITY, smax = -INFINITY;
+          bool ok = n >= 2 && (int64_t)X.size() == n;
+          for (int64_t o = 0; o < n_orb; ++o) {
+            const double v = sh[t.scenario * n_orb + o];
+            if (!(v > 0.0) || !std::isfinite(v)) ok = false;
+            smin = std::min(smin, v);
+            smax = std::max(smax, v);
+          }
+          auto bracket = [&](double v) -> int64_t {
+            int64_t j = (int64_t)(std::upper_bound(X.begin(), X.end(), v) - X.begin()) - 1;
+            return j < 0 ? 0 : (j > n - 2 ? n - 2 : j);
+          };
+          for (int64_t b = 0; ok && b < nb; ++b) {
+            double lmin = INFINITY, lmax = -INFINITY;
+            bool fin = true;
+            for (int64_t w = b * prom::kSigBlockW; w < std::min<int64_t>(tr.n_wav, (b + 1) * prom::kSigBlockW); ++w) {
+              const double l = pb->wavelength[w];
+              if (!(l > 0.0) || !std::isfinite(l)) fin = false;
+              lmin = std::min(lmin, l);
+              lmax = std::max(lmax, l);
+            }
+            if (!fin) continue;
+            const double tlo = smin * lmin, thi = smax * lmax;
+            const int64_t lo = bracket(tlo);
+            const int64_t hi = thi >= X[n - 1] ? n - 1 : bracket(thi) + 1;
+            const int64_t m = hi - lo + 1;
+            if (m < 2 || m > prom::kSigSeg) continue;
+            seg[2 * (b * n_atoms + ia)] = (int32_t)lo;
+            seg[2 * (b * n_atoms + ia) + 1] = (int32_t)m;
+          }
+          ++ia;
+        }
+        upload(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
+        tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
+      }
     }
     tr.star = pb->has_star != 0;
     tr.star_table_id = tr.star ? pb->star_table : -1;

@@ -76,6 +76,11 @@ constexpr int kWinMaxSpecies = 4;
 // (prom_kernels.hip Monos / TailDeg: degree 7 for one effective species, 3 otherwise)
 inline int n_tail_moments(int S) { return S == 1 ? 8 : (S + 1) * (S + 2) * (S + 3) / 6; }
 
+// Doppler cross-section rows: table nodes a resampling workgroup stages in LDS per species (prom_api.hip
+// sigma segments; larger slices gather from the global table).
+constexpr int kSigSeg = 1024;
+constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
+
 // Stellar-spectrum path: star-table nodes a tau workgroup stages in LDS (prom_api.hip rm_slices).
 constexpr int kRmStarMax = 1024;
 
@@ -258,6 +263,10 @@ struct TransitDev {
   SigTabDev star_tab{};                     // the F_star table (x, log10 F, offset 0; shift unused)
   DevBuf crho, cclv, cshift;                // [n_pr]
   DevBuf rm_slices;                         // [n_wav tiles of kBlock][3] {lo, m, half}: LDS slice
+  // orbital Doppler shift: per 256-wavelength block and atomic slot, the table nodes {lo, m} every
+  // phase's shifted targets fall between (m = 0: more than kSigSeg, the block gathers per target)
+  DevBuf sig_seg;                           // [n_wav blocks][n_atoms] int2
+  bool sig_seg_ok = false;
   RunSlot slot[kMaxSlots];
   // PROM_GRAPH=1: a fast-path run is one hipGraph per slot, captured at the slot's first untimed run
   // and replayed (one host call instead of three launches; slower on ROCm 7.2, so off by default)
@@ -305,6 +314,10 @@ void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, 
 // tau pair (the fast path carries them on the tau kernel's dispatch packet)
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events);
+// orbital Doppler shift: the per-phase cross-section rows, Y or sigma_s, and the Q ranges (prom_sigma.hip)
+void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
+                       int32_t n_rows, const int2* seg, double* sig, float4* tq, int32_t merge_sp, double nscale_m,
+                       uint8_t* zfl, hipEvent_t ev_start);
 // the fused tau kernels of the molecular and stellar-spectrum paths (prom_mol.hip, prom_rm.hip)
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev);

@@ -1015,7 +1015,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     PROM_TS(o * 16 + 5);
     const bool wtab = sorted && window;
     const int32_t pfl = (sorted ? 1 : 0) | (nnf ? 4 : 0);
-    constexpr int HCAP = (int)(sizeof(skey) / sizeof(int4)) / 2;   // staged entries per list
+    constexpr int HCAP = (int)(sizeof(skey) / (sizeof(int4))) / 2;   // staged entries per list
     int4* hbuf = reinterpret_cast<int4*>(skey);                    // [0, HCAP) small, [HCAP, 2 HCAP) big
     const float4* tqo = tq + (tq_rows > 1 ? (int64_t)o * n_tiles : 0);
     const int32_t t_all = sorted ? G : nact;
@@ -1971,7 +1971,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   *variant = (na <= 4 ? na : 0) + (tr.exp_mode ? (wpath && tr.window ? 20 : 10) : 0);
   // stage events ride on the fast path's dispatch packets (hipExtLaunchKernelGGL start/stop events):
   // no separate event packets between the kernels
-  hipEvent_t ev0 = (ev && stage_events) ? ev[0] : nullptr;
+  hipEvent_t ev0 = (ev && stage_events) ? ev[0] : nullptr;   // not const: k_sigma_rows may take it
   hipEvent_t ev1 = (ev && stage_events) ? ev[1] : nullptr;
   // timed runs (no stage events): the tau kernel's interval opens at the ordering kernel's completion
   // (its stop event), not at the tau packet's own start, which the command processor stamps before the
@@ -1985,8 +1985,16 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // with resampling: chord workgroups padded to a multiple of 8, sigma workgroups rounded up to one
     const unsigned chord_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
     // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
-    const unsigned sig_blocks = pre_sigma ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
-    const unsigned col_blocks = pre_sigma ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
+    // orbital Doppler shift with sigma segments: the rows come from their own kernel (k_sigma_rows)
+    const bool rows_seg = pre_sigma && sig_rows > 1 && tr.sig_seg_ok;
+    const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
+    const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
+    if (rows_seg) {
+      launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<int2>(),
+                        rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale,
+                        rs.zfl.as<uint8_t>(), ev0);
+      ev0 = nullptr;
+    }
 #define PROM_COLS(SV, NSV)                                                                               \
   hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
                      dim3(col_blocks),                                                                    \
@@ -2003,7 +2011,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
   else if (tr.n_x <= 32) PROM_COLS(4, NSV);    \
   else PROM_COLS(8, NSV);
-    if (!pre_sigma) { PROM_COLS_L(0) }
+    if (!pre_sigma || rows_seg) { PROM_COLS_L(0) }
     else if (nsig == 1) { PROM_COLS_L(1) }
     else if (nsig == 2) { PROM_COLS_L(2) }
     else if (nsig == 3) { PROM_COLS_L(3) }

@@ -431,3 +431,22 @@ def test_graph_replay_matches(dev, monkeypatch):
         dev.synchronize()
         assert np.array_equal(dev.transit_result(), R0)
     assert rel(R0, d["R"]) < R_TOL
+
+
+@pytest.mark.parametrize("name,merge", [("C3r", "1"), ("C3r", "0"), ("C4r", "1"), ("exomoon", "1"), ("C3", "1"),
+                                        ("C3", "0"), ("C4", "1")])
+def test_sigma_rows_bitwise(dev, name, merge, monkeypatch):
+    """Orbital Doppler shift: the per-phase cross-section rows from k_sigma_rows (table slices staged in
+    LDS per wavelength block, slopes divided per node, brackets walked from row to row;
+    PROM_SIGMA_ROWS=1) are bit-for-bit the per-target directory lookups (PROM_SIGMA_ROWS=0), merged
+    (Y = sum_s chi_s sigma_s) and per species: R is identical."""
+    from prometheus_amd import configs
+    cfg = configs.get(name) if name in ("C3", "C4") else json.loads(str(load("transit_" + name)["config"]))
+    tr = _product_transit(cfg)
+    monkeypatch.setenv("PROM_SPECIES_MERGE", merge)
+    monkeypatch.setenv("PROM_SIGMA_ROWS", "1")
+    R_a = tr.sumOverChords(devices=[0])
+    monkeypatch.setenv("PROM_SIGMA_ROWS", "0")
+    R_b = tr.sumOverChords(devices=[0])
+    print(name, "merge", merge, "max rel diff %.3e" % rel(R_a, R_b))
+    assert np.array_equal(R_a, R_b)
