@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PROM_ABI_VERSION 2
+#define PROM_ABI_VERSION 3
 
 typedef struct prom_ctx prom_ctx;
 
@@ -104,7 +104,11 @@ enum prom_density_kind {
   PROM_DENSITY_HYDROSTATIC = 2, /* :185-204  p = {n_0, R, G*mu*M, k_B*T, Jeans_0}                */
   PROM_DENSITY_POWERLAW = 3,    /* :228-244, :311-330, :356-374  p = {n_0, R, q} (planet or moon) */
   PROM_DENSITY_TORUS = 4,       /* :491-516  p = {n_0, a_torus, 4*H_torus, H_torus}              */
-  PROM_DENSITY_TABULATED = 5    /* any other plugin: n(c, x) evaluated by the caller              */
+  PROM_DENSITY_TABULATED = 5,   /* any other plugin: n(c, x) evaluated by the caller              */
+  PROM_DENSITY_GRIDDED = 6      /* SerpensExosphere :548-601: scipy RegularGridInterpolator (linear,
+                                   bounds_error) of a 3-D grid at (x - body_x, y - body_y, z);
+                                   p = {n_gx, n_gy, n_gz}, grid in prom_scenario.n_tabulated as
+                                   [gx[n_gx], gy[n_gy], gz[n_gz], values[n_gx][n_gy][n_gz]]        */
 };
 
 typedef struct prom_density_model {
@@ -119,6 +123,14 @@ int32_t prom_number_density(prom_ctx* ctx, const prom_density_model* model, int3
                             const double* x, int64_t n_chords, const double* y, const double* z,
                             const double* body_x, const double* body_y, double* n_out);
 
+/* SerpensExosphere.InterpolatedDensity (gasProperties.py:583-601; scipy RegularGridInterpolator, method
+ * linear): out[i] = trilinear value of values[n_gx][n_gy][n_gz] on the ascending axes gx, gy, gz at
+ * (px[i], py[i], pz[i]), in scipy's corner order.  A point outside the grid in any dimension gives NaN
+ * (the reference raises: bounds_error=True). */
+int32_t prom_gridded_density(prom_ctx* ctx, int32_t n_gx, const double* gx, int32_t n_gy, const double* gy,
+                             int32_t n_gz, const double* gz, const double* values, int64_t n_points,
+                             const double* px, const double* py, const double* pz, double* out);
+
 /* ---- the fused transit integrator (Transit.sumOverChords, gasProperties.py:1160-1258, with
  *      Atmosphere.getLOSopticalDepth_Batch :885-956 and the density / sigma lookups inside) ----- */
 typedef struct prom_constituent {
@@ -132,8 +144,9 @@ typedef struct prom_scenario {
   const double* body_x;        /* [n_orb] density centre per phase (planet or moon)          */
   const double* body_y;        /* [n_orb]                                                     */
   const double* shift;         /* [n_orb] Doppler factor per phase (constants.py:31-45)       */
-  const double* n_tabulated;   /* TABULATED only: n[c][x] in the reference's chord order
-                                  (c = ip * n_orb + o, geometryHandler.py:202-207)            */
+  const double* n_tabulated;   /* TABULATED: n[c][x] in the reference's chord order
+                                  (c = ip * n_orb + o, geometryHandler.py:202-207);
+                                  GRIDDED: the packed axes and values (prom_density_kind)      */
   double T;                    /* molecular constituents: lookup temperature                  */
   int32_t n_constituents;
   int32_t reserved;

@@ -24,6 +24,7 @@ DENSITY_HYDROSTATIC = 2
 DENSITY_POWERLAW = 3
 DENSITY_TORUS = 4
 DENSITY_TABULATED = 5
+DENSITY_GRIDDED = 6
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -62,7 +63,7 @@ class TransitProblem(C.Structure):
                 ("chord_rho", _dp), ("chord_clv", _dp), ("chord_star_shift", _dp)]
 
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
 OPT_NO_WINDOW = 4
@@ -102,6 +103,8 @@ SIGNATURES = {
                                          C.c_int64, _dp, _dp]),
     "prom_number_density": (C.c_int32, [C.c_void_p, C.POINTER(DensityModel), C.c_int32, _dp, C.c_int64,
                                         _dp, _dp, _dp, _dp, _dp]),
+    "prom_gridded_density": (C.c_int32, [C.c_void_p, C.c_int32, _dp, C.c_int32, _dp, C.c_int32, _dp, _dp,
+                                         C.c_int64, _dp, _dp, _dp, _dp]),
     "prom_transit_set": (C.c_int32, [C.c_void_p, C.POINTER(TransitProblem)]),
     "prom_transit_run": (C.c_int32, [C.c_void_p, C.POINTER(TransitStats)]),
     "prom_transit_result": (C.c_int32, [C.c_void_p, _dp]),
@@ -277,6 +280,20 @@ class Device:
         out = np.empty((len(y), len(x)))
         self._check(self.lib.prom_number_density(self.h, C.byref(m), len(x), _d(x), len(y), _d(y), _d(z), _d(bx),
                                                  _d(by), _d(out)), "prom_number_density")
+        return out
+
+    def gridded_density(self, gx, gy, gz, values, px, py, pz) -> np.ndarray:
+        """prom_gridded_density: scipy RegularGridInterpolator (linear) of values on (gx, gy, gz) at the
+        points (px, py, pz); NaN outside the grid."""
+        gx, gy, gz = _f64(gx), _f64(gy), _f64(gz)
+        v = _f64(values)
+        if v.shape != (len(gx), len(gy), len(gz)):
+            raise ValueError("values must have shape (len(gx), len(gy), len(gz))")
+        px, py, pz = np.broadcast_arrays(_f64(px), _f64(py), _f64(pz))
+        px, py, pz = _f64(px), _f64(py), _f64(pz)
+        out = np.empty(px.shape)
+        self._check(self.lib.prom_gridded_density(self.h, len(gx), _d(gx), len(gy), _d(gy), len(gz), _d(gz), _d(v),
+                                                  px.size, _d(px), _d(py), _d(pz), _d(out)), "prom_gridded_density")
         return out
 
     # ---- transit ------------------------------------------------------------------------

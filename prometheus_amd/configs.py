@@ -121,6 +121,34 @@ def exomoon():
     return cfg
 
 
+def synthetic_serpens_particles(path, n=60000, seed=11, planet="WASP-49b"):
+    """Seeded stand-in for a SERPENS output file (no SERPENS run or file in this image): one particle
+    per row, x y z in metres (SerpensExosphere reads it with np.loadtxt and multiplies by 100), written
+    with 17 significant digits so the file reads back bit-exactly.  A Gaussian cloud about the planet at
+    orbital phase 0, (a, 0, 0), of 1.2 R_p along x and y and 0.8 R_p along z, with a trailing tail
+    towards -y (2/5 of the particles).  Returns path."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    a, Rp, _ = _system(planet)
+    n_tail = 2 * n // 5
+    core = rng.normal(0.0, 1.0, (n - n_tail, 3)) * np.array([1.2 * Rp, 1.2 * Rp, 0.8 * Rp])
+    s = rng.uniform(0.0, 1.0, n_tail)
+    tail = np.stack([rng.normal(0.0, 0.6 * Rp, n_tail), -s * 6.0 * Rp + rng.normal(0.0, 0.4 * Rp, n_tail),
+                     rng.normal(0.0, 0.5 * Rp, n_tail)], axis=1)
+    pos = np.concatenate([core, tail]) + np.array([a, 0.0, 0.0])
+    np.savetxt(path, pos / 1e2, fmt="%.17g")
+    return path
+
+
+def serpens(path):
+    """SERPENS exosphere of Na (prometheus.py:100-105) over the particle file at ``path``, Doppler on."""
+    return {"Fundamentals": _fund(True),
+            "Scenarios": {"serpens": {"serpensPath": path}},
+            "Architecture": {"planetName": "WASP-49b"},
+            "Species": {"serpens": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 2e32}}},
+            "Grids": _grids(5884e-8, 5902e-8, 1e-9, 5e-11, orbphase_steps=4)}
+
+
 PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C5": c5, "exomoon": exomoon}
 
 

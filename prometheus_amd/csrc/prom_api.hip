@@ -48,7 +48,18 @@ prom::DensityDev to_dev(const prom_density_model& m) {
   return d;
 }
 
-bool valid_kind(int32_t k) { return k >= PROM_DENSITY_BAROMETRIC && k <= PROM_DENSITY_TABULATED; }
+bool valid_kind(int32_t k) { return k >= PROM_DENSITY_BAROMETRIC && k <= PROM_DENSITY_GRIDDED; }
+
+// GRIDDED: grid sizes from p[0..2] (each >= 2) and the packed length of [gx, gy, gz, values]
+bool gridded_dims(const prom_density_model& m, int64_t* nx, int64_t* ny, int64_t* nz, int64_t* len) {
+  for (int i = 0; i < 3; ++i)
+    if (!(m.p[i] >= 2.0 && m.p[i] <= 1.0e6 && m.p[i] == std::floor(m.p[i]))) return false;
+  *nx = (int64_t)m.p[0];
+  *ny = (int64_t)m.p[1];
+  *nz = (int64_t)m.p[2];
+  *len = *nx + *ny + *nz + *nx * *ny * *nz;
+  return *nx * *ny * *nz < ((int64_t)1 << 31);
+}
 
 // Table slots: an upload takes the lowest free slot (freed ids are reused), so a loop that builds and
 // drops tables keeps the context's device memory flat.
@@ -159,6 +170,8 @@ static void build_directory(prom_ctx* ctx, prom::AtomTable& t, const double* x, 
     d[j] = (int32_t)(std::upper_bound(x, x + n, b) - x);
   }
   upload(t.dir, d.data(), nd + 1, ctx->stream);
+  t.rec.ensure(sizeof(double4) * n);
+  prom::launch_table_recs(ctx->stream, t.x.as<double>(), t.y.as<double>(), n, t.rec.as<double4>());
   t.hx.assign(x, x + n);
   t.n_dir = (int32_t)nd;
   t.dir_x0 = x0;
@@ -350,8 +363,9 @@ int32_t prom_number_density(prom_ctx* ctx, const prom_density_model* model, int3
                             int64_t n_chords, const double* y, const double* z, const double* body_x,
                             const double* body_y, double* n_out) {
   return guarded(ctx, [&] {
-    PROM_REQUIRE(model && valid_kind(model->kind) && model->kind != PROM_DENSITY_TABULATED,
-                 "prom_number_density: unknown or tabulated density kind");
+    PROM_REQUIRE(model && valid_kind(model->kind) && model->kind != PROM_DENSITY_TABULATED &&
+                     model->kind != PROM_DENSITY_GRIDDED,
+                 "prom_number_density: unknown, tabulated or gridded density kind (gridded: prom_gridded_density)");
     PROM_REQUIRE(n_x >= 0 && n_chords >= 0, "prom_number_density: bad sizes");
     upload(ctx->scratch[0], x, n_x, ctx->stream);
     upload(ctx->scratch[1], y, n_chords, ctx->stream);
@@ -363,6 +377,37 @@ int32_t prom_number_density(prom_ctx* ctx, const prom_density_model* model, int3
                          ctx->scratch[1].as<double>(), ctx->scratch[2].as<double>(), ctx->scratch[3].as<double>(),
                          ctx->scratch[4].as<double>(), n_chords, ctx->scratch[5].as<double>());
     download(n_out, ctx->scratch[5], n_chords * n_x, ctx->stream);
+    PROM_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int32_t prom_gridded_density(prom_ctx* ctx, int32_t n_gx, const double* gx, int32_t n_gy, const double* gy,
+                             int32_t n_gz, const double* gz, const double* values, int64_t n_points,
+                             const double* px, const double* py, const double* pz, double* out) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(n_gx >= 2 && n_gy >= 2 && n_gz >= 2 && gx && gy && gz && values,
+                 "prom_gridded_density: need >= 2 nodes per axis");
+    PROM_REQUIRE((int64_t)n_gx * n_gy * n_gz < ((int64_t)1 << 31), "prom_gridded_density: grid too large");
+    PROM_REQUIRE(n_points >= 0 && (n_points == 0 || (px && py && pz && out)), "prom_gridded_density: bad points");
+    for (const auto& ax : {std::make_pair(gx, n_gx), std::make_pair(gy, n_gy), std::make_pair(gz, n_gz)})
+      for (int32_t i = 1; i < ax.second; ++i)
+        PROM_REQUIRE(ax.first[i] > ax.first[i - 1], "prom_gridded_density: axes must be strictly ascending");
+    const int64_t nv = (int64_t)n_gx * n_gy * n_gz;
+    std::vector<double> g;
+    g.reserve(n_gx + n_gy + n_gz + nv);
+    g.insert(g.end(), gx, gx + n_gx);
+    g.insert(g.end(), gy, gy + n_gy);
+    g.insert(g.end(), gz, gz + n_gz);
+    g.insert(g.end(), values, values + nv);
+    upload(ctx->scratch[0], g.data(), (int64_t)g.size(), ctx->stream);
+    upload(ctx->scratch[1], px, n_points, ctx->stream);
+    upload(ctx->scratch[2], py, n_points, ctx->stream);
+    upload(ctx->scratch[3], pz, n_points, ctx->stream);
+    ctx->scratch[4].ensure(sizeof(double) * std::max<int64_t>(n_points, 1));
+    prom::launch_gridded(ctx->stream, ctx->scratch[0].as<double>(), n_gx, n_gy, n_gz, n_points,
+                         ctx->scratch[1].as<double>(), ctx->scratch[2].as<double>(), ctx->scratch[3].as<double>(),
+                         ctx->scratch[4].as<double>());
+    download(out, ctx->scratch[4], n_points, ctx->stream);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
   });
 }
@@ -428,6 +473,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         PROM_REQUIRE(S.n_tabulated, "transit: tabulated scenario without n_tabulated");
         tr.tab_off[sc] = tab_total;
         tab_total += n_orb * tr.n_pr * tr.n_x;
+      } else if (S.density.kind == PROM_DENSITY_GRIDDED) {
+        int64_t gnx, gny, gnz, glen;
+        PROM_REQUIRE(S.n_tabulated && gridded_dims(S.density, &gnx, &gny, &gnz, &glen),
+                     "transit: gridded scenario needs p = {n_gx, n_gy, n_gz} (>= 2 each) and the packed grid");
+        tr.tab_off[sc] = tab_total;
+        tab_total += glen;
       } else {
         PROM_REQUIRE(S.body_x && S.body_y, "transit: scenario body position missing");
       }
@@ -502,6 +553,16 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
             if (std::isfinite(v) && v > m) m = v;
           }
           nref[sc] = m;
+        } else if (S.density.kind == PROM_DENSITY_GRIDDED) {
+          // a trilinear value is a convex combination of corners (weights sum to 1 within rounding)
+          int64_t gnx, gny, gnz, glen;
+          gridded_dims(S.density, &gnx, &gny, &gnz, &glen);
+          double m = 0.0;
+          for (int64_t i = gnx + gny + gnz; i < glen; ++i) {
+            const double v = std::fabs(S.n_tabulated[i]);
+            if (std::isfinite(v) && v > m) m = v;
+          }
+          nref[sc] = m * (1.0 + 1e-9);
         } else {
           // p[0] bounds the built-in profile only where it decays away from its body: a growing power
           // law (q < 0), a negative scale height, a hydrostatic J_0 below J(R) or a negative n_0 would
@@ -530,7 +591,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         const double inv = (c > 0.0 && std::isfinite(c)) ? bound : 0.0;
         st.push_back({tb.x.as<double>(), tb.y.as<double>(), tb.n, tb.offset,
                       tr.shift.as<double>() + (int64_t)t.scenario * n_orb, tb.dir.as<int32_t>(), tb.n_dir, 0,
-                      tb.dir_x0, tb.dir_inv_h, std::isfinite(c) ? c : 0.0, inv, t.chi, tb.hx.front(), tb.hx.back()});
+                      tb.dir_x0, tb.dir_inv_h, std::isfinite(c) ? c : 0.0, inv, t.chi, tb.hx.front(), tb.hx.back(),
+                      tb.rec.as<double4>()});
       }
       // species merging: one scenario carries every atomic constituent (and there are >= 2 of them)
       int32_t sc0 = -1;
@@ -571,13 +633,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       }
       tr.sigtab_v = prom::SigTabs4{};
       for (size_t i = 0; i < st.size() && i < 4; ++i) tr.sigtab_v.t[i] = st[i];
-      // sigma segments of the Doppler rows (k_columns8 sigma_rows_block): per 256-wavelength block and
-      // atomic slot, nodes [lo, hi] with X[lo] <= fl(s_min lambda_first) and fl(s_max lambda_last) < X[hi]
-      // (numpy's bracket j of a target: the largest j <= n-2 with X[j] <= t)
+      // sigma segments of the Doppler rows (k_sigma_rows): per 256-wavelength block and atomic slot, nodes
+      // [lo, hi] with X[lo] <= fl(s_min lambda_first) and fl(s_max lambda_last) < X[hi] (numpy's bracket j of
+      // a target: the largest j <= n-2 with X[j] <= t), and a linear bracket guess verified over the slice
       tr.sig_seg_ok = false;
       if (!tr.uniform_shift && n_atoms >= 1 && n_atoms <= 4) {
         const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
-        std::vector<int32_t> seg(2 * nb * n_atoms, 0);
+        std::vector<prom::SigSeg> seg(nb * n_atoms, prom::SigSeg{0, 0, 0, 0, 0.0, 0.0});
         int32_t ia = 0;
         for (const auto& t : tr.terms) {
           if (t.is_molecule) continue;
@@ -607,16 +669,51 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
             }
             if (!fin) continue;
             const double tlo = smin * lmin, thi = smax * lmax;
+            // every target inside [x_0, x_{n-1}): no clamp or end rule
+            if (!(tlo >= X[0] && thi < X[n - 1])) continue;
             const int64_t lo = bracket(tlo);
-            const int64_t hi = thi >= X[n - 1] ? n - 1 : bracket(thi) + 1;
+            const int64_t hi = bracket(thi) + 1;
             const int64_t m = hi - lo + 1;
-            if (m < 2 || m > prom::kSigSeg) continue;
-            seg[2 * (b * n_atoms + ia)] = (int32_t)lo;
-            seg[2 * (b * n_atoms + ia) + 1] = (int32_t)m;
+            if (m < 2 || m > INT32_MAX / 2) continue;
+            prom::SigSeg& e = seg[b * n_atoms + ia];
+            e.lo = (int32_t)lo;
+            e.m = (int32_t)m;
+            // linear guess over the slice, verified at both ends of every node interval (g and numpy's
+            // bracket are monotone step functions, and the bracket is constant inside an interval)
+            const double xs = X[lo], span = X[hi] - X[lo];
+            const double inv = span > 0.0 ? (double)(m - 1) / span : 0.0;
+            bool lin = span > 0.0 && std::isfinite(inv);
+            auto guess = [&](double v) -> int64_t {
+              const double f = (v - xs) * inv;
+              int64_t g = f < 0.0 ? 0 : (f >= (double)(m - 2) ? m - 2 : (int64_t)f);
+              return g;
+            };
+            for (int64_t i = lo; lin && i < hi; ++i) {
+              if (X[i] == X[i + 1]) continue;
+              const double a = std::max(X[i], tlo), z = std::nextafter(X[i + 1], -INFINITY);
+              if (a > z) continue;
+              const int64_t k = i - lo;   // numpy's bracket on [X[i], X[i+1]) (i <= hi - 1 <= n - 2)
+              const int64_t ga = guess(a), gz = guess(z);
+              if (ga < k - 1 || ga > k + 1 || gz < k - 1 || gz > k + 1) lin = false;
+            }
+            if (lin) {
+              e.kind = m <= prom::kSigSeg ? 1 : 2;
+              e.xs = xs;
+              e.inv = inv;
+            }
           }
           ++ia;
         }
         upload(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
+        std::vector<int32_t> fbl;
+        for (int64_t b = 0; b < nb; ++b) {
+          bool lds = true;
+          for (int32_t a = 0; a < n_atoms; ++a) lds = lds && seg[b * n_atoms + a].kind == 1;
+          if (!lds) fbl.push_back((int32_t)b);
+        }
+        tr.n_sig_fb = (int32_t)fbl.size();
+        if (fbl.empty()) fbl.push_back(0);
+        upload(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
         tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
       }
     }
@@ -634,7 +731,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       PROM_REQUIRE(sb.offset == 0.0, "transit: the star table must have offset 0 (n_interp_log(..., 0.0))");
       tr.star_tab = prom::SigTabDev{sb.x.as<double>(), sb.y.as<double>(), sb.n, sb.offset, nullptr,
                                     sb.dir.as<int32_t>(), sb.n_dir, 0, sb.dir_x0, sb.dir_inv_h, 0.0, 0.0, 0.0,
-                                    sb.hx.front(), sb.hx.back()};
+                                    sb.hx.front(), sb.hx.back(), sb.rec.as<double4>()};
       upload(tr.crho, pb->chord_rho, tr.n_pr, s);
       upload(tr.cclv, pb->chord_clv, tr.n_pr, s);
       upload(tr.cshift, pb->chord_star_shift, tr.n_pr, s);
@@ -694,9 +791,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       for (int32_t i = 0; i < tr.n_terms && i < 8; ++i) tr.colargs.t[i] = tr.terms[i];
     }
     for (int32_t sc = 0; sc < tr.n_sc; ++sc)
-      if (tr.tab_off[sc] >= 0)
+      if (tr.tab_off[sc] >= 0) {
+        int64_t len = n_orb * tr.n_pr * tr.n_x, gnx, gny, gnz;
+        if (pb->scenarios[sc].density.kind == PROM_DENSITY_GRIDDED)
+          gridded_dims(pb->scenarios[sc].density, &gnx, &gny, &gnz, &len);
         PROM_HIP(hipMemcpyAsync(tr.tab.as<double>() + tr.tab_off[sc], pb->scenarios[sc].n_tabulated,
-                                sizeof(double) * n_orb * tr.n_pr * tr.n_x, hipMemcpyHostToDevice, s));
+                                sizeof(double) * len, hipMemcpyHostToDevice, s));
+      }
     // work buffers
     const int64_t nc = n_orb * tr.n_pr;
     tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);

@@ -194,6 +194,24 @@ __device__ __forceinline__ double lane_read(double v, int l) {
 }
 __device__ __forceinline__ int32_t lane_read(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// op over all 64 lanes of a float (every lane active), on DPP moves and four readlanes: no LDS traffic
+template <int CTRL>
+__device__ __forceinline__ float dpp_movf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <typename Op>
+__device__ __forceinline__ float wave_reduce_f(float v, Op op) {
+  v = op(v, dpp_movf<0xB1>(v));    // quad_perm [1,0,3,2]
+  v = op(v, dpp_movf<0x4E>(v));    // quad_perm [2,3,0,1]
+  v = op(v, dpp_movf<0x141>(v));   // row_half_mirror
+  v = op(v, dpp_movf<0x140>(v));   // row_mirror
+  const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return op(op(a, b), op(c, d));
+}
+
 // inclusive prefix over lanes 0..63 (op applied as op(earlier, later))
 template <typename T, typename Op>
 __device__ __forceinline__ T wave_prefix(T v, Op op) {
@@ -590,6 +608,27 @@ __device__ __forceinline__ double mol_value(const double* __restrict__ V, int32_
     value = value + V[((ip + dp) * n_t + (it + dt)) * n_w + (iw + dw)] * weight;
   }
   return value;
+}
+
+// SerpensExosphere's density (gasProperties.py:583-601): scipy RegularGridInterpolator (linear) of the
+// packed grid g = [gx[nx], gy[ny], gz[nz], values[nx][ny][nz]] at (x, y, z); NaN outside (bounds_error).
+// Same brackets, weights and corner order as the molecular lookup (mol_value).
+__device__ __forceinline__ double grid_value(const double* __restrict__ g, int32_t nx, int32_t ny, int32_t nz,
+                                             double x, double y, double z) {
+  const double* gx = g;
+  const double* gy = gx + nx;
+  const double* gz = gy + ny;
+  const double* V = gz + nz;
+  int64_t ix, iy, iz;
+  double tx, ty, tz;
+  if (!rgi_bracket(gx, nx, x, &ix, &tx) || !rgi_bracket(gy, ny, y, &iy, &ty) || !rgi_bracket(gz, nz, z, &iz, &tz))
+    return __builtin_nan("");
+  return mol_value(V, ny, nz, ix, tx, iy, ty, iz, tz);
+}
+
+__device__ __forceinline__ double grid_density(const DensityDev& m, const double* __restrict__ g, double xv,
+                                               double y, double z, double bx, double by) {
+  return grid_value(g, (int32_t)m.p[0], (int32_t)m.p[1], (int32_t)m.p[2], xv - bx, y - by, z);
 }
 
 }  // namespace prom

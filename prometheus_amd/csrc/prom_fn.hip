@@ -106,6 +106,41 @@ void launch_molecular_sigma(hipStream_t s, const MolTable& t, int64_t n_chords, 
   PROM_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------------------------ gridded density (SERPENS)
+__global__ void k_gridded(const double* __restrict__ g, int32_t nx, int32_t ny, int32_t nz, int64_t n,
+                          const double* __restrict__ px, const double* __restrict__ py,
+                          const double* __restrict__ pz, double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  if (i >= n) return;
+  out[i] = grid_value(g, nx, ny, nz, px[i], py[i], pz[i]);
+}
+
+void launch_gridded(hipStream_t s, const double* g, int32_t nx, int32_t ny, int32_t nz, int64_t n,
+                    const double* px, const double* py, const double* pz, double* out) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gridded, dim3(grid_for(n, kBlock, (int64_t)1 << 31)), dim3(kBlock), 0, s, g, nx, ny, nz,
+                     n, px, py, pz, out);
+  PROM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ interval records
+// rec[i] = {x_i, y_i, numpy.interp's slope of [x_i, x_{i+1}], 0}: the Doppler-row lookups read a bracket's
+// node and slope in one 32-byte record (the same IEEE division as sigma_of's)
+__global__ void k_table_recs(const double* __restrict__ x, const double* __restrict__ y, int64_t n,
+                             double4* __restrict__ rec) {
+  const int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double xv = x[i], yv = y[i];
+  const double sl = i + 1 < n ? (y[i + 1] - yv) / (x[i + 1] - xv) : 0.0;
+  rec[i] = make_double4(xv, yv, sl, 0.0);
+}
+
+void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_table_recs, dim3(grid_for(n, kBlock, (int64_t)1 << 31)), dim3(kBlock), 0, s, x, y, n, rec);
+  PROM_HIP(hipGetLastError());
+}
+
 // ------------------------------------------------------------------ reductions
 __global__ void k_max(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
   __shared__ double sm[kBlock];

@@ -78,8 +78,9 @@ inline int n_tail_moments(int S) { return S == 1 ? 8 : (S + 1) * (S + 2) * (S + 
 
 // Doppler cross-section rows: table nodes a resampling workgroup stages in LDS per species (prom_api.hip
 // sigma segments; larger slices gather from the global table).
-constexpr int kSigSeg = 1024;
+constexpr int kSigSeg = 512;
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
+constexpr int kSigRowChunk = 8;   // rows per resampling workgroup
 
 // Stellar-spectrum path: star-table nodes a tau workgroup stages in LDS (prom_api.hip rm_slices).
 constexpr int kRmStarMax = 1024;
@@ -121,6 +122,17 @@ struct SigTabDev {
   double nscale;         // 1 / c_s (0 when c_s == 0)
   double chi;            // the constituent's mixing ratio (species merging: Y = sum_s chi_s sigma_s)
   double xfirst, xlast;  // x[0], x[n - 1] (range test without a dependent load)
+  const double4* rec;    // [n] {x_i, y_i, slope_i = (y_{i+1} - y_i) / (x_{i+1} - x_i), 0} (AtomTable::rec)
+};
+
+// Per 256-wavelength block and atomic slot of a Doppler-row problem (prom_api.hip sigma segments): the
+// table nodes [lo, lo + m) every row's targets fall between, and, for kind > 0, a linear bracket guess
+// g(t) = clamp((int)((t - xs) * inv), 0, m - 2) that the host verified to be within one node of numpy's
+// bracket for every target in the slice.  kind 0: no guess (general lookup); 1: the slice fits in LDS;
+// 2: too large for LDS, the guess indexes the global records.
+struct SigSeg {
+  int32_t lo, m, kind, pad;
+  double xs, inv;
 };
 
 // Per molecular slot of a transit problem.
@@ -161,6 +173,7 @@ struct AtomTable {
   // bucket directory for O(1) bracketing: dir[j] = #{i : x[i] <= x0 + j h}, j = 0 .. n_dir,
   // h = (x[n-1] - x0) / n_dir (prom_api.hip build_directory)
   DevBuf dir;
+  DevBuf rec;               // [n] double4 {x, y, slope, 0} (k_table_recs)
   std::vector<double> hx;   // host copy of x (stellar-spectrum slice bounds)
   int32_t n_dir = 0;
   double dir_x0 = 0.0, dir_inv_h = 0.0;
@@ -265,7 +278,9 @@ struct TransitDev {
   DevBuf rm_slices;                         // [n_wav tiles of kBlock][3] {lo, m, half}: LDS slice
   // orbital Doppler shift: per 256-wavelength block and atomic slot, the table nodes {lo, m} every
   // phase's shifted targets fall between (m = 0: more than kSigSeg, the block gathers per target)
-  DevBuf sig_seg;                           // [n_wav blocks][n_atoms] int2
+  DevBuf sig_seg;                           // [n_wav blocks][n_atoms] SigSeg
+  DevBuf sig_fb;                            // blocks with an oversize slice (m = 0 for some species)
+  int32_t n_sig_fb = 0;
   bool sig_seg_ok = false;
   RunSlot slot[kMaxSlots];
   // PROM_GRAPH=1: a fast-path run is one hipGraph per slot, captured at the slot's first untimed run
@@ -316,12 +331,17 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events);
 // orbital Doppler shift: the per-phase cross-section rows, Y or sigma_s, and the Q ranges (prom_sigma.hip)
 void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
-                       int32_t n_rows, const int2* seg, double* sig, float4* tq, int32_t merge_sp, double nscale_m,
-                       uint8_t* zfl, hipEvent_t ev_start);
+                       int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start);
 // the fused tau kernels of the molecular and stellar-spectrum paths (prom_mol.hip, prom_rm.hip)
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
+// prom_gridded_density (prom_fn.hip)
+void launch_gridded(hipStream_t s, const double* g, int32_t nx, int32_t ny, int32_t nz, int64_t n,
+                    const double* px, const double* py, const double* pz, double* out);
+// AtomTable::rec from a table's x and y (prom_fn.hip)
+void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec);
 // per phase: sum / count of R over the band-selected wavelengths, max of R over all (prom_transit_band_stats)
 void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,
                        int32_t n_bands, const double* bounds, double* sum, int64_t* count, double* mx);

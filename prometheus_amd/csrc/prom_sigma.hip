@@ -4,149 +4,203 @@
 
 namespace prom {
 
-constexpr int kSigRowChunk = 8;   // rows kept in registers per pass over the species
 static_assert(kSigBlockW == kBlock, "sigma segments are built per kBlock wavelengths");
+constexpr int kSigFbRows = 4;   // rows per gathering workgroup (independent lookups in flight per lane)
 
 // ---- Doppler-shifted cross-section rows (orbital Doppler shift: one row per phase) ----------------
-// One workgroup per 256-wavelength block, a thread per wavelength, looping over the rows (phases).
-// The host (prom_api.hip sigma segments) gives, per block and atomic slot, the table nodes
-// [lo, lo + m) that every row's shifted targets shift_o * lambda_w fall between: positive factors
-// and IEEE multiplication are monotone, so fl(shift_o lambda_w) lies in [fl(s_min lambda_first),
-// fl(s_max lambda_last)].  Those nodes go to LDS once per 8 rows, with numpy.interp's slope of
-// each interval divided once per node instead of once per target; a target's bracket is a
-// bisection of the slice for a chunk's first row, then a short walk from the previous row's
-// bracket (the rows' factors are close).  Blocks whose slice exceeds kSigSeg nodes (the
-// high-resolution line windows, where the table is 10x finer than the grid) keep the per-target
-// directory gather of sigma_of.  Same bracket rule, slope, products and exp10 as sigma_of /
-// sigma_multi: the rows are bit-for-bit those of the per-target lookups.
-static_assert(kSigBlockW == kBlock, "sigma segments are built per kBlock wavelengths");
+// The host (prom_api.hip sigma segments) gives, per 256-wavelength block and atomic slot, the table nodes
+// [lo, lo + m) that every row's shifted targets shift_o * lambda_w fall between: positive factors and
+// IEEE multiplication are monotone, so fl(shift_o lambda_w) lies in [fl(s_min lambda_first),
+// fl(s_max lambda_last)].  Same bracket rule, slope, products and exp10 as sigma_of / sigma_multi: the
+// rows are bit-for-bit those of the per-target lookups.
 
+// One row's outputs at one wavelength: the cross sections (or the merged absorber Y and its zero flag)
+// and the row's Q range over each 64-wavelength half tile (wavefront min / max, widened by 2^-20).
+template <int NSIG>
+__device__ __forceinline__ void sigma_row_out(int32_t orow, int32_t nse, const double (&v)[NSIG], const SigTabs4& tabv,
+                                              bool live, int64_t w, int64_t n_wav, int64_t hw, int64_t n_halves,
+                                              int lane, int32_t merge_sp, double nscale_m, double* __restrict__ sig,
+                                              float4* __restrict__ tq, uint8_t* __restrict__ zfl) {
+  double Qv = 0.0;
+  if (merge_sp) {
+    double Y = 0.0;
+    bool z = false;
+#pragma unroll
+    for (int s = 0; s < NSIG; ++s) {
+      const double cv = tabv.t[s].chi * v[s];
+      if (!(cv > 0.0)) z = true;
+      Y += cv;
+    }
+    if (live) {
+      sig[(int64_t)orow * n_wav + w] = Y;
+      zfl[(int64_t)orow * n_wav + w] = z ? 1u : 0u;
+    }
+    const double qs = Y * nscale_m;
+    Qv = qs > 0.0 ? qs : 0.0;
+  } else {
+#pragma unroll
+    for (int s = 0; s < NSIG; ++s) {
+      if (live) sig[((int64_t)orow * nse + s) * n_wav + w] = v[s];
+      const double qs = v[s] * tabv.t[s].nscale;
+      Qv += qs > 0.0 ? qs : 0.0;
+    }
+  }
+  const float qf = (float)Qv;
+  const float qh = wave_reduce_f(qf * (1.0f + 0x1p-20f), [](float a, float b) { return fmaxf(a, b); });
+  const float ql = wave_reduce_f(qf * (1.0f - 0x1p-20f), [](float a, float b) { return fminf(a, b); });
+  const bool bad = __ballot(!(Qv <= 1.0e100)) != 0ull;
+  if (lane == 0 && hw < n_halves)
+    reinterpret_cast<float2*>(tq)[(int64_t)orow * n_halves + hw] = bad ? make_float2(-1.0f, 0.0f) : make_float2(ql, qh);
+}
+
+// numpy.interp of one target from its bracket guess g (within one node of the bracket, SigSeg): x_g and
+// x_{g+1} decide between g - 1, g and g + 1, then the bracket's record {x, f, slope} gives the value --
+// two dependent reads, no branches on the common path.  X2(g) reads x_g and x_{g+1}, REC(k, ...) node k's
+// x, f and slope.
+template <class XF, class RF>
+__device__ __forceinline__ double interp_guess(double t, int32_t g, XF X2, RF REC) {
+  const double2 xg = X2(g);   // x_g, x_{g+1}
+  const int32_t k = t < xg.x ? g - 1 : (t >= xg.y ? g + 1 : g);
+  double xa, fa, sl;
+  REC(k, xa, fa, sl);
+  double rv;
+  if (xa == t) rv = fa;
+  else {
+    rv = sl * (t - xa) + fa;
+    if (rv != rv) {   // numpy's retry from the right node
+      double xb, fb, sb;
+      REC(k + 1, xb, fb, sb);
+      rv = sl * (t - xb) + fb;
+      if (rv != rv && fa == fb) rv = fa;
+    }
+  }
+  return rv;
+}
+
+__device__ __forceinline__ int32_t seg_guess(double t, double xs, double inv, int32_t m) {
+  const double f = (t - xs) * inv;
+  return f < 0.0 ? 0 : (f >= (double)(m - 2) ? m - 2 : (int32_t)f);
+}
+
+// Workgroups [0, n_blk * n_rc): one per (256-wavelength block whose slices all fit in LDS, chunk of
+// kSigRowChunk rows).  Per species the block's node records go to LDS; a target's bracket comes from the
+// slice's verified linear guess (interp_guess), so the rows' lookups are independent and their LDS round
+// trips overlap.
+// Workgroups [n_blk * n_rc, + n_fb * ceil(n_rows / kSigFbRows)): one per (other block, chunk of
+// kSigFbRows rows) -- a species of these blocks has
+// a slice larger than kSigSeg nodes (the high-resolution line windows, where the refined table is 10x
+// finer than the grid and the rows' shifts spread the targets over thousands of nodes: the guess then
+// reads the global records) or no verified guess (slices straddling a change of node spacing, targets
+// outside the table: sigma_of's directory lookup).
 template <int NSIG>
 __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
-                                                 int32_t n_rows, const int2* __restrict__ seg,
+                                                 int32_t n_rows, const SigSeg* __restrict__ seg,
+                                                 const int32_t* __restrict__ fb, int32_t n_blk, int32_t n_rc,
                                                  double* __restrict__ sig, float4* __restrict__ tq, int32_t merge_sp,
                                                  double nscale_m, uint8_t* __restrict__ zfl) {
-  __shared__ double sx[kSigSeg], sy[kSigSeg], ss[kSigSeg];
-  const int64_t wb = blockIdx.x;
+  // the slice as three conflict-free arrays: x (bracket tests), (x, f) pairs and slopes (the value)
+  __shared__ double sx[kSigSeg];
+  __shared__ double2 sxf[kSigSeg];
+  __shared__ double ssl[kSigSeg];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int64_t w = wb * kBlock + tid;
-  const bool live = w < n_wav;
-  const double lam = wav[live ? w : n_wav - 1];
   const int64_t n_halves = 2 * ((n_wav + kTW - 1) / kTW);
-  const int64_t hw = wb * (kBlock / 64) + (tid >> 6);
   const int32_t nse = merge_sp ? 1 : NSIG;
-  for (int32_t r0 = 0; r0 < n_rows; r0 += kSigRowChunk) {
-    double Y[kSigRowChunk], Q[kSigRowChunk];
-    uint32_t zbits = 0;
-#pragma unroll
-    for (int r = 0; r < kSigRowChunk; ++r) { Y[r] = 0.0; Q[r] = 0.0; }
+  const int64_t n_main = (int64_t)n_blk * n_rc;
+  if ((int64_t)blockIdx.x >= n_main) {
+    const int64_t item = (int64_t)blockIdx.x - n_main;
+    const int32_t n_fc = (n_rows + kSigFbRows - 1) / kSigFbRows;
+    const int32_t f0 = (int32_t)(item % n_fc) * kSigFbRows;
+    const int64_t wb = fb[item / n_fc];
+    const int64_t w = wb * kBlock + tid;
+    const bool live = w < n_wav;
+    const double lam = wav[live ? w : n_wav - 1];
+    double v[kSigFbRows][NSIG];
 #pragma unroll
     for (int s = 0; s < NSIG; ++s) {
       const SigTabDev& tb = tabv.t[s];
-      const int2 sg = seg[wb * NSIG + s];
-      const int32_t m = sg.y;
-      __syncthreads();   // the previous species' slice is no longer read
-      if (m > 0) {
-        for (int32_t i = tid; i < m; i += kBlock) {
-          const double xv = tb.x[sg.x + i], yv = tb.y[sg.x + i];
-          sx[i] = xv;
-          sy[i] = yv;
-          if (i + 1 < m) {
-            const double xn = tb.x[sg.x + i + 1], yn = tb.y[sg.x + i + 1];
-            ss[i] = (yn - yv) / (xn - xv);
-          }
-        }
-      }
-      __syncthreads();
-      const double f_first = tb.y[0], f_last = tb.y[tb.n - 1];
-      int32_t k = 0;
-      if (m > 0) {   // the chunk's first row: bisection, sx[a] <= t < sx[b] (out-of-range t: an end)
-        const double t = tb.shift[r0] * lam;
-        int32_t a = 0, b = m - 1;
-        while (b - a > 1) {
-          const int32_t mid = (a + b) >> 1;
-          if (sx[mid] <= t) a = mid; else b = mid;
-        }
-        k = a;
-      }
+      const SigSeg sg = seg[wb * NSIG + s];
+      const double4* __restrict__ rc = tb.rec + sg.lo;
 #pragma unroll
-      for (int r = 0; r < kSigRowChunk; ++r) {
-        const int32_t orow = r0 + r;
-        if (orow >= n_rows) break;
+      for (int r = 0; r < kSigFbRows; ++r) {
+        const int32_t orow = f0 + r < n_rows ? f0 + r : n_rows - 1;
         const double t = tb.shift[orow] * lam;
-        double v;
-        if (m > 0) {
-          double rv;
-          if (t != t) rv = t;
-          else if (!(t >= tb.xfirst)) rv = f_first;
-          else if (t >= tb.xlast) rv = f_last;
-          else {
-            // walk from the previous row's bracket (the rows' factors are close)
-            while (k > 0 && sx[k] > t) --k;
-            while (k < m - 2 && sx[k + 1] <= t) ++k;
-            const double xa = sx[k], fa = sy[k];
-            if (xa == t) rv = fa;
-            else {
-              const double slope = ss[k];
-              rv = slope * (t - xa) + fa;
-              if (rv != rv) {
-                const double xb = sx[k + 1], fb = sy[k + 1];
-                rv = slope * (t - xb) + fb;
-                if (rv != rv && fa == fb) rv = fa;
-              }
-            }
-          }
-          v = exp10(rv) - tb.offset;
+        if (sg.kind > 0) {
+          const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+          v[r][s] = exp10(interp_guess(
+                        t, g, [&](int32_t i) { return make_double2(rc[i].x, rc[i + 1].x); },
+                        [&](int32_t i, double& x, double& f, double& sl) {
+                          const double4 q = rc[i];
+                          x = q.x; f = q.y; sl = q.z;
+                        })) - tb.offset;
         } else {
-          v = sigma_of(t, tb);
-        }
-        if (merge_sp) {
-          const double cv = tb.chi * v;
-          if (!(cv > 0.0)) zbits |= 1u << r;
-          Y[r] += cv;
-        } else {
-          if (live) sig[((int64_t)orow * nse + s) * n_wav + w] = v;
-          const double qs = v * tb.nscale;
-          Q[r] += qs > 0.0 ? qs : 0.0;
+          v[r][s] = sigma_of(t, tb);
         }
       }
     }
+    const int64_t hw = wb * (kBlock / 64) + (tid >> 6);
+#pragma unroll
+    for (int r = 0; r < kSigFbRows; ++r) {
+      if (f0 + r >= n_rows) break;
+      sigma_row_out<NSIG>(f0 + r, nse, v[r], tabv, live, w, n_wav, hw, n_halves, lane, merge_sp, nscale_m, sig, tq, zfl);
+    }
+    return;
+  }
+  const int64_t wb = blockIdx.x / n_rc;
+  const int32_t r0 = (int32_t)(blockIdx.x % n_rc) * kSigRowChunk;
+  bool lds_ok = true;
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && seg[wb * NSIG + s].kind == 1;
+  if (!lds_ok) return;   // its rows are the trailing workgroups'
+  const int64_t w = wb * kBlock + tid;
+  const bool live = w < n_wav;
+  const double lam = wav[live ? w : n_wav - 1];
+  const int64_t hw = wb * (kBlock / 64) + (tid >> 6);
+  double V[kSigRowChunk][NSIG];
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) {
+    const SigTabDev& tb = tabv.t[s];
+    const SigSeg sg = seg[wb * NSIG + s];
+    if (s > 0) __syncthreads();   // the previous species' slice is no longer read
+    for (int32_t i = tid; i < sg.m; i += kBlock) {
+      const double4 q = tb.rec[sg.lo + i];
+      sx[i] = q.x;
+      sxf[i] = make_double2(q.x, q.y);
+      ssl[i] = q.z;
+    }
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSigRowChunk; ++r) {
-      const int32_t orow = r0 + r;
-      if (orow >= n_rows) break;
-      double Qv = Q[r];
-      if (merge_sp) {
-        if (live) {
-          sig[(int64_t)orow * n_wav + w] = Y[r];
-          zfl[(int64_t)orow * n_wav + w] = (zbits >> r) & 1u;
-        }
-        const double qs = Y[r] * nscale_m;
-        Qv = qs > 0.0 ? qs : 0.0;
-      }
-      const float qf = (float)Qv;
-      float qh = qf * (1.0f + 0x1p-20f), ql = qf * (1.0f - 0x1p-20f);
-      for (int off = 32; off > 0; off >>= 1) {
-        qh = fmaxf(qh, __shfl_xor(qh, off, 64));
-        ql = fminf(ql, __shfl_xor(ql, off, 64));
-      }
-      const bool bad = __ballot(!(Qv <= 1.0e100)) != 0ull;
-      if (lane == 0 && hw < n_halves)
-        reinterpret_cast<float2*>(tq)[(int64_t)orow * n_halves + hw] =
-            bad ? make_float2(-1.0f, 0.0f) : make_float2(ql, qh);
+      const int32_t orow = r0 + r < n_rows ? r0 + r : n_rows - 1;
+      const double t = tb.shift[orow] * lam;
+      const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+      V[r][s] = exp10(interp_guess(
+                    t, g, [&](int32_t i) { return make_double2(sx[i], sx[i + 1]); },
+                    [&](int32_t i, double& x, double& f, double& sl) {
+                      const double2 q = sxf[i];
+                      x = q.x; f = q.y; sl = ssl[i];
+                    })) - tb.offset;
     }
+  }
+#pragma unroll
+  for (int r = 0; r < kSigRowChunk; ++r) {
+    const int32_t orow = r0 + r;
+    if (orow >= n_rows) break;
+    sigma_row_out<NSIG>(orow, nse, V[r], tabv, live, w, n_wav, hw, n_halves, lane, merge_sp, nscale_m, sig, tq, zfl);
   }
 }
 
 
 void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
-                       int32_t n_rows, const int2* seg, double* sig, float4* tq, int32_t merge_sp, double nscale_m,
-                       uint8_t* zfl, hipEvent_t ev_start) {
-  const unsigned nb = grid_for(n_wav);
+                       int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start) {
+  const int32_t n_blk = (int32_t)grid_for(n_wav);
+  const int32_t n_rc = (n_rows + kSigRowChunk - 1) / kSigRowChunk;
+  const int32_t n_fc = (n_rows + kSigFbRows - 1) / kSigFbRows;
+  const unsigned nb = (unsigned)((int64_t)n_blk * n_rc + (int64_t)n_fb * n_fc);
 #define PROM_SIGR(NS)                                                                                        \
   hipExtLaunchKernelGGL((k_sigma_rows<NS>), dim3(nb), dim3(kBlock), 0, s, ev_start, nullptr, 0, tabv, wav, n_wav, \
-                        n_rows, seg, sig, tq, merge_sp, nscale_m, zfl)
+                        n_rows, seg, fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl)
   switch (nsig) {
     case 1: PROM_SIGR(1); break;
     case 2: PROM_SIGR(2); break;

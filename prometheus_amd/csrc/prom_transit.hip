@@ -35,6 +35,8 @@ __global__ void k_ntot(DensityDev m, int32_t sc, const double* __restrict__ x, i
     double v;
     if (m.kind == PROM_DENSITY_TABULATED)
       v = tab[((int64_t)ip * n_orb + o) * n_x + ix];
+    else if (m.kind == PROM_DENSITY_GRIDDED)
+      v = grid_density(m, tab, x[ix], cy[ip], cz[ip], bx[sc * n_orb + o], by[sc * n_orb + o]);
     else
       v = density_at(m, x[ix], cy[ip], cz[ip], bx[sc * n_orb + o], by[sc * n_orb + o]);
     ntot[(int64_t)sc * per + i] = v;
@@ -118,7 +120,8 @@ __global__ void k_columns(const TermDev* __restrict__ terms, int32_t n_terms,
   }
 }
 
-// Per-scenario device view for the streaming column kernel (tab: TABULATED n[(ip*n_orb+o)*n_x+ix]).
+// Per-scenario device view for the streaming column kernel (tab: TABULATED n[(ip*n_orb+o)*n_x+ix], or
+// GRIDDED's packed grid).
 using ScDev = ScDevHost;
 
 // Blocking masks + column densities + transparency culling in one pass for atomic-only problems with
@@ -259,7 +262,8 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
         const int32_t i = gl + 8 * k;
         nv[k] = 0.0;
         if (valid && !blocked && i < n_x)
-          nv[k] = sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + i] : density_at(sc.m, xs[k], y, z, bxo, byo);
+          nv[k] = sc.m.kind == PROM_DENSITY_GRIDDED ? grid_density(sc.m, sc.tab, xs[k], y, z, bxo, byo)
+                  : sc.tab ? sc.tab[((int64_t)ip * n_orb + o) * n_x + i] : density_at(sc.m, xs[k], y, z, bxo, byo);
       }
     }
     double av[SPL];
@@ -1990,8 +1994,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
     const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
     if (rows_seg) {
-      launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<int2>(),
-                        rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale,
+      launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
+                        tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale,
                         rs.zfl.as<uint8_t>(), ev0);
       ev0 = nullptr;
     }
@@ -2024,7 +2028,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
       const DensityDev& m = tr.dens[sc];
       const double* tab = nullptr;
-      if (m.kind == PROM_DENSITY_TABULATED) tab = tr.tab.as<double>() + tr.tab_off[sc];
+      if (m.kind == PROM_DENSITY_TABULATED || m.kind == PROM_DENSITY_GRIDDED) tab = tr.tab.as<double>() + tr.tab_off[sc];
       hipLaunchKernelGGL(k_ntot, dim3(grid_for(per)), dim3(kBlock), 0, s, m, sc, tr.x.as<double>(), tr.n_x,
                          tr.cy.as<double>(), tr.cz.as<double>(), tr.n_pr, tr.n_orb, tr.body_x.as<double>(),
                          tr.body_y.as<double>(), tab, tr.ntot.as<double>());

@@ -290,8 +290,15 @@ class TorusExosphere(EvaporativeExosphere):
 
 
 class SerpensExosphere(EvaporativeExosphere):
-    """SERPENS particle-cloud density (gasProperties.py:519-601).  Out of the fused path's scope
-    (SURVEY.md §8f rank 3): it is a host plugin, tabulated onto the device like any user plugin."""
+    """SERPENS particle cloud (gasProperties.py:519-601): the particles are histogrammed onto a 3-D grid
+    (numpy, once, as the reference does) and the density is scipy's RegularGridInterpolator (linear) of
+    that grid, sampled on the device (PROM_DENSITY_GRIDDED, ``prom_gridded_density``).
+
+    The grid is fixed in the star frame: the density does not depend on the orbital phase
+    (``calculateNumberDensity`` ignores ``orbphase``, :587-601).  Unlike the reference, whose
+    ``calculateNumberDensity`` builds a ragged coordinate array for batched chords and fails inside
+    ``getLOSopticalDepth_Batch`` (:905), chords may be batched: phi, rho of shape (B,) give n of shape
+    (B, n_x), each row equal to the reference's scalar call for that chord."""
 
     def __init__(self, filename: str, N: float, planet: Any, sigmaSmoothing: float):
         super().__init__(N)
@@ -299,12 +306,62 @@ class SerpensExosphere(EvaporativeExosphere):
         self.planet = planet
         self.sigmaSmoothing = sigmaSmoothing
 
+    def addInterpolatedDensity(self, spatialGrid: Any) -> None:
+        """Histogram the SERPENS particles (file in m, one particle per row, x y z first) onto the
+        spatial grid's cells and keep the grid for the device sampler (:548-583)."""
+        serpensOutput = np.loadtxt(self.filename) * 1e2
+        particlePos = serpensOutput[:, 0:3]
+        xBins = spatialGrid.constructXaxis(midpoints=False)
+        yBins = np.linspace(-spatialGrid.rho_border, spatialGrid.rho_border, 2 * int(spatialGrid.rho_steps) + 1)
+        zBins = np.linspace(-spatialGrid.rho_border, spatialGrid.rho_border, 2 * int(spatialGrid.rho_steps) + 1)
+        cellVolume = (xBins[1] - xBins[0]) * (yBins[1] - yBins[0]) * (zBins[1] - zBins[0])
+        n_histogram = np.histogramdd(particlePos, bins=[xBins, yBins, zBins])[0] * self.N / (
+            np.size(particlePos, axis=0) * cellVolume)
+        if self.sigmaSmoothing > 0.:
+            from scipy.ndimage import gaussian_filter
+            n_histogram = gaussian_filter(n_histogram, sigma=self.sigmaSmoothing)
+        xPoints = spatialGrid.constructXaxis()
+        half = 2. * spatialGrid.rho_border / (4. * spatialGrid.rho_steps)
+        yPoints = np.linspace(-spatialGrid.rho_border, spatialGrid.rho_border, 2 * int(spatialGrid.rho_steps),
+                              endpoint=False) + half
+        zPoints = np.linspace(-spatialGrid.rho_border, spatialGrid.rho_border, 2 * int(spatialGrid.rho_steps),
+                              endpoint=False) + half
+        self.gridAxes = tuple(np.ascontiguousarray(a, dtype=np.float64) for a in (xPoints, yPoints, zPoints))
+        self.gridValues = np.ascontiguousarray(n_histogram, dtype=np.float64)
+        self._packed = np.concatenate(self.gridAxes + (self.gridValues.ravel(),))
+
+    def _require_grid(self):
+        if not hasattr(self, "gridValues"):
+            raise AttributeError("SerpensExosphere: call addInterpolatedDensity(spatialGrid) first "
+                                 "(prometheus.py:103-104)")
+
+    def checkBounds(self, x, y, z) -> None:
+        """RegularGridInterpolator's bounds_error (scipy _rgi.py _prepare_xi): every coordinate inside
+        [axis[0], axis[-1]], else ValueError naming the first offending dimension."""
+        self._require_grid()
+        for i, (ax, p) in enumerate(zip(self.gridAxes, (x, y, z))):
+            p = np.asarray(p, dtype=np.float64)
+            if not np.logical_and(np.all(ax[0] <= p), np.all(p <= ax[-1])):
+                raise ValueError("One of the requested xi is out of bounds in dimension %d" % i)
+
     def densityModel(self):
-        raise NotImplementedError
+        self._require_grid()
+        nx, ny, nz = (len(a) for a in self.gridAxes)
+        return _native.DENSITY_GRIDDED, [nx, ny, nz], None
 
     def calculateNumberDensity(self, x, phi, rho, orbphase):
-        raise NotImplementedError("SerpensExosphere needs the SERPENS particle file and a 3-D density "
-                                  "sampler; not part of this build (SURVEY.md §8f rank 3)")
+        x = np.asarray(x, dtype=np.float64)
+        scalar = np.ndim(phi) == 0 and np.ndim(rho) == 0
+        phi_, rho_ = np.broadcast_arrays(np.atleast_1d(phi), np.atleast_1d(rho))
+        y, z = geom.Grid.getCartesianFromCylinder(phi_, rho_)
+        px = np.broadcast_to(x[None, :], (len(y), len(x)))
+        py = np.broadcast_to(np.asarray(y, dtype=np.float64)[:, None], px.shape)
+        pz = np.broadcast_to(np.asarray(z, dtype=np.float64)[:, None], px.shape)
+        self.checkBounds(px, py, pz)
+        dev = _device()
+        with dev.lock:
+            n = dev.gridded_density(*self.gridAxes, self.gridValues, px, py, pz)
+        return n[0] if scalar else n
 
 
 # ============================================================================== cross sections
@@ -562,8 +619,13 @@ class Transit:
             entry = {"dist": d, "shift": self.atmosphere.shifts(d, orb), "T": float(getattr(d, "T", 0.0) or 0.0)}
             try:
                 kind, params, body = d.densityModel()
-                bx, by = body.getPosition(orb)
-                entry.update(kind=kind, params=params, body_x=np.asarray(bx, float), body_y=np.asarray(by, float))
+                if kind == _native.DENSITY_GRIDDED:
+                    d.checkBounds(g.constructXaxis()[None, :], y[:, None], z[:, None])
+                    entry.update(kind=kind, params=params, n_tabulated=d._packed)
+                else:
+                    bx, by = body.getPosition(orb)
+                    entry.update(kind=kind, params=params, body_x=np.asarray(bx, float),
+                                 body_y=np.asarray(by, float))
             except NotImplementedError:
                 entry.update(kind=_native.DENSITY_TABULATED, params=[])
                 need_tab.append(entry)

@@ -61,7 +61,9 @@ def build_transit(param: dict) -> gasprop.Transit:
         elif key == "torus":
             models.append(gasprop.TorusExosphere(nparticles, prm["a_torus"], prm["v_ej"], planet))
         elif key == "serpens":
+            # sigmaSmoothing hard-coded to 0 as in prometheus.py:103-104
             models.append(gasprop.SerpensExosphere(prm["serpensPath"], nparticles, planet, 0.))
+            models[-1].addInterpolatedDensity(sgrid)
         else:
             raise ValueError("unknown scenario %r" % key)
     atoms = const.AvailableSpecies().listSpeciesNames()
