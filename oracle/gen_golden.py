@@ -302,8 +302,122 @@ def gen_molecular_kat():
     _save("molecular_kat", P=P, T=np.float64(1234.5), wav=wav, sigma=sig, **{"tab_" + k: v for k, v in tab.items()})
 
 
+def gen_serpens():
+    """SerpensExosphere (gasProperties.py:519-601) on a seeded synthetic particle file: the reference's
+    own histogram grid (sigmaSmoothing 0 and 1.5), scalar calculateNumberDensity calls at seeded chords,
+    and R of a reduced transit.  The reference's calculateNumberDensity takes one chord at a time (its
+    batched call inside getLOSopticalDepth_Batch builds a ragged array and fails, :905 / :598-600), so
+    for the transit each batch is evaluated chord by chord with that same scalar method."""
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="serpens_golden_")
+    path = configs.synthetic_serpens_particles(os.path.join(tmp, "serpens.txt"))
+    cfg = configs.reduced(configs.serpens(path), orbphase_steps=4)
+    g = cfg["Grids"]
+    planet = bodies.AvailablePlanets().findPlanet(cfg["Architecture"]["planetName"])
+    sgrid = geom.Grid(g["x_midpoint"], g["x_border"], int(g["x_steps"]), g["upper_rho"], int(g["rho_steps"]),
+                      int(g["phi_steps"]), g["orbphase_border"], int(g["orbphase_steps"]))
+    N = cfg["Species"]["serpens"]["NaI"]["Nparticles"]
+    smooth = gasprop.SerpensExosphere(path, N, planet, 1.5)
+    smooth.addInterpolatedDensity(sgrid)
+    sc = gasprop.SerpensExosphere(path, N, planet, 0.)
+    sc.addInterpolatedDensity(sgrid)
+    rgi = sc.InterpolatedDensity
+    rng = np.random.default_rng(21)
+    x = sgrid.constructXaxis()
+    kat_phi = rng.uniform(0., 2. * np.pi, 24)
+    kat_rho = rng.uniform(0., 0.95 * g["upper_rho"], 24)
+    kat_n = np.stack([sc.calculateNumberDensity(x, p_, r_, 0.) for p_, r_ in zip(kat_phi, kat_rho)])
+    scalar = sc.calculateNumberDensity
+
+    def batched(xx, phi, rho, orb):
+        return np.stack([scalar(xx, p_, r_, o_) for p_, r_, o_ in
+                         zip(np.atleast_1d(phi), np.atleast_1d(rho), np.atleast_1d(orb))])
+
+    sc.calculateNumberDensity = batched
+    sc.addConstituent("NaI", cfg["Species"]["serpens"]["NaI"]["sigma_v"])
+    wgrid = gasprop.WavelengthGrid(g["lower_w"], g["upper_w"], g["widthHighRes"], g["resolutionLow"],
+                                   g["resolutionHigh"])
+    sc.constituents[-1].addLookupFunctionToConstituent(wgrid)
+    tr = gasprop.Transit(gasprop.Atmosphere([sc], cfg["Fundamentals"]["DopplerOrbitalMotion"]), wgrid, sgrid)
+    tr.addWavelength()
+    R = tr.sumOverChords(max_memory_gb=2.0)
+    cfg["Scenarios"]["serpens"]["serpensPath"] = "<particle file>"
+    _save("serpens", R=R, wavelength=tr.wavelength, orbphase=sgrid.constructOrbphaseAxis(),
+          config=np.array(json.dumps(cfg)), grid_x=rgi.grid[0], grid_y=rgi.grid[1], grid_z=rgi.grid[2],
+          values=rgi.values, values_smoothed=smooth.InterpolatedDensity.values, kat_x=x, kat_phi=kat_phi,
+          kat_rho=kat_rho, kat_n=kat_n, particles_n=np.int64(60000), particles_seed=np.int64(11))
+
+
+def gen_tidal():
+    """TidallyHeatedMoon (gasProperties.py:377-461) on a seeded synthetic M_dot file: absorber numbers
+    at seeded phases, batched densities and R of a reduced exomoon-architecture transit."""
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="tidal_golden_")
+    path = configs.synthetic_mdot(os.path.join(tmp, "mdot.txt"))
+    cfg = configs.reduced(configs.exomoon(), orbphase_steps=4)
+    g, arch, T = cfg["Grids"], cfg["Architecture"], configs.TIDAL
+    planet = bodies.AvailablePlanets().findPlanet(arch["planetName"])
+    moon = bodies.Moon(arch["starting_orbphase_moon"], arch["R_moon"], arch["a_moon"], planet)
+    sgrid = geom.Grid(g["x_midpoint"], g["x_border"], int(g["x_steps"]), g["upper_rho"], int(g["rho_steps"]),
+                      int(g["phi_steps"]), g["orbphase_border"], int(g["orbphase_steps"]))
+    wgrid = gasprop.WavelengthGrid(g["lower_w"], g["upper_w"], g["widthHighRes"], g["resolutionLow"],
+                                   g["resolutionHigh"])
+    sc = gasprop.TidallyHeatedMoon(T["q"], moon)
+    sc.addSourceRateFunction(path, T["tau"], T["mass"])
+    sc.addConstituent("NaI", T["sigma_v"])
+    sc.constituents[-1].addLookupFunctionToConstituent(wgrid)
+    rng = np.random.default_rng(8)
+    kat_orb = rng.uniform(-3., 3., 32)
+    kat_N = sc.calculateAbsorberNumber(kat_orb)
+    cg = sgrid.getChordGrid()[:200]
+    x = sgrid.constructXaxis()
+    kat_n = sc.calculateNumberDensity(x, cg[:, 0], cg[:, 1], cg[:, 2])
+    tr = gasprop.Transit(gasprop.Atmosphere([sc], True), wgrid, sgrid)
+    tr.addWavelength()
+    R = tr.sumOverChords(max_memory_gb=2.0)
+    _save("tidal", R=R, wavelength=tr.wavelength, orbphase=sgrid.constructOrbphaseAxis(),
+          config=np.array(json.dumps(cfg)), kat_orb=kat_orb, kat_N=kat_N, kat_chords=cg, kat_x=x, kat_n=kat_n,
+          mdot_n=np.int64(40), mdot_seed=np.int64(5))
+
+
+def gen_harness():
+    """The reference's own CLI harness (prometheus.py:23-165) end to end: setup JSON -> output file.
+    prometheus.py reads <PATH>/setupFiles/<name>.txt and writes <PATH>/output/<name>.txt with PATH the
+    folder enclosing the checkout; it is executed here (its source compiled as is, under the name
+    __main__) with __file__ pointing into a scratch tree, so PATH is that scratch folder and nothing is
+    written under /root/reference."""
+    import contextlib
+    import io
+    import tempfile
+    src_path = os.path.join(REF, "prometheus.py")
+    with open(src_path) as fh:
+        code = compile(fh.read(), src_path, "exec")
+    out = {}
+    for name, cfg in (("C1", configs.c1()),
+                      ("C2h", configs.reduced(configs.c2(), orbphase_steps=3, res_low=5e-9, res_high=2e-10,
+                                              lower_w=5886e-8, upper_w=5900e-8))):
+        tmp = tempfile.mkdtemp(prefix="harness_golden_")
+        os.makedirs(os.path.join(tmp, "setupFiles"))
+        os.makedirs(os.path.join(tmp, "output"))
+        text = json.dumps(cfg, indent=2)
+        with open(os.path.join(tmp, "setupFiles", name + ".txt"), "w") as fh:
+            fh.write(text)
+        argv = sys.argv
+        sys.argv = ["prometheus.py", name]
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                exec(code, {"__name__": "__main__", "__file__": os.path.join(tmp, "Prometheus", "prometheus.py")})
+        finally:
+            sys.argv = argv
+        with open(os.path.join(tmp, "output", name + ".txt")) as fh:
+            out["output_" + name] = np.array(fh.read())
+        out["setup_" + name] = np.array(text)
+    _save("harness", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["interp", "tables", "density", "grids", "molecular", "transits", "stars"]
+    which = sys.argv[1:] or ["interp", "tables", "density", "grids", "molecular", "transits", "stars",
+                             "serpens", "tidal", "harness"]
     if "interp" in which:
         gen_interp_kats()
     if "tables" in which:
@@ -318,3 +432,9 @@ if __name__ == "__main__":
         gen_transits()
     if "stars" in which:
         gen_stars()
+    if "serpens" in which:
+        gen_serpens()
+    if "tidal" in which:
+        gen_tidal()
+    if "harness" in which:
+        gen_harness()

@@ -282,7 +282,7 @@ def distance_to(bx, by, x, phi, rho):
 @dataclass
 class Scenario:
     """One density distribution.  kind in
-    barometric | hydrostatic | powerLawAtm | powerLawExo | exomoon | torus | tabulated."""
+    barometric | hydrostatic | powerLawAtm | powerLawExo | exomoon | torus | serpens | tidal | tabulated."""
     kind: str
     planet: Body
     params: dict
@@ -292,10 +292,11 @@ class Scenario:
     constituents: List[dict] = field(default_factory=list)
     T: float = 0.0
     tabulated_fn: object = None
+    grid: object = None   # serpens: (xPoints, yPoints, zPoints, values)
 
     @property
     def has_moon(self):
-        return self.kind == "exomoon"
+        return self.kind in ("exomoon", "tidal")
 
 
 def number_density(sc: Scenario, x, phi, rho, orb) -> np.ndarray:
@@ -305,6 +306,16 @@ def number_density(sc: Scenario, x, phi, rho, orb) -> np.ndarray:
     prm = sc.params
     if k == "tabulated":
         return sc.tabulated_fn(x, phi, rho, orb)
+    if k == "serpens":                                           # :585-601, one chord at a time
+        return np.stack([serpens_density(sc.grid, x, ph, rh) for ph, rh in zip(np.atleast_1d(phi), np.atleast_1d(rho))])
+    if k == "tidal":                                             # :440-461
+        N = tidal_absorber_number(sc, orb)
+        r = distance_to(*moon_position(sc.moon, orb), x, phi, rho)
+        N_ = np.asarray(N)
+        if N_.ndim > 0:
+            N_ = N_[:, np.newaxis]
+        n0 = (prm["q"] - 3.) / (4. * np.pi * sc.moon.R ** 3) * N_
+        return n0 * (sc.moon.R / r) ** prm["q"] * np.heaviside(r - sc.moon.R, 1.)
     if k in ("barometric", "hydrostatic", "powerLawAtm", "powerLawExo"):
         xp, yp = planet_position(p, orb)
         r = distance_to(xp, yp, x, phi, rho)
@@ -344,6 +355,55 @@ def number_density(sc: Scenario, x, phi, rho, orb) -> np.ndarray:
         n0 = 1. / (2. * np.pi ** 1.5 * Ht * (t1 + t2)) * prm["N"]
         return n0 * np.multiply(n_a, n_z)
     raise ValueError(k)
+
+
+# --- SERPENS particle grid: gasProperties.py:548-601 ---------------------------
+def serpens_grid(filename, N, g, sigma_smoothing=0.0):
+    """addInterpolatedDensity (:548-583): particles [m] -> histogramdd over the x cell edges and
+    2 rho_steps sky-plane cells per axis -> density (optionally Gaussian-smoothed) on the cell
+    midpoints.  Returns (xPoints, yPoints, zPoints, values)."""
+    pos = (np.loadtxt(filename) * 1e2)[:, 0:3]
+    lo, hi, n = g["x_midpoint"] - g["x_border"], g["x_midpoint"] + g["x_border"], int(g["x_steps"])
+    xb = np.linspace(lo, hi, n + 1)
+    rb, nr = g["upper_rho"], int(g["rho_steps"])
+    yb = np.linspace(-rb, rb, 2 * nr + 1)
+    zb = np.linspace(-rb, rb, 2 * nr + 1)
+    vol = (xb[1] - xb[0]) * (yb[1] - yb[0]) * (zb[1] - zb[0])
+    vals = np.histogramdd(pos, bins=[xb, yb, zb])[0] * N / (np.size(pos, axis=0) * vol)
+    if sigma_smoothing > 0.:
+        from scipy.ndimage import gaussian_filter
+        vals = gaussian_filter(vals, sigma=sigma_smoothing)
+    xp = np.linspace(lo, hi, n, endpoint=False) + g["x_border"] / float(n)
+    yp = np.linspace(-rb, rb, 2 * nr, endpoint=False) + 2. * rb / (4. * nr)
+    zp = np.linspace(-rb, rb, 2 * nr, endpoint=False) + 2. * rb / (4. * nr)
+    return xp, yp, zp, vals
+
+
+def serpens_density(grid, x, phi, rho):
+    """calculateNumberDensity (:585-601) for one chord: scipy RegularGridInterpolator (linear,
+    bounds_error=True) at (x, rho sin phi, rho cos phi)."""
+    from scipy.interpolate import RegularGridInterpolator
+    xp, yp, zp, vals = grid
+    y, z = rho * np.sin(phi), rho * np.cos(phi)
+    pts = np.array([x, np.repeat(y, np.size(x)), np.repeat(z, np.size(x))]).T
+    return RegularGridInterpolator((xp, yp, zp), vals)(pts)
+
+
+# --- tidally heated moon: gasProperties.py:377-461 -----------------------------
+def tidal_source(filename, tau_photoionization, mass_absorber):
+    """addSourceRateFunction (:404-424): the mirrored M_dot profile on [0, 2 pi] -> log10 N nodes."""
+    mdot = np.loadtxt(filename)
+    mdot = np.concatenate((mdot, mdot[::-1]))
+    return np.linspace(0., 2. * np.pi, len(mdot)), np.log10(mdot * tau_photoionization / mass_absorber)
+
+
+def tidal_absorber_number(sc, orb):
+    """calculateAbsorberNumber (:426-438): 10^interp1d(phi_moon, log10 N) at the moon's phase mod 2 pi
+    (scipy interp1d, linear: bracket from searchsorted-left clipped to [1, n-1])."""
+    from scipy.interpolate import interp1d
+    xs, ys = sc.params["source"]
+    om = moon_orbphase(sc.moon, orb) % (2. * np.pi)
+    return 10 ** interp1d(xs, ys)(om)
 
 
 # --- molecular table: gasProperties.py:765-818 ---------------------------------
@@ -530,6 +590,11 @@ def from_setup(cfg: dict, molecular_tables: Optional[dict] = None):
             first = list(spec["torus"].keys())[0]
             sc = Scenario("torus", planet, {"N": spec["torus"][first]["Nparticles"],
                                             "a_torus": prm["a_torus"], "v_ej": prm["v_ej"]})
+        elif key == "serpens":
+            first = list(spec["serpens"].keys())[0]
+            N = spec["serpens"][first]["Nparticles"]
+            sc = Scenario("serpens", planet, {"N": N})
+            sc.grid = serpens_grid(prm["serpensPath"], N, grids, 0.)   # sigmaSmoothing 0 (prometheus.py:103)
         else:
             raise ValueError("scenario %r is not restated by the oracle" % key)
         collisional = "T" in prm

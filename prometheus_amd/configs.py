@@ -149,6 +149,21 @@ def serpens(path):
             "Grids": _grids(5884e-8, 5902e-8, 1e-9, 5e-11, orbphase_steps=4)}
 
 
+def synthetic_mdot(path, n=40, seed=5):
+    """Seeded stand-in for a tidally heated moon's mass-loss-rate file (TidallyHeatedMoon
+    .addSourceRateFunction, gasProperties.py:404-424): n values of M_dot [g/s] over half a moon orbit,
+    log-normal about 1e4 g/s, written with 17 significant digits.  Returns path."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    np.savetxt(path, 1e4 * np.exp(0.8 * rng.standard_normal(n)), fmt="%.17g")
+    return path
+
+
+# the tidally heated moon fixture (not reachable from a setup file: the reference CLI has no scenario
+# key for it): the exomoon architecture, q, photoionisation lifetime [s] and absorber mass [g]
+TIDAL = {"q": 3.34, "tau": 1.2e4, "mass": 22.99 * _AMU, "sigma_v": 10. * _KMS}
+
+
 PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C5": c5, "exomoon": exomoon}
 
 

@@ -244,7 +244,8 @@ class TidallyHeatedMoon(EvaporativeExosphere):
     """Moon exosphere with a phase-dependent source rate (gasProperties.py:377-461).
 
     Not a built-in device scenario: its density is evaluated on the host by the plugin itself
-    (``calculateNumberDensity``) and handed to the device as a tabulated n(c, x)."""
+    (``calculateNumberDensity``, numpy/scipy as in the reference) and handed to the device as a
+    tabulated n(c, x) (PROM_DENSITY_TABULATED), like any user plugin."""
 
     def __init__(self, q: float, moon: Any):
         self.q = q
@@ -253,14 +254,17 @@ class TidallyHeatedMoon(EvaporativeExosphere):
         self.planet = moon.hostPlanet
 
     def addSourceRateFunction(self, filename: str, tau_photoionization: float, mass_absorber: float) -> None:
+        """M_dot(moon phase) from a file, mirrored onto [0, 2 pi]; N = M_dot tau / m (:404-424)."""
+        from scipy.interpolate import interp1d
         mdot = np.loadtxt(filename)
         mdot = np.concatenate((mdot, mdot[::-1]))
-        self._phi_src = np.linspace(0., 2. * np.pi, len(mdot))
-        self._logN_src = np.log10(mdot * tau_photoionization / mass_absorber)
+        phi_moon = np.linspace(0., 2. * np.pi, len(mdot))
+        self.N_function = interp1d(phi_moon, np.log10(mdot * tau_photoionization / mass_absorber))
 
     def calculateAbsorberNumber(self, orbphase):
+        """N = 10^N_function(moon phase mod 2 pi) (:426-438; scipy interp1d, as the reference)."""
         om = self.moon.getOrbphase(orbphase) % (2. * np.pi)
-        return 10 ** np.interp(om, self._phi_src, self._logN_src)
+        return 10 ** self.N_function(om)
 
     def calculateNumberDensity(self, x, phi, rho, orbphase):
         N = np.asarray(self.calculateAbsorberNumber(orbphase))

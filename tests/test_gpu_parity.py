@@ -450,3 +450,70 @@ def test_sigma_rows_bitwise(dev, name, merge, monkeypatch):
     R_b = tr.sumOverChords(devices=[0])
     print(name, "merge", merge, "max rel diff %.3e" % rel(R_a, R_b))
     assert np.array_equal(R_a, R_b)
+
+
+# ---- SERPENS gridded density, tidally heated moon, setup-file harness (fixtures: oracle/gen_golden.py)
+def test_serpens_golden(dev, tmp_path):
+    """SerpensExosphere through the CLI loader (prometheus.py:100-105): the histogram grid sampled on the
+    device (PROM_DENSITY_GRIDDED) inside the fused path, and the standalone sampler on the reference's
+    scalar calculateNumberDensity calls."""
+    from prometheus_amd import configs, setupfile
+    d = load("serpens")
+    path = configs.synthetic_serpens_particles(str(tmp_path / "serpens.txt"), n=int(d["particles_n"]),
+                                               seed=int(d["particles_seed"]))
+    cfg = json.loads(str(d["config"]))
+    cfg["Scenarios"]["serpens"]["serpensPath"] = path
+    tr = setupfile.build_transit(cfg)
+    assert np.array_equal(tr.wavelength, d["wavelength"])
+    sc = tr.atmosphere.densityDistributionList[0]
+    for i in range(len(d["kat_phi"])):
+        n = sc.calculateNumberDensity(d["kat_x"], d["kat_phi"][i], d["kat_rho"][i], 0.)
+        assert rel(n, d["kat_n"][i]) < 1e-13
+    # batched chords (the reference's batch call fails; each row equals its scalar call)
+    nb = sc.calculateNumberDensity(d["kat_x"], d["kat_phi"], d["kat_rho"], np.zeros(len(d["kat_phi"])))
+    assert rel(nb, d["kat_n"]) < 1e-13
+    R = tr.sumOverChords()
+    assert rel(R, d["R"]) < R_TOL
+    assert np.min(d["R"]) < 0.99   # the cloud absorbs
+
+
+def test_tidal_golden(dev, tmp_path):
+    """TidallyHeatedMoon (host plugin, tabulated onto the device) against the reference's R."""
+    from prometheus_amd import configs, gasProperties as gp, celestialBodies as bodies, geometryHandler as geom
+    d = load("tidal")
+    path = configs.synthetic_mdot(str(tmp_path / "mdot.txt"), n=int(d["mdot_n"]), seed=int(d["mdot_seed"]))
+    cfg = json.loads(str(d["config"]))
+    g, arch, T = cfg["Grids"], cfg["Architecture"], configs.TIDAL
+    planet = bodies.AvailablePlanets().findPlanet(arch["planetName"])
+    moon = bodies.Moon(arch["starting_orbphase_moon"], arch["R_moon"], arch["a_moon"], planet)
+    sgrid = geom.Grid(g["x_midpoint"], g["x_border"], int(g["x_steps"]), g["upper_rho"], int(g["rho_steps"]),
+                      int(g["phi_steps"]), g["orbphase_border"], int(g["orbphase_steps"]))
+    wgrid = gp.WavelengthGrid(g["lower_w"], g["upper_w"], g["widthHighRes"], g["resolutionLow"], g["resolutionHigh"])
+    sc = gp.TidallyHeatedMoon(T["q"], moon)
+    sc.addSourceRateFunction(path, T["tau"], T["mass"])
+    sc.addConstituent("NaI", T["sigma_v"])
+    sc.constituents[-1].addLookupFunctionToConstituent(wgrid)
+    tr = gp.Transit(gp.Atmosphere([sc], True), wgrid, sgrid)
+    tr.addWavelength()
+    assert np.array_equal(tr.wavelength, d["wavelength"])
+    assert rel(tr.sumOverChords(), d["R"]) < R_TOL
+
+
+@pytest.mark.parametrize("name", ["C1", "C2h"])
+def test_setup_harness_golden(dev, name, tmp_path):
+    """setup JSON -> output file through `python -m prometheus_amd.setupfile` (prometheus.py:56-156): same
+    header, phase row and wavelength column bitwise, R within the north-star tolerance."""
+    from prometheus_amd import setupfile
+    d = load("harness")
+    (tmp_path / "setupFiles").mkdir()
+    (tmp_path / "setupFiles" / (name + ".txt")).write_text(str(d["setup_" + name]))
+    setupfile.run(name, path=str(tmp_path))
+    ours = (tmp_path / "output" / (name + ".txt")).read_text()
+    ref = str(d["output_" + name])
+    head = [l for l in ref.splitlines() if l.startswith("#")]
+    assert [l for l in ours.splitlines() if l.startswith("#")] == head
+    a = np.loadtxt(str(tmp_path / "output" / (name + ".txt")))
+    b = np.loadtxt(ref.splitlines())
+    assert a.shape == b.shape
+    assert np.array_equal(a[0, 1:], b[0, 1:]) and np.array_equal(a[1:, 0], b[1:, 0])
+    assert rel(a[1:, 1:], b[1:, 1:]) < R_TOL
