@@ -623,8 +623,11 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         tm.chi = 1.0;
         tr.colargs_m.t[0] = tm;
         upload(tr.sigma_max_m, &smax_m, 1, s);
+        tr.qbound_m = smax_m * tr.sigtab_m.t[0].nscale;
       }
       upload(tr.sigtab, st.data(), (int64_t)st.size(), s);
+      tr.qbound_v = 0.0;
+      for (size_t i = 0; i < st.size(); ++i) tr.qbound_v += tr.atom_sigma_max[i] * st[i].nscale;
       tr.uniform_shift = true;
       for (const auto& t : tr.terms) {
         if (t.is_molecule) continue;

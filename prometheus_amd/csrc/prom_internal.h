@@ -257,6 +257,9 @@ struct TransitDev {
   ColArgs colargs_m{};                      // the single chi = 1 term
   SigTabs4 sigtab_m{};                      // t[0]: the effective absorber's normalisation (ncoef, nscale)
   DevBuf sigma_max_m;                       // [1] sum_s chi_s sigma_max_s
+  // upper bounds of the normalised Q = sum_s sigma_s / c_s over every wavelength and phase (per species /
+  // merged): k_order's always-tail threshold btail = tail epsilon / Q bound
+  double qbound_v = 0.0, qbound_m = 0.0;
   int32_t taup_resident = 0;                // k_tau_p wavefronts resident at once (set at the first run)
   // timed runs: k_tau_p stamps each workgroup's first and last device-clock tick into ts_out[2 b],
   // ts_out[2 b + 1] when it has at most ts_cap workgroups; ts_blocks reports the count (0: no stamps)

@@ -63,11 +63,12 @@ __device__ __forceinline__ double interp_guess(double t, int32_t g, XF X2, RF RE
   const int32_t k = t < xg.x ? g - 1 : (t >= xg.y ? g + 1 : g);
   double xa, fa, sl;
   REC(k, xa, fa, sl);
-  double rv;
-  if (xa == t) rv = fa;
-  else {
-    rv = sl * (t - xa) + fa;
-    if (rv != rv) {   // numpy's retry from the right node
+  // numpy: an exact node hit returns f; with a finite slope sl (t - x) + f is that f already, so the
+  // test is only needed where the interpolation is NaN (non-finite slope), as is numpy's right-node retry
+  double rv = sl * (t - xa) + fa;
+  if (rv != rv) {
+    if (xa == t) rv = fa;
+    else {
       double xb, fb, sb;
       REC(k + 1, xb, fb, sb);
       rv = sl * (t - xb) + fb;
@@ -78,8 +79,9 @@ __device__ __forceinline__ double interp_guess(double t, int32_t g, XF X2, RF RE
 }
 
 __device__ __forceinline__ int32_t seg_guess(double t, double xs, double inv, int32_t m) {
+  // = (f < 0 ? 0 : f >= m - 2 ? m - 2 : (int)f), the host's verified map (NaN t never reaches here)
   const double f = (t - xs) * inv;
-  return f < 0.0 ? 0 : (f >= (double)(m - 2) ? m - 2 : (int32_t)f);
+  return (int32_t)__builtin_fmin(__builtin_fmax(f, 0.0), (double)(m - 2));
 }
 
 // Workgroups [0, n_blk * n_rc): one per (256-wavelength block whose slices all fit in LDS, chunk of

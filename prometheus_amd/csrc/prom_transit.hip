@@ -560,7 +560,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
                                                    const float4* __restrict__ tq, int32_t tq_rows,
                                                    int32_t n_tiles, int64_t n_wav,
                                                    int4* __restrict__ trec, int4* __restrict__ hlist, int64_t hcap,
-                                                   int32_t* __restrict__ hcnt) {
+                                                   int32_t* __restrict__ hcnt, double btail) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
@@ -597,12 +597,15 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   }
   if (tid < 2) sHc[tid] = 0;   // (barriers of steps 1-6 order it before step 7)
   for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }
-  // ---- 1. load, classify, keys, combined scan/reduction
+  // ---- 1. load, classify, keys, combined scan/reduction.  Active chords whose bound b is below btail
+  //         (b Q < the tail epsilon at every wavelength of the problem) are tail records everywhere: they
+  //         are compacted behind the others, unsorted (single sweep only)
+  const bool part = n_pr <= kWinMax && btail > 0.0;
   double fs = 0.0, ts = 0.0;
-  int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0;
+  int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0, ncand = 0;
   for (int32_t sw = 0; sw < n_pr; sw += kWinMax) {
     int32_t f[kLD];
-    double fo[kLD], nv[kLD][NS];
+    double fo[kLD], nv[kLD][NS], bk[kLD];
 #pragma unroll
     for (int k = 0; k < kLD; ++k) {
       const int32_t ip = sw + tid + k * kWBlock;
@@ -613,62 +616,74 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       for (int s = 0; s < NS; ++s) nv[k][s] = in ? nc0[s * nstride + ip] : 0.0;
     }
     double fp = 0.0, tp = 0.0;
-    int32_t c[5] = {0, 0, 0, 0, 0};   // active, transparent, blocked, nonfinite
+    int32_t c[5] = {0, 0, 0, 0, 0};   // active (not tail), transparent, blocked, nonfinite, tail
+    uint32_t tailbits = 0;
 #pragma unroll
     for (int k = 0; k < kLD; ++k) {
+      bk[k] = 0.0;
       if (f[k] == 3) continue;
       fp += fo[k];
       if (f[k] == 1) { tp += fo[k]; ++c[1]; }
       else if (f[k] == 2) ++c[2];
       else {
-        ++c[0];
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          if (!__builtin_isfinite(nv[k][s])) { ++c[3]; break; }
-      }
-    }
-    // combined: prefix of the active count, wavefront totals of everything (DPP scans)
-    const int32_t inc = wave_prefix<int32_t>(c[0], OpAdd());
-    const double fpw = lane_read(wave_prefix<double>(fp, OpAdd()), 63);
-    const double tpw = lane_read(wave_prefix<double>(tp, OpAdd()), 63);
-    const int32_t c1w = lane_read(wave_prefix<int32_t>(c[1], OpAdd()), 63);
-    const int32_t c2w = lane_read(wave_prefix<int32_t>(c[2], OpAdd()), 63);
-    const int32_t c3w = lane_read(wave_prefix<int32_t>(c[3], OpAdd()), 63);
-    __syncthreads();
-    if (lane == 63) pi_[wid][0] = inc;
-    if (lane == 0) {
-      pi_[wid][1] = c1w; pi_[wid][2] = c2w; pi_[wid][3] = c3w;
-      pd_[wid][0] = fpw; pd_[wid][1] = tpw;
-    }
-    __syncthreads();
-    int32_t pos = nact + inc - c[0];
-    for (int w = 0; w < NW; ++w) {
-      if (w < wid) pos += pi_[w][0];
-      nact += pi_[w][0]; ntr += pi_[w][1]; nbl += pi_[w][2]; nnf += pi_[w][3];
-      fs += pd_[w][0]; ts += pd_[w][1];
-    }
-#pragma unroll
-    for (int k = 0; k < kLD; ++k) {
-      if (f[k] != 0) continue;
-      if (pos < kWinMax) {
         double b = 0.0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if (!__builtin_isfinite(nv[k][s])) { ++c[3]; break; }
+        }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const double v = nv[k][s] * cs[s];
           b = v > b ? v : b;
         }
         b = b < 1.0 ? b : 1.0;   // NaN -> 1.0 (such phases take the unsorted path anyway)
-        const unsigned long long d =
-            (__builtin_bit_cast(unsigned long long, 1.0) - __builtin_bit_cast(unsigned long long, b)) >> 22;
-        skey[pos] = (d << 24) | (unsigned long long)pos;
-        sIp[pos] = sw + tid + k * kWBlock;
-        if (pos < PAY) {
-          sF[pos] = fo[k];
+        bk[k] = b;
+        if (part && b < btail) { ++c[4]; tailbits |= 1u << k; }
+        else ++c[0];
+      }
+    }
+    // combined: prefixes of the candidate and tail counts, wavefront totals of everything (DPP scans)
+    const int32_t inc = wave_prefix<int32_t>(c[0], OpAdd());
+    const int32_t inct = wave_prefix<int32_t>(c[4], OpAdd());
+    const double fpw = lane_read(wave_prefix<double>(fp, OpAdd()), 63);
+    const double tpw = lane_read(wave_prefix<double>(tp, OpAdd()), 63);
+    const int32_t c1w = lane_read(wave_prefix<int32_t>(c[1], OpAdd()), 63);
+    const int32_t c2w = lane_read(wave_prefix<int32_t>(c[2], OpAdd()), 63);
+    const int32_t c3w = lane_read(wave_prefix<int32_t>(c[3], OpAdd()), 63);
+    __syncthreads();
+    if (lane == 63) { pi_[wid][0] = inc; pi_[wid][4] = inct; }
+    if (lane == 0) {
+      pi_[wid][1] = c1w; pi_[wid][2] = c2w; pi_[wid][3] = c3w;
+      pd_[wid][0] = fpw; pd_[wid][1] = tpw;
+    }
+    __syncthreads();
+    int32_t sc_ = 0;   // candidates of this sweep
+    for (int w = 0; w < NW; ++w) sc_ += pi_[w][0];
+    int32_t pos = nact + inc - c[0];
+    int32_t post = nact + sc_ + inct - c[4];
+    for (int w = 0; w < NW; ++w) {
+      if (w < wid) { pos += pi_[w][0]; post += pi_[w][4]; }
+      nact += pi_[w][0] + pi_[w][4]; ntr += pi_[w][1]; nbl += pi_[w][2]; nnf += pi_[w][3];
+      fs += pd_[w][0]; ts += pd_[w][1];
+    }
+    ncand += sc_;
 #pragma unroll
-          for (int s = 0; s < NS; ++s) sN[s][pos] = nv[k][s];
+    for (int k = 0; k < kLD; ++k) {
+      if (f[k] != 0) continue;
+      const bool tl = (tailbits >> k) & 1u;
+      const int32_t pk = tl ? post : pos;
+      if (pk < kWinMax) {
+        const unsigned long long d =
+            (__builtin_bit_cast(unsigned long long, 1.0) - __builtin_bit_cast(unsigned long long, bk[k])) >> 22;
+        skey[pk] = (d << 24) | (unsigned long long)pk;
+        sIp[pk] = sw + tid + k * kWBlock;
+        if (pk < PAY) {
+          sF[pk] = fo[k];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) sN[s][pk] = nv[k][s];
         }
       }
-      ++pos;
+      if (tl) ++post; else ++pos;
     }
   }
   __syncthreads();   // keys visible to the sort
@@ -704,7 +719,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     }
   } else {
     const int32_t n = nact;
-    // ---- 3. sort
+    const int32_t n_all = n;
+    // ---- 3. sort the candidates [0, ncand); tail records [ncand, n) keep their compaction order
+    {
+    const int32_t n = ncand;
     if (n <= kRankMax) {
       // rank = number of smaller keys (keys are unique: they carry the chord index); only the
       // wavefronts holding keys count, against LDS broadcasts
@@ -803,6 +821,12 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         }
       }
     }
+    }
+    // tail keys: only their compaction position (low 24 bits) is read from here on; the sort's padding
+    // may have overwritten some, so they are rewritten
+    __syncthreads();
+    for (int32_t i = ncand + tid; i < n_all; i += kWBlock) skey[i] = (unsigned long long)i;
+    __syncthreads();
     PROM_TS(o * 16 + 2);
     // ---- 4. this thread's sorted positions [i0, i0 + cnt)
     const int32_t per = (n + kWBlock - 1) / kWBlock;   // <= kWPer
@@ -954,7 +978,8 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           // later members' a are within 2^-40 of the head's: A is widened by 2^-38 to cover them
           // envelopes -> histograms over the threshold-table index (1/8 octave): slot 0 below the
           // table, slot kEnvN + 1 above it
-          const double Bg = bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28);
+          // (tail records, unsorted behind every candidate: B = btail covers all of them)
+          const double Bg = i >= ncand ? btail * (1.0 + 0x1p-28) : (bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28));
           const double Ag = ak[k] * (1.0 - 0x1p-38);
           atomicAdd(&hB[env_slot(Bg)], 1);
           atomicAdd(&hA[env_slot(Ag)], 1);
@@ -2074,7 +2099,14 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>(), \
                      pre_sigma ? rs.tq.as<float4>() : nullptr, sig_rows, n_wtiles, tr.n_wav,            \
                      rs.trec.as<int4>(), (pre_sigma && tr.plan) ? rs.hlist.as<int4>() : nullptr, hcap, \
-                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr)
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, btail)
+    // always-tail threshold: b Q < the tail epsilon at every wavelength.  Any value keeps R exact (the
+    // unsorted records' envelope is btail itself); a tight one keeps most far chords out of the sort.  The
+    // factor 2^-1/4 keeps btail below every window threshold the tables can return (1/8-octave slots
+    // rounded conservatively, float Q ranges widened by 2^-20), so tail records are never evaluated one by one
+    const double qb = msp ? tr.qbound_m : tr.qbound_v;
+    const double btail = (tr.window && qb > 0.0 && std::isfinite(qb) && !std::getenv("PROM_NO_TAIL_SPLIT"))
+                             ? (na == 1 ? tail_eps<1>() : tail_eps<2>()) / qb * 0.8408964152537145 : 0.0;
     switch (na) {
       case 1: PROM_CHW(1); break;
       case 2: PROM_CHW(2); break;

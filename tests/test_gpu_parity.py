@@ -139,9 +139,12 @@ def test_transit_ocml_exp_mode(dev, name):
 
 
 @pytest.mark.parametrize("name", ["C1", "C2r", "C4r", "exomoon"])
-def test_chord_merging(dev, name):
-    """Merging chords with equal (2^-40) column densities moves R by <= 2^-40/e."""
+def test_chord_merging(dev, name, monkeypatch):
+    """Merging chords with equal (2^-40) column densities moves R by <= 2^-40/e.  Checked with
+    every active chord sorted (PROM_NO_TAIL_SPLIT): always-tail chords are otherwise left unsorted behind
+    the others, where equal neighbours are not adjacent (test_tail_split)."""
     from prometheus_amd import _native
+    monkeypatch.setenv("PROM_NO_TAIL_SPLIT", "1")
     d = load("transit_" + name)
     tr = _product_transit(json.loads(str(d["config"])))
     R_m = tr.sumOverChords(devices=[0])
@@ -155,6 +158,20 @@ def test_chord_merging(dev, name):
     print(name, "records merged %d -> %d" % (st_m["active_chords"], st_m["tau_records"]))
     if name == "C1":   # one phase with the planet at the disk centre: whole rings merge
         assert st_m["tau_records"] * 10 < st_m["active_chords"]
+
+
+@pytest.mark.parametrize("name", ["C1", "C2r", "C3r", "C4r", "exomoon"])
+def test_tail_split(dev, name, monkeypatch):
+    """k_order leaves chords with b Q_bound < the tail epsilon unsorted behind the sorted ones (their
+    envelope is the threshold itself): R moves by no more than the windowed bound, and stays within the
+    north-star tolerance of the reference."""
+    d = load("transit_" + name)
+    cfg = json.loads(str(d["config"]))
+    R_s = _product_transit(cfg).sumOverChords(devices=[0])
+    monkeypatch.setenv("PROM_NO_TAIL_SPLIT", "1")
+    R_n = _product_transit(cfg).sumOverChords(devices=[0])
+    assert np.max(np.abs(R_s - R_n)) <= 1e-13   # each run within 4e-14 of the full evaluation
+    assert rel(R_s, d["R"]) < R_TOL
 
 
 def test_sharding_bitwise(dev):
