@@ -5,7 +5,7 @@
 namespace prom {
 
 static_assert(kSigBlockW == kBlock, "sigma segments are built per kBlock wavelengths");
-constexpr int kSigFbRows = 4;   // rows per gathering workgroup (independent lookups in flight per lane)
+constexpr int kSigFbRows = 1;   // rows per gathering workgroup (independent lookups in flight per lane)
 
 // ---- Doppler-shifted cross-section rows (orbital Doppler shift: one row per phase) ----------------
 // The host (prom_api.hip sigma segments) gives, per 256-wavelength block and atomic slot, the table nodes
@@ -14,13 +14,13 @@ constexpr int kSigFbRows = 4;   // rows per gathering workgroup (independent loo
 // fl(s_max lambda_last)].  Same bracket rule, slope, products and exp10 as sigma_of / sigma_multi: the
 // rows are bit-for-bit those of the per-target lookups.
 
-// One row's outputs at one wavelength: the cross sections (or the merged absorber Y and its zero flag)
-// and the row's Q range over each 64-wavelength half tile (wavefront min / max, widened by 2^-20).
+// One row's outputs at one wavelength: the cross sections (or the merged absorber Y and its zero flag).
+// Returns the lane's Q value for the row's half-tile Q range, -1 when it is not finite or above 1e100.
 template <int NSIG>
-__device__ __forceinline__ void sigma_row_out(int32_t orow, int32_t nse, const double (&v)[NSIG], const SigTabs4& tabv,
-                                              bool live, int64_t w, int64_t n_wav, int64_t hw, int64_t n_halves,
-                                              int lane, int32_t merge_sp, double nscale_m, double* __restrict__ sig,
-                                              float4* __restrict__ tq, uint8_t* __restrict__ zfl) {
+__device__ __forceinline__ float sigma_row_store(int32_t orow, int32_t nse, const double (&v)[NSIG],
+                                                 const SigTabs4& tabv, bool live, int64_t w, int64_t n_wav,
+                                                 int32_t merge_sp, double nscale_m, double* __restrict__ sig,
+                                                 uint8_t* __restrict__ zfl) {
   double Qv = 0.0;
   if (merge_sp) {
     double Y = 0.0;
@@ -45,12 +45,26 @@ __device__ __forceinline__ void sigma_row_out(int32_t orow, int32_t nse, const d
       Qv += qs > 0.0 ? qs : 0.0;
     }
   }
-  const float qf = (float)Qv;
-  const float qh = wave_reduce_f(qf * (1.0f + 0x1p-20f), [](float a, float b) { return fmaxf(a, b); });
-  const float ql = wave_reduce_f(qf * (1.0f - 0x1p-20f), [](float a, float b) { return fminf(a, b); });
-  const bool bad = __ballot(!(Qv <= 1.0e100)) != 0ull;
-  if (lane == 0 && hw < n_halves)
-    reinterpret_cast<float2*>(tq)[(int64_t)orow * n_halves + hw] = bad ? make_float2(-1.0f, 0.0f) : make_float2(ql, qh);
+  return Qv <= 1.0e100 ? (float)Qv : -1.0f;
+}
+
+// A half tile's Q range from its lanes' values q (>= 0, or -1 for a non-finite one): [min q (1 - 2^-20),
+// max q (1 + 2^-20)], or (-1, 0) when any value is -1.  (fl(q c) is monotone in q, so scaling after the
+// min / max is the same as scaling every lane's value first.)
+__device__ __forceinline__ float2 q_range(float qmin, float qmax) {
+  return qmin < 0.0f ? make_float2(-1.0f, 0.0f) : make_float2(qmin * (1.0f - 0x1p-20f), qmax * (1.0f + 0x1p-20f));
+}
+
+// One row's outputs and its wavefront's half-tile Q range (DPP reductions over the 64 lanes).
+template <int NSIG>
+__device__ __forceinline__ void sigma_row_out(int32_t orow, int32_t nse, const double (&v)[NSIG], const SigTabs4& tabv,
+                                              bool live, int64_t w, int64_t n_wav, int64_t hw, int64_t n_halves,
+                                              int lane, int32_t merge_sp, double nscale_m, double* __restrict__ sig,
+                                              float4* __restrict__ tq, uint8_t* __restrict__ zfl) {
+  const float q = sigma_row_store<NSIG>(orow, nse, v, tabv, live, w, n_wav, merge_sp, nscale_m, sig, zfl);
+  const float qh = wave_reduce_f(q, [](float a, float b) { return fmaxf(a, b); });
+  const float ql = wave_reduce_f(q, [](float a, float b) { return fminf(a, b); });
+  if (lane == 0 && hw < n_halves) reinterpret_cast<float2*>(tq)[(int64_t)orow * n_halves + hw] = q_range(ql, qh);
 }
 
 // numpy.interp of one target from its bracket guess g (within one node of the bracket, SigSeg): x_g and
@@ -122,18 +136,21 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
     for (int s = 0; s < NSIG; ++s) {
       const SigTabDev& tb = tabv.t[s];
       const SigSeg sg = seg[wb * NSIG + s];
-      const double4* __restrict__ rc = tb.rec + sg.lo;
+      const double* __restrict__ gx = tb.x + sg.lo;
+      const double* __restrict__ gy = tb.y + sg.lo;
 #pragma unroll
       for (int r = 0; r < kSigFbRows; ++r) {
         const int32_t orow = f0 + r < n_rows ? f0 + r : n_rows - 1;
         const double t = tb.shift[orow] * lam;
         if (sg.kind > 0) {
+          // the x and f arrays (16 bytes per lane and array: the high-resolution slices are sparse in the
+          // targets, so bytes per lane decide), the slope divided here as numpy does
           const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
           v[r][s] = exp10(interp_guess(
-                        t, g, [&](int32_t i) { return make_double2(rc[i].x, rc[i + 1].x); },
+                        t, g, [&](int32_t i) { return make_double2(gx[i], gx[i + 1]); },
                         [&](int32_t i, double& x, double& f, double& sl) {
-                          const double4 q = rc[i];
-                          x = q.x; f = q.y; sl = q.z;
+                          x = gx[i]; f = gy[i];
+                          sl = (gy[i + 1] - f) / (gx[i + 1] - x);
                         })) - tb.offset;
         } else {
           v[r][s] = sigma_of(t, tb);
@@ -157,7 +174,6 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
   const int64_t w = wb * kBlock + tid;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
-  const int64_t hw = wb * (kBlock / 64) + (tid >> 6);
   double V[kSigRowChunk][NSIG];
 #pragma unroll
   for (int s = 0; s < NSIG; ++s) {
@@ -184,11 +200,34 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
                     })) - tb.offset;
     }
   }
+  // rows' outputs; their Q values go through LDS (over the slice, no longer read) so that the half-tile
+  // ranges of all rows take one pass: thread (r, h, p) reduces 8 values, then 8 lanes combine by DPP
+  float* sq = reinterpret_cast<float*>(sxf);   // [kSigRowChunk][kBlock]
+  static_assert(sizeof(sxf) >= sizeof(float) * kSigRowChunk * kBlock, "Q staging fits the slice");
+  float qv[kSigRowChunk];
 #pragma unroll
   for (int r = 0; r < kSigRowChunk; ++r) {
-    const int32_t orow = r0 + r;
-    if (orow >= n_rows) break;
-    sigma_row_out<NSIG>(orow, nse, V[r], tabv, live, w, n_wav, hw, n_halves, lane, merge_sp, nscale_m, sig, tq, zfl);
+    const int32_t orow = r0 + r < n_rows ? r0 + r : n_rows - 1;
+    qv[r] = sigma_row_store<NSIG>(orow, nse, V[r], tabv, live && r0 + r < n_rows, w, n_wav, merge_sp, nscale_m,
+                                  sig, zfl);
+  }
+  __syncthreads();   // every lane's lookups done: the slice arrays are free
+#pragma unroll
+  for (int r = 0; r < kSigRowChunk; ++r) sq[r * kBlock + tid] = qv[r];
+  __syncthreads();
+  {
+    static_assert(kSigRowChunk * 4 * 8 == kBlock, "one thread per (row, half tile, eighth)");
+    const int r = tid >> 5, h = (tid >> 3) & 3, pp = tid & 7;
+    const float* q8 = sq + r * kBlock + h * 64 + pp * 8;
+    float mn = q8[0], mx = q8[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) { mn = fminf(mn, q8[i]); mx = fmaxf(mx, q8[i]); }
+    mn = fminf(mn, dpp_movf<0xB1>(mn)); mx = fmaxf(mx, dpp_movf<0xB1>(mx));     // quad_perm [1,0,3,2]
+    mn = fminf(mn, dpp_movf<0x4E>(mn)); mx = fmaxf(mx, dpp_movf<0x4E>(mx));     // quad_perm [2,3,0,1]
+    mn = fminf(mn, dpp_movf<0x141>(mn)); mx = fmaxf(mx, dpp_movf<0x141>(mx));   // row_half_mirror
+    const int64_t hw2 = wb * (kBlock / 64) + h;
+    if (pp == 0 && r0 + r < n_rows && hw2 < n_halves)
+      reinterpret_cast<float2*>(tq)[(int64_t)(r0 + r) * n_halves + hw2] = q_range(mn, mx);
   }
 }
 
