@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-workers", type=int, default=None,
                     help="processes of the multi-core CPU baseline leg (default: this process's CPU share, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-R", default=None, metavar="DIR",
+                    help="after the timed loop, save this rank's R shard and its wavelength range under DIR "
+                         "(tests: the gathered shards against a single-rank run)")
     ap.add_argument("--cpu-sample-wavelengths", type=int, default=None,
                     help="oracle sample size (default: ~10 s of reference-speed CPU work per config)")
     return ap.parse_args()
@@ -78,12 +81,13 @@ def flops_per_eval(n_atoms: int) -> int:
     return 2 * n_atoms - 1 + 12
 
 
-def tau_bytes_per_launch(n_wav: int, n_orb: int, n_sigma: int) -> int:
+def tau_bytes_per_launch(n_wav: int, n_orb: int, n_sigma: int, sigma_rows: int = 1) -> int:
     """Algorithmic HBM bytes of one tau-kernel launch (DESIGN.md "Roofline"): R[n_orb][n_wav] written
-    and the n_sigma cross-section arrays the column kernel resampled (one per species, or one for
-    merged species) read once per wavelength; window records, windows and tail moments (~1 %) are not
+    and the resampled cross sections read once: n_sigma arrays (one per species, or one for merged
+    species) of sigma_rows rows (one per phase with orbital Doppler shift -- each phase sees its own
+    shifted sigma -- else one shared row); window records, windows and tail moments (~1 %) are not
     counted."""
-    return 8 * n_orb * n_wav + 8 * n_wav * n_sigma
+    return 8 * n_orb * n_wav + 8 * n_wav * n_sigma * sigma_rows
 
 
 def latest_profile_traffic(kernel: str, config: str):
@@ -200,7 +204,10 @@ def main():
         import torch.distributed as dist  # noqa: F811  (gloo: barrier + max-reduce of times only)
         dist.init_process_group("gloo")
     from prometheus_amd import _native, setupfile, gasProperties, sharding  # noqa: F401
-    _native.set_default_device(local_rank)
+    # one process per GPU; ranks beyond the visible devices share them round robin (a world-size-2 run on
+    # a one-GPU box puts both ranks on device 0)
+    dev_id = local_rank % max(1, _native.device_count())
+    _native.set_default_device(dev_id)
 
     cfg = global_config(args.config, world, args.scaling)
     cfg_name = args.config
@@ -209,7 +216,7 @@ def main():
         gasProperties.register_molecular_table("H2O", synthetic_molecular_table())
     t_setup = time.perf_counter()
     tr = setupfile.build_transit(cfg)   # lambda grid + device Voigt tables on this rank's GPU
-    dev = _native.get_device(local_rank)
+    dev = _native.get_device(dev_id)
     n_wav_global = len(tr.wavelength)
     w0, w1 = sharding.shard_for_rank(n_wav_global, world, rank)   # tile-aligned contiguous shards
     host = tr._host_inputs()
@@ -242,6 +249,11 @@ def main():
     sync()
     t1 = time.perf_counter()
     ms_runs = dev.timing_end(max_runs=args.steps)
+    if args.dump_R:
+        os.makedirs(args.dump_R, exist_ok=True)
+        np.save(os.path.join(args.dump_R, "R_rank%d.npy" % rank), dev.transit_result())
+        with open(os.path.join(args.dump_R, "range_rank%d.json" % rank), "w") as fh:
+            json.dump({"w0": int(w0), "w1": int(w1), "n_wav": int(n_wav_global), "world": world}, fh)
     if dist:
         dist.barrier()
     elapsed, total_pts = sharding.reduce_timing(dist, t1 - t0, n_pts_rank)
@@ -266,7 +278,10 @@ def main():
     n_atoms = st["tau_kernel_variant"] % 10 or prob.n_atoms
     cle = st["chord_lambda_evals"]
     evals = st["exp_evals"]
-    tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, n_atoms)
+    # one sigma row per phase unless every phase has the same Doppler factor (prom_api.hip uniform_shift)
+    same_shift = all(np.all(np.asarray(e["shift"]) == np.asarray(e["shift"])[0]) for e in host["scenarios"])
+    sigma_rows = 1 if same_shift else n_orb
+    tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, n_atoms, sigma_rows)
     achieved_gbs = tau_bytes / (tau_ms * 1e-3) / 1e9
     flops_unit = flops_per_eval(n_atoms)
     if tau_kernel == "k_tau_mol":
@@ -277,7 +292,7 @@ def main():
     traffic = latest_profile_traffic("prom::" + tau_kernel, cfg_name)
     # end-to-end (host prep + H2D + run + D2H) for reference, one call
     t_e2e = time.perf_counter()
-    R = tr.sumOverChords(devices=[local_rank]) if world == 1 else None
+    R = tr.sumOverChords(devices=[dev_id]) if world == 1 else None
     e2e_s = time.perf_counter() - t_e2e
     result = {
         "metric": "spectrum points/sec (phase x wavelength)",
@@ -299,7 +314,8 @@ def main():
                    "parallelism": "wavelength shards x%d (no collective)" % world},
         "roofline": {"bound": "hbm", "kernel": tau_kernel, "achieved": achieved_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic, "algorithmic_bytes": tau_bytes, "tau_ms": tau_ms,
+                     "traffic": traffic, "algorithmic_bytes": tau_bytes, "sigma_rows": sigma_rows,
+                     "tau_ms": tau_ms,
                      "tau_ms_source": tau_clock, "tau_ms_hip_events": tau_ms_events,
                      "tau_ms_sampled_runs": int(len(ms_runs)),
                      "exp_evals": evals, "chord_lambda_evals": cle,

@@ -1,0 +1,59 @@
+"""bench.py's multi-process path on the GPU: torch.distributed.run with two ranks (both on device 0 of a
+one-GPU box), wavelength shards without any collective on the data, gathered on the host and compared
+bitwise with a single-rank run of the same (strong-scaling) spectrum.  Reference: the chunker this
+replaces, memoryHandler.py:55-66; SURVEY.md 8(e)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(tmp, world, config):
+    out = os.path.join(tmp, "w%d" % world)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", str(world), "--steps", "3", "--warmup", "1", "--config", config, "--scaling", "strong",
+           "--no-cpu-baseline", "--dump-R", out]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    shards = []
+    for r in range(world):
+        with open(os.path.join(out, "range_rank%d.json" % r)) as fh:
+            rg = json.load(fh)
+        shards.append((rg["w0"], rg["w1"], np.load(os.path.join(out, "R_rank%d.npy" % r))))
+    return json.loads(line), shards
+
+
+@pytest.mark.parametrize("config", ["C2", "C4"])
+def test_two_rank_bench_gathers_bitwise(config, tmp_path):
+    res1, (s1,) = _bench(str(tmp_path), 1, config)
+    res2, sh = _bench(str(tmp_path), 2, config)
+    assert res2["n_gpus"] == 2 and res2["scaling"] == "strong"
+    n_wav = s1[2].shape[1]
+    assert s1[0] == 0 and s1[1] == n_wav
+    R = np.empty_like(s1[2])
+    edge = 0
+    for w0, w1, part in sh:
+        assert w0 == edge and part.shape == (R.shape[0], w1 - w0)
+        R[:, w0:w1] = part
+        edge = w1
+    assert edge == n_wav
+    assert np.array_equal(R, s1[2])
+    # whole-job points / s counts every rank's shard once
+    assert res2["config"]["global_wavelengths"] == res1["config"]["global_wavelengths"]
