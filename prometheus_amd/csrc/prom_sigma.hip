@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
   const int lane = tid & 63;
   const int64_t n_halves = 2 * ((n_wav + kTW - 1) / kTW);
   const int32_t nse = merge_sp ? 1 : NSIG;
-  const int64_t n_main = (int64_t)n_blk * n_rc;
+  const int64_t n_main = (int64_t)((n_blk + 7) / 8) * 8 * n_rc;
   if ((int64_t)blockIdx.x >= n_main) {
     const int64_t item = (int64_t)blockIdx.x - n_main;
     const int32_t n_fc = (n_rows + kSigFbRows - 1) / kSigFbRows;
@@ -165,8 +165,12 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
     }
     return;
   }
-  const int64_t wb = blockIdx.x / n_rc;
-  const int32_t r0 = (int32_t)(blockIdx.x % n_rc) * kSigRowChunk;
+  // XCD-aware order (workgroup i runs on XCD i % 8): the n_rc row chunks of a block are 8 workgroups apart,
+  // so they share an XCD's L2 for the block's slices
+  const int64_t grp = blockIdx.x / (8 * n_rc), rem = blockIdx.x % (8 * n_rc);
+  const int64_t wb = grp * 8 + rem % 8;
+  const int32_t r0 = (int32_t)(rem / 8) * kSigRowChunk;
+  if (wb >= n_blk) return;
   bool lds_ok = true;
 #pragma unroll
   for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && seg[wb * NSIG + s].kind == 1;
@@ -180,11 +184,12 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
     const SigTabDev& tb = tabv.t[s];
     const SigSeg sg = seg[wb * NSIG + s];
     if (s > 0) __syncthreads();   // the previous species' slice is no longer read
+    // the x and f arrays (16 bytes a node); slopes divided here, once per node and workgroup
     for (int32_t i = tid; i < sg.m; i += kBlock) {
-      const double4 q = tb.rec[sg.lo + i];
-      sx[i] = q.x;
-      sxf[i] = make_double2(q.x, q.y);
-      ssl[i] = q.z;
+      const double xv = tb.x[sg.lo + i], yv = tb.y[sg.lo + i];
+      sx[i] = xv;
+      sxf[i] = make_double2(xv, yv);
+      if (i + 1 < sg.m) ssl[i] = (tb.y[sg.lo + i + 1] - yv) / (tb.x[sg.lo + i + 1] - xv);
     }
     __syncthreads();
 #pragma unroll
@@ -238,7 +243,7 @@ void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const 
   const int32_t n_blk = (int32_t)grid_for(n_wav);
   const int32_t n_rc = (n_rows + kSigRowChunk - 1) / kSigRowChunk;
   const int32_t n_fc = (n_rows + kSigFbRows - 1) / kSigFbRows;
-  const unsigned nb = (unsigned)((int64_t)n_blk * n_rc + (int64_t)n_fb * n_fc);
+  const unsigned nb = (unsigned)((int64_t)((n_blk + 7) / 8) * 8 * n_rc + (int64_t)n_fb * n_fc);
 #define PROM_SIGR(NS)                                                                                        \
   hipExtLaunchKernelGGL((k_sigma_rows<NS>), dim3(nb), dim3(kBlock), 0, s, ev_start, nullptr, 0, tabv, wav, n_wav, \
                         n_rows, seg, fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl)
