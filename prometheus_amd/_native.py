@@ -310,8 +310,12 @@ class Device:
         self._check(self.lib.prom_transit_run(self.h, C.byref(st) if st is not None else None), "prom_transit_run")
         return st.as_dict() if st is not None else None
 
-    def transit_result(self) -> np.ndarray:
-        out = np.empty(self._shape)
+    def transit_result(self, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """R of the last run, [n_orb, n_wav]; ``out``: a C-contiguous float64 array of that shape to fill."""
+        if out is None:
+            out = np.empty(self._shape)
+        elif out.shape != self._shape or out.dtype != np.float64 or not out.flags.c_contiguous:
+            raise ValueError("transit_result: out must be a C-contiguous float64 array of shape %s" % (self._shape,))
         self._check(self.lib.prom_transit_result(self.h, _d(out)), "prom_transit_result")
         return out
 

@@ -51,7 +51,7 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = OUT, 
 
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+    cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-pthread", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True, cwd=HERE)

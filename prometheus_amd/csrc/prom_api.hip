@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstring>
 #include <exception>
+#include <thread>
 
 #include "prom_internal.h"
 
@@ -140,6 +141,8 @@ void prom_destroy(prom_ctx* ctx) {
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->tev) (void)hipEventDestroy(e);
+  for (auto& e : ctx->pin_ev) (void)hipEventDestroy(e);
+  if (ctx->pin) (void)hipHostFree(ctx->pin);
   for (auto& st : ctx->streams)
     if (st) {
       (void)hipStreamSynchronize(st);
@@ -661,7 +664,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
             int64_t j = (int64_t)(std::upper_bound(X.begin(), X.end(), v) - X.begin()) - 1;
             return j < 0 ? 0 : (j > n - 2 ? n - 2 : j);
           };
-          for (int64_t b = 0; ok && b < nb; ++b) {
+          auto blocks = [&](int64_t b0, int64_t b1) {
+          for (int64_t b = b0; ok && b < b1; ++b) {
             double lmin = INFINITY, lmax = -INFINITY;
             bool fin = true;
             for (int64_t w = b * prom::kSigBlockW; w < std::min<int64_t>(tr.n_wav, (b + 1) * prom::kSigBlockW); ++w) {
@@ -705,6 +709,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
               e.inv = inv;
             }
           }
+          };
+          // independent blocks: split over host threads (the guess verification visits every slice node)
+          const int64_t n_thr = std::max<int64_t>(1, std::min<int64_t>(8, nb / 64));
+          std::vector<std::thread> pool;
+          for (int64_t t = 1; t < n_thr; ++t) pool.emplace_back(blocks, nb * t / n_thr, nb * (t + 1) / n_thr);
+          blocks(0, nb / n_thr);
+          for (auto& th : pool) th.join();
           ++ia;
         }
         upload(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
@@ -958,8 +969,46 @@ int32_t prom_transit_result(prom_ctx* ctx, double* R_out) {
     if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_result: no completed run");
     PROM_REQUIRE(R_out, "prom_transit_result: null output");
     for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
-    download(R_out, tr.slot[tr.last].R, (int64_t)tr.n_orb * tr.n_wav, ctx->stream);
-    PROM_HIP(hipStreamSynchronize(ctx->stream));
+    // D2H in chunks into pinned staging (one DMA per chunk, full link rate) while host threads copy the
+    // finished chunks out to the caller's (pageable) array: the copy-out overlaps the transfer and runs on
+    // several cores instead of one
+    const size_t bytes = sizeof(double) * (size_t)tr.n_orb * (size_t)tr.n_wav;
+    constexpr size_t kChunk = (size_t)2 << 20;
+    const size_t n_chunks = (bytes + kChunk - 1) / kChunk;
+    if (ctx->pin_cap < bytes) {
+      if (ctx->pin) PROM_HIP(hipHostFree(ctx->pin));
+      ctx->pin = nullptr;
+      ctx->pin_cap = 0;
+      PROM_HIP(hipHostMalloc(&ctx->pin, bytes, hipHostMallocDefault));
+      ctx->pin_cap = bytes;
+    }
+    while (ctx->pin_ev.size() < n_chunks) {
+      hipEvent_t e;
+      PROM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->pin_ev.push_back(e);
+    }
+    const char* src = static_cast<const char*>(tr.slot[tr.last].R.p);
+    char* pin = static_cast<char*>(ctx->pin);
+    for (size_t c = 0; c < n_chunks; ++c) {
+      const size_t off = c * kChunk, len = std::min(kChunk, bytes - off);
+      PROM_HIP(hipMemcpyAsync(pin + off, src + off, len, hipMemcpyDeviceToHost, ctx->stream));
+      PROM_HIP(hipEventRecord(ctx->pin_ev[c], ctx->stream));
+    }
+    const size_t n_thr = std::min<size_t>(n_chunks, 8);
+    std::vector<hipError_t> errs(n_thr, hipSuccess);
+    auto copier = [&](size_t t) {
+      for (size_t c = t; c < n_chunks; c += n_thr) {
+        const hipError_t e = hipEventSynchronize(ctx->pin_ev[c]);
+        if (e != hipSuccess) { errs[t] = e; return; }
+        const size_t off = c * kChunk, len = std::min(kChunk, bytes - off);
+        std::memcpy(reinterpret_cast<char*>(R_out) + off, pin + off, len);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < n_thr; ++t) pool.emplace_back(copier, t);
+    copier(0);
+    for (auto& th : pool) th.join();
+    for (auto e : errs) PROM_HIP(e);
   });
 }
 

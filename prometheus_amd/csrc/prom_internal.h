@@ -314,6 +314,10 @@ struct prom_ctx {
   int32_t timed_runs = 0;
   int32_t timing_stride = 1;     // prom_timing_stride: events on every k-th run of a timing window
   int64_t window_runs = 0;       // runs since prom_timing_begin
+  // prom_transit_result: pinned staging for the D2H of R, copied out by host threads chunk by chunk
+  void* pin = nullptr;
+  size_t pin_cap = 0;
+  std::vector<hipEvent_t> pin_ev;
 };
 
 namespace prom {

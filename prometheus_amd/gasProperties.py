@@ -745,7 +745,10 @@ class Transit:
                         dev.transit_set(self._problem(dev, host, a, b, cull_tau, options))
                         st = dev.transit_run(stats=True)
                         if R is not None:
-                            R[:, a:b] = dev.transit_result()
+                            if a == 0 and b == n_wav:   # one chunk: straight into the result
+                                dev.transit_result(out=R)
+                            else:
+                                R[:, a:b] = dev.transit_result()
                         if acc is not None:
                             part = dev.transit_band_stats(bounds)
                             with acc_lock:
