@@ -112,6 +112,13 @@ int32_t prom_create(int32_t device, prom_ctx** out) {
     delete ctx;
     return PROM_E_HIP;
   }
+  for (int i = 0; i < prom::kMaxSlots; ++i) {
+    if (hipEventCreateWithFlags(&ctx->fork_ev[i], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming) != hipSuccess) {
+      prom_destroy(ctx);
+      return PROM_E_HIP;
+    }
+  }
   for (auto& e : ctx->ev) {
     if (hipEventCreate(&e) != hipSuccess) {
       delete ctx;
@@ -142,6 +149,10 @@ void prom_destroy(prom_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->tev) (void)hipEventDestroy(e);
   for (auto& e : ctx->pin_ev) (void)hipEventDestroy(e);
+  for (int i = 0; i < prom::kMaxSlots; ++i) {
+    if (ctx->fork_ev[i]) (void)hipEventDestroy(ctx->fork_ev[i]);
+    if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
+  }
   if (ctx->pin) (void)hipHostFree(ctx->pin);
   for (auto& st : ctx->streams)
     if (st) {
@@ -894,6 +905,13 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     const int si = (tr.last + 1) % tr.depth;
     const hipStream_t st = ctx->streams[si];
     prom::RunSlot& rs = tr.slot[si];
+    // the slot's second stream: the one kMaxSlots / 2 away (free when depth <= kMaxSlots / 2); PROM_SIGMA_FORK=0
+    // keeps every kernel of a run on one stream
+    const char* fk = std::getenv("PROM_SIGMA_FORK");
+    const bool fork_ok = tr.depth <= prom::kMaxSlots / 2 && !(fk && std::atoi(fk) == 0);
+    rs.aux = fork_ok ? ctx->streams[si + prom::kMaxSlots / 2] : nullptr;
+    rs.ev_fork = fork_ok ? ctx->fork_ev[si] : nullptr;
+    rs.ev_join = fork_ok ? ctx->join_ev[si] : nullptr;
     if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
     if (!stats && !timed && tr.graphs && tr.depth > 1) {
       // untimed fast-path run: replay the slot's graph (captured here the first time)

@@ -215,6 +215,10 @@ struct RunSlot {
                                             //     list [n_orb * 2 n_tiles], then big list [n_orb * 2 n_tiles] int4
   DevBuf hcnt;                              // ... their counts (int32 small, big; zeroed by k_columns8)
   DevBuf R;                                 // [n_orb][n_wav]
+  // second stream of the slot and its fork / join events (the Doppler sigma rows run beside the column
+  // and ordering kernels); set per run by prom_transit_run, null: one stream
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 // Everything the transit kernels need, as device pointers.
@@ -318,6 +322,7 @@ struct prom_ctx {
   void* pin = nullptr;
   size_t pin_cap = 0;
   std::vector<hipEvent_t> pin_ev;
+  hipEvent_t fork_ev[prom::kMaxSlots] = {}, join_ev[prom::kMaxSlots] = {};
 };
 
 namespace prom {

@@ -557,10 +557,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
                                                    double* __restrict__ fsum,
                                                    int32_t* __restrict__ wenv,
                                                    double* __restrict__ wmom,
-                                                   const float4* __restrict__ tq, int32_t tq_rows,
-                                                   int32_t n_tiles, int64_t n_wav,
-                                                   int4* __restrict__ trec, int4* __restrict__ hlist, int64_t hcap,
-                                                   int32_t* __restrict__ hcnt, double btail) {
+                                                   double btail) {
   constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int NW = kWBlock / 64;
@@ -577,7 +574,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   __shared__ double pd_[NW][2];
   __shared__ double pm_[NW][K + 2];
   __shared__ int32_t pg_[NW];
-  __shared__ int32_t sHc[4];                     // step 7: heavy entries staged in LDS (small, big), global bases
   const int32_t o = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int32_t* fl = flags + (int64_t)o * n_pr;
@@ -588,14 +584,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   for (int s = 0; s < NS; ++s) cs[s] = tabv.t[s].ncoef;
 
   PROM_TS(o * 16 + 0);
-  constexpr int TQP = 4;   // tiles per thread whose Q range is loaded now, for step 7
-  float4 tqv[TQP];
-#pragma unroll
-  for (int k = 0; k < TQP; ++k) {
-    const int32_t tl = tid + k * kWBlock;
-    tqv[k] = (tq && tl < n_tiles) ? tq[(tq_rows > 1 ? (int64_t)o * n_tiles : 0) + tl] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-  if (tid < 2) sHc[tid] = 0;   // (barriers of steps 1-6 order it before step 7)
   for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }
   // ---- 1. load, classify, keys, combined scan/reduction.  Active chords whose bound b is below btail
   //         (b Q < the tail epsilon at every wavelength of the problem) are tail records everywhere: they
@@ -1020,87 +1008,6 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         et[tid * PT + k] = cb[k] + bc;
         et[kEnvN + tid * PT + k] = ca_[k] + ac;
       }
-      if (tq) {
-        // the tables stay in LDS (over the histograms) for the per-tile windows below
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < PT; ++k) {
-          hB[tid * PT + k] = cb[k] + bc;
-          hA[tid * PT + k] = ca_[k] + ac;
-        }
-      }
-    }
-  }
-  if (tq) {
-    // ---- 7. tau window [h, t) of every wavelength tile for this phase (Q ranges per half tile from
-    //         k_columns8: one row per phase with orbital Doppler shift, else one shared row), exactly as
-    //         k_tau_w would pick it from the tables for the tile's union Q range.  With trec (the planned
-    //         tau kernel): the tile record {h, t, flags, tail moments at t}; a tile whose window holds more
-    //         than kHeavy records instead becomes two heavy entries, one per live 64-wavelength half, each
-    //         with the window of its own Q range: halves of at most kChunk records go to the small list
-    //         (one wavefront each), longer ones to the big list (one workgroup each, chunks of kChunk).
-    //         Two global counters (zeroed by k_columns8); list order is free.
-    __syncthreads();   // moments (step 6) visible to the whole workgroup
-    PROM_TS(o * 16 + 5);
-    const bool wtab = sorted && window;
-    const int32_t pfl = (sorted ? 1 : 0) | (nnf ? 4 : 0);
-    constexpr int HCAP = (int)(sizeof(skey) / (sizeof(int4))) / 2;   // staged entries per list
-    int4* hbuf = reinterpret_cast<int4*>(skey);                    // [0, HCAP) small, [HCAP, 2 HCAP) big
-    const float4* tqo = tq + (tq_rows > 1 ? (int64_t)o * n_tiles : 0);
-    const int32_t t_all = sorted ? G : nact;
-    auto window_of = [&](float ql, float qh, int32_t* hp, int32_t* tp) {
-      int32_t h = 0, t = t_all;
-      if (wtab && ql >= 0.0f) {
-        const int vt = env_floor((float)tail_eps<NS>() / qh * (1.0f - 0x1p-20f));
-        const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
-        t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : hB[vt - kEnvVmin]);
-        h = vh >= kEnvVmax ? 0 : hA[vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin];
-      }
-      *hp = h < t ? h : t;
-      *tp = t;
-    };
-    auto tile_window = [&](int32_t tl, float4 q) {
-      const bool live1 = (int64_t)tl * kTW + 64 < n_wav;   // the second half holds wavelengths
-      const bool bad = q.x < 0.0f || (live1 && q.z < 0.0f);
-      const float ql = bad ? -1.0f : (live1 ? fminf(q.x, q.z) : q.x);
-      const float qh = bad ? 0.0f : (live1 ? fmaxf(q.y, q.w) : q.y);
-      int32_t h, t;
-      window_of(ql, qh, &h, &t);
-      const int32_t fl = pfl | ((wtab && t < G) ? 2 : 0);
-      trec[(int64_t)o * n_tiles + tl] = make_int4(h, t, fl, 0);
-      if (hlist) {
-        if (!nnf && t - h > kHeavy) {
-          // staged in LDS over the sort keys (free after step 6); one global append per list and workgroup
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-            if (hf == 1 && !live1) continue;
-            int32_t hh, tt;
-            window_of(hf ? q.z : q.x, hf ? q.w : q.y, &hh, &tt);
-            const int32_t ff = pfl | ((wtab && tt < G) ? 2 : 0);
-            const int4 e = make_int4(2 * tl + hf, hh, tt, ff | (o << 8));
-            const int big = tt - hh > kChunk ? 1 : 0;
-            const int32_t k = atomicAdd(&sHc[big], 1);
-            if (k < HCAP) hbuf[big * HCAP + k] = e;
-            else hlist[(int64_t)big * hcap + atomicAdd(&hcnt[big], 1)] = e;
-          }
-        }
-      }
-    };
-#pragma unroll
-    for (int k = 0; k < TQP; ++k) {
-      const int32_t tl = tid + k * kWBlock;
-      if (tl < n_tiles) tile_window(tl, tqv[k]);
-    }
-    for (int32_t tl = tid + TQP * kWBlock; tl < n_tiles; tl += kWBlock) tile_window(tl, tqo[tl]);
-    if (hlist) {
-      __syncthreads();
-      const int32_t ns = sHc[0] < HCAP ? sHc[0] : HCAP;
-      const int32_t nb = sHc[1] < HCAP ? sHc[1] : HCAP;
-      if (tid == 0) sHc[2] = ns > 0 ? atomicAdd(&hcnt[0], ns) : 0;
-      if (tid == 64) sHc[3] = nb > 0 ? atomicAdd(&hcnt[1], nb) : 0;
-      __syncthreads();
-      for (int32_t i = tid; i < ns; i += kWBlock) hlist[sHc[2] + i] = hbuf[i];
-      for (int32_t i = tid; i < nb; i += kWBlock) hlist[hcap + sHc[3] + i] = hbuf[HCAP + i];
     }
   }
   if (tid == 0) {
@@ -1116,6 +1023,86 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     counts[o * kCnt + 7] = 0;
   }
   PROM_TS(o * 16 + 8);
+}
+
+// ---- tile windows (the planned path's step after k_order) -------------------------------------------------
+// The tau window [h, t) of every (phase, 128-wavelength tile) from the phase's threshold tables (k_order,
+// wenv) and the tile's Q range (tq: two halves per tile; one row per phase with orbital Doppler shift,
+// else one shared row), exactly as k_tau_w would pick it for the tile's union Q range: the tile record
+// {h, t, flags}; a tile whose window holds more than kHeavy records instead becomes two heavy entries, one
+// per live 64-wavelength half, each with the window of its own Q range: halves of at most kChunk records go
+// to the small list (one wavefront each in k_tau_p), longer ones to the big list (one workgroup each).  Two
+// global counters (zeroed by k_columns8); list order is free.  A workgroup per (256 tiles, phase): the
+// phase's tables are staged in LDS and its entries appended with one global atomic per list.  Its own
+// kernel (not k_order's last step), so the ordering does not wait for the Doppler sigma rows.
+template <int NS>
+__global__ void __launch_bounds__(kBlock) k_windows(const float4* __restrict__ tq, int32_t tq_rows, int32_t n_tiles,
+                                                    int64_t n_wav, const int32_t* __restrict__ counts,
+                                                    const int32_t* __restrict__ wenv, int4* __restrict__ trec,
+                                                    int4* __restrict__ hlist, int64_t hcap,
+                                                    int32_t* __restrict__ hcnt) {
+  constexpr int HCAP = 2 * kBlock;   // a workgroup's tiles give at most two entries each
+  __shared__ int32_t stab[2 * kEnvN];
+  __shared__ int4 hbuf[2][HCAP];
+  __shared__ int32_t sHc[4];
+  const int32_t o = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int32_t tl = blockIdx.x * kBlock + tid;
+  const int32_t* c = counts + o * kCnt;
+  const int32_t nact = c[0], nnf = c[3], G = c[4];
+  const bool sorted = c[5] != 0, wtab = c[6] != 0;
+  const float4 q = tl < n_tiles ? tq[(tq_rows > 1 ? (int64_t)o * n_tiles : 0) + tl] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (wtab) {
+    const int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
+    for (int i = tid; i < 2 * kEnvN; i += kBlock) stab[i] = et[i];
+  }
+  if (tid < 2) sHc[tid] = 0;
+  __syncthreads();
+  const int32_t* hB = stab;
+  const int32_t* hA = stab + kEnvN;
+  const int32_t pfl = (sorted ? 1 : 0) | (nnf ? 4 : 0);
+  const int32_t t_all = sorted ? G : nact;
+  auto window_of = [&](float ql, float qh, int32_t* hp, int32_t* tp) {
+    int32_t h = 0, t = t_all;
+    if (wtab && ql >= 0.0f) {
+      const int vt = env_floor((float)tail_eps<NS>() / qh * (1.0f - 0x1p-20f));
+      const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
+      t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : hB[vt - kEnvVmin]);
+      h = vh >= kEnvVmax ? 0 : hA[vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin];
+    }
+    *hp = h < t ? h : t;
+    *tp = t;
+  };
+  if (tl < n_tiles) {
+    const bool live1 = (int64_t)tl * kTW + 64 < n_wav;   // the second half holds wavelengths
+    const bool bad = q.x < 0.0f || (live1 && q.z < 0.0f);
+    const float ql = bad ? -1.0f : (live1 ? fminf(q.x, q.z) : q.x);
+    const float qh = bad ? 0.0f : (live1 ? fmaxf(q.y, q.w) : q.y);
+    int32_t h, t;
+    window_of(ql, qh, &h, &t);
+    const int32_t fl = pfl | ((wtab && t < G) ? 2 : 0);
+    trec[(int64_t)o * n_tiles + tl] = make_int4(h, t, fl, 0);
+    if (hlist && !nnf && t - h > kHeavy) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        if (hf == 1 && !live1) continue;
+        int32_t hh, tt;
+        window_of(hf ? q.z : q.x, hf ? q.w : q.y, &hh, &tt);
+        const int32_t ff = pfl | ((wtab && tt < G) ? 2 : 0);
+        const int4 e = make_int4(2 * tl + hf, hh, tt, ff | (o << 8));
+        const int big = tt - hh > kChunk ? 1 : 0;
+        hbuf[big][atomicAdd(&sHc[big], 1)] = e;
+      }
+    }
+  }
+  if (!hlist) return;
+  __syncthreads();
+  const int32_t ns = sHc[0], nb = sHc[1];
+  if (tid == 0) sHc[2] = ns > 0 ? atomicAdd(&hcnt[0], ns) : 0;
+  if (tid == 64) sHc[3] = nb > 0 ? atomicAdd(&hcnt[1], nb) : 0;
+  __syncthreads();
+  for (int32_t i = tid; i < ns; i += kBlock) hlist[sHc[2] + i] = hbuf[0][i];
+  for (int32_t i = tid; i < nb; i += kBlock) hlist[hcap + sHc[3] + i] = hbuf[1][i];
 }
 
 // Fused sigma lookup -> tau -> exp(-tau) -> disk sum -> ratio.
@@ -2016,13 +2003,23 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
     // orbital Doppler shift with sigma segments: the rows come from their own kernel (k_sigma_rows)
     const bool rows_seg = pre_sigma && sig_rows > 1 && tr.sig_seg_ok;
+    const bool sig_fork = rows_seg && rs.aux && rs.ev_fork && rs.ev_join;
     const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
     const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
     if (rows_seg) {
-      launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
-                        tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale,
-                        rs.zfl.as<uint8_t>(), ev0);
-      ev0 = nullptr;
+      // the sigma rows do not depend on the columns or the ordering: with a second stream for the slot they
+      // run beside k_columns8 / k_order (VALU-bound full chip beside latency-bound per-phase workgroups) and
+      // join before the tile windows
+      if (sig_fork) {
+        PROM_HIP(hipEventRecord(rs.ev_fork, s));
+        PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
+      }
+      launch_sigma_rows(sig_fork ? rs.aux : s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
+                        tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(),
+                        rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(),
+                        sig_fork ? nullptr : ev0);
+      if (sig_fork) PROM_HIP(hipEventRecord(rs.ev_join, rs.aux));
+      else ev0 = nullptr;
     }
 #define PROM_COLS(SV, NSV)                                                                               \
   hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
@@ -2091,15 +2088,13 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   const int64_t hcap = (int64_t)tr.n_orb * 2 * n_wtiles;   // heavy entries per list: at most one per half tile
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
-  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, ev_ord, 0,             \
+  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, pre_sigma ? nullptr : ev_ord, 0, \
                      rs.flags.as<int32_t>(),                                                              \
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
                      tr.window ? 1 : 0, tabs4, rs.recs.as<double>(),                                     \
                      rs.act_ip.as<int32_t>(), rs.mrecs.as<double>(), rs.counts.as<int32_t>(),            \
                      rs.tsum.as<double>(), rs.fsum.as<double>(), rs.wenv.as<int32_t>(), rs.wmom.as<double>(), \
-                     pre_sigma ? rs.tq.as<float4>() : nullptr, sig_rows, n_wtiles, tr.n_wav,            \
-                     rs.trec.as<int4>(), (pre_sigma && tr.plan) ? rs.hlist.as<int4>() : nullptr, hcap, \
-                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, btail)
+                     btail)
     // always-tail threshold: b Q < the tail epsilon at every wavelength.  Any value keeps R exact (the
     // unsorted records' envelope is btail itself); a tight one keeps most far chords out of the sort.  The
     // factor 2^-1/4 keeps btail below every window threshold the tables can return (1/8-octave slots
@@ -2114,6 +2109,23 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       default: PROM_CHW(4); break;
     }
 #undef PROM_CHW
+    if (pre_sigma) {
+      // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
+      if (sig_rows > 1 && tr.sig_seg_ok && rs.aux && rs.ev_join) PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
+      const dim3 gw((unsigned)((n_wtiles + kBlock - 1) / kBlock), (unsigned)tr.n_orb);
+#define PROM_WIN(NSV)                                                                                    \
+  hipExtLaunchKernelGGL(k_windows<NSV>, gw, dim3(kBlock), 0, s, nullptr, ev_ord, 0, rs.tq.as<float4>(),      \
+                        sig_rows, n_wtiles, tr.n_wav, rs.counts.as<int32_t>(), rs.wenv.as<int32_t>(),       \
+                        rs.trec.as<int4>(), tr.plan ? rs.hlist.as<int4>() : nullptr, hcap,                  \
+                        tr.plan ? rs.hcnt.as<int32_t>() : nullptr)
+      switch (na) {
+        case 1: PROM_WIN(1); break;
+        case 2: PROM_WIN(2); break;
+        case 3: PROM_WIN(3); break;
+        default: PROM_WIN(4); break;
+      }
+#undef PROM_WIN
+    }
   } else {
     hipLaunchKernelGGL(k_chords, dim3(tr.n_orb), dim3(kChordBlock), 0, s, rs.flags.as<int32_t>(),
                        tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
