@@ -415,9 +415,30 @@ def gen_harness():
     _save("harness", **out)
 
 
+def gen_lightcurve():
+    """mainRetrieval.py's light-curve extraction (:73-93), executed from the reference's own source text:
+    the section from `filterBandwidth = ...` to `lightcurve = np.array(lightcurve)` runs with the
+    reference's planet, constants and an R the reference computed (the exomoon fixture's problem).  The
+    script as a whole cannot run here (its source-rate file is a path on the author's machine)."""
+    with open(os.path.join(REF, "mainRetrieval.py")) as fh:
+        text = fh.read()
+    a = text.index("filterBandwidth = ")
+    b = text.index("lightcurve = np.array(lightcurve)") + len("lightcurve = np.array(lightcurve)")
+    code = compile(text[a:b], os.path.join(REF, "mainRetrieval.py"), "exec")
+    cfg = configs.fixture_configs()["exomoon"]
+    tr, lst, sgrid = reference_transit(cfg)
+    R = tr.sumOverChords(max_memory_gb=2.0)
+    planet = bodies.AvailablePlanets().findPlanet(cfg["Architecture"]["planetName"])
+    g = {"np": np, "const": const, "W49b": planet, "R": R, "wavelength": tr.wavelength,
+         "orbphase": sgrid.constructOrbphaseAxis()}
+    exec(code, g)
+    _save("lightcurve", R=R, wavelength=tr.wavelength, orbphase=g["orbphase"], lightcurve=g["lightcurve"],
+          config=np.array(json.dumps(cfg)))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["interp", "tables", "density", "grids", "molecular", "transits", "stars",
-                             "serpens", "tidal", "harness"]
+                             "serpens", "tidal", "harness", "lightcurve"]
     if "interp" in which:
         gen_interp_kats()
     if "tables" in which:
@@ -438,3 +459,5 @@ if __name__ == "__main__":
         gen_tidal()
     if "harness" in which:
         gen_harness()
+    if "lightcurve" in which:
+        gen_lightcurve()

@@ -534,3 +534,13 @@ def test_setup_harness_golden(dev, name, tmp_path):
     assert a.shape == b.shape
     assert np.array_equal(a[0, 1:], b[0, 1:]) and np.array_equal(a[1:, 0], b[1:, 0])
     assert rel(a[1:, 1:], b[1:, 1:]) < R_TOL
+
+
+def test_band_lightcurve_reference_script(dev):
+    """Transit.bandLightcurve (k_band_stats over R in HBM) against the light curve computed by the
+    reference's own mainRetrieval.py section (lightcurve.npz): the light curve is pinned, not only restated."""
+    d = load("lightcurve")
+    tr = _product_transit(json.loads(str(d["config"])))
+    lc, R = tr.bandLightcurve(return_spectrum=True)
+    assert rel(R, d["R"]) < R_TOL
+    assert rel(lc, d["lightcurve"]) < R_TOL

@@ -124,3 +124,13 @@ def test_harness_oracle_and_writer(name, tmp_path):
     out = tmp_path / "out.txt"
     setupfile.write_output(str(out), wav, orb, R)
     assert out.read_text() == ref_text
+
+
+def test_lightcurve_oracle_matches_reference_script():
+    """The oracle's light curve (mainRetrieval.py:73-93 restated) on the reference's R equals the light curve
+    the reference's own script section computed (lightcurve.npz)."""
+    d = load("lightcurve")
+    cfg = json.loads(str(d["config"]))
+    planet = O.load_planet(cfg["Architecture"]["planetName"])
+    lc = O.lightcurve(d["R"], d["wavelength"], d["orbphase"], planet)
+    assert np.array_equal(lc, d["lightcurve"])
