@@ -266,8 +266,11 @@ def main():
     # not apply); mean launch duration from the start/stop events carried on its own dispatch packets
     # over the timed runs
     # (molecular species: the fused molecular kernel k_tau_mol)
+    # variant // 10: 3 planned tau kernel on sigma rows, 5 planned with the Doppler sigma fused in
+    tv = st.get("tau_kernel_variant", 0) // 10
+    fused = tv == 5
     tau_kernel = ("k_tau_mol" if getattr(prob, "n_molecules", 0) else
-                  "k_tau_p" if st.get("tau_kernel_variant", 0) // 10 == 3 else "k_tau_w")
+                  "k_tau_p" if tv in (3, 5) else "k_tau_w")
     # k_tau_p: its span on the device clock (first workgroup start -> last workgroup end), which is what
     # rocprofv3's dispatch durations measure; the HIP event pair (ordering kernel done -> tau kernel
     # done) also holds the tau kernel's dispatch behind the ordering kernel and is reported beside it
@@ -283,7 +286,8 @@ def main():
     # one sigma row per phase unless every phase has the same Doppler factor (prom_api.hip uniform_shift)
     same_shift = all(np.all(np.asarray(e["shift"]) == np.asarray(e["shift"])[0]) for e in host["scenarios"])
     sigma_rows = 1 if same_shift else n_orb
-    tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, n_atoms, sigma_rows)
+    # fused: no sigma rows are read (the kernel looks the cross sections up in the tables itself)
+    tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, 0 if fused else n_atoms, sigma_rows) + (8 * (w1 - w0) if fused else 0)
     achieved_gbs = tau_bytes / (tau_ms * 1e-3) / 1e9
     flops_unit = flops_per_eval(n_atoms)
     if tau_kernel == "k_tau_mol":
@@ -320,6 +324,8 @@ def main():
                      "tau_ms": tau_ms,
                      "tau_ms_source": tau_clock, "tau_ms_hip_events": tau_ms_events,
                      "tau_ms_sampled_runs": int(len(ms_runs)),
+                     "fused_sigma": fused,
+                     "sigma_lookups": (n_orb * (w1 - w0) * prob.n_atoms) if fused else 0,
                      "exp_evals": evals, "chord_lambda_evals": cle,
                      "valu": {"flops": flops, "flops_per_exp_eval": flops_unit,
                               "achieved_tflops": flops / (tau_ms * 1e-3) / 1e12,

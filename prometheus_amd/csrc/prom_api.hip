@@ -863,6 +863,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       rs.hcnt.ensure(sizeof(int32_t) * 4);
       rs.trec.ensure(sizeof(int32_t) * 4 * n_orb * n_wtiles);   // {h, t, flags, 0} per (phase, tile)
       tr.taup_resident = 0;
+      tr.taup_resident_f = 0;
       rs.tsum.ensure(sizeof(double) * n_orb);
       rs.fsum.ensure(sizeof(double) * n_orb);
       rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);

@@ -126,6 +126,82 @@ __device__ __forceinline__ double sigma_of(double t, const SigTabDev& tb) {
   return exp10(v) - tb.offset;
 }
 
+// numpy.interp of one target from its bracket guess g (within one node of the bracket, SigSeg): x_g and
+// x_{g+1} decide between g - 1, g and g + 1, then the bracket's record {x, f, slope} gives the value --
+// two dependent reads, no branches on the common path.  X2(g) reads x_g and x_{g+1}, REC(k, ...) node k's
+// x, f and slope.
+template <class XF, class RF>
+__device__ __forceinline__ double interp_guess(double t, int32_t g, XF X2, RF REC) {
+  const double2 xg = X2(g);   // x_g, x_{g+1}
+  const int32_t k = t < xg.x ? g - 1 : (t >= xg.y ? g + 1 : g);
+  double xa, fa, sl;
+  REC(k, xa, fa, sl);
+  // numpy: an exact node hit returns f; with a finite slope sl (t - x) + f is that f already, so the
+  // test is only needed where the interpolation is NaN (non-finite slope), as is numpy's right-node retry
+  double rv = sl * (t - xa) + fa;
+  if (rv != rv) {
+    if (xa == t) rv = fa;
+    else {
+      double xb, fb, sb;
+      REC(k + 1, xb, fb, sb);
+      rv = sl * (t - xb) + fb;
+      if (rv != rv && fa == fb) rv = fa;
+    }
+  }
+  return rv;
+}
+
+__device__ __forceinline__ int32_t seg_guess(double t, double xs, double inv, int32_t m) {
+  // = (f < 0 ? 0 : f >= m - 2 ? m - 2 : (int)f), the host's verified map (NaN t never reaches here)
+  const double f = (t - xs) * inv;
+  return (int32_t)__builtin_fmin(__builtin_fmax(f, 0.0), (double)(m - 2));
+}
+
+// sigma_s(t) for the fused Doppler path (no sigma rows in HBM): the verified linear guess of the target's
+// 256-wavelength block (SigSeg, kind > 0) and two dependent reads of the global x / f arrays (numpy's slope
+// divided here), else the directory lookup.  Bit for bit the value k_sigma_rows would have stored.
+__device__ __forceinline__ double sigma_seg(double t, const SigTabDev& tb, const SigSeg& sg) {
+  if (sg.kind > 0) {
+    const double* __restrict__ gx = tb.x + sg.lo;
+    const double* __restrict__ gy = tb.y + sg.lo;
+    const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+    return exp10(interp_guess(
+               t, g, [&](int32_t i) { return make_double2(gx[i], gx[i + 1]); },
+               [&](int32_t i, double& x, double& f, double& sl) {
+                 x = gx[i]; f = gy[i];
+                 sl = (gy[i + 1] - f) / (gx[i + 1] - x);
+               })) - tb.offset;
+  }
+  return sigma_of(t, tb);
+}
+
+// The tau kernel's cross sections at (phase o, wavelength lam) on the fused path: FS table species; NS == 1
+// with FS > 1 is the merged absorber Y = sum_s chi_s sigma_s (and z: some chi_s sigma_s not > 0), else the
+// species' sigma_s.
+template <int FS, int NS>
+__device__ __forceinline__ void fused_sigma(const SigTabs4& tabf, const SigSeg* __restrict__ sg, int32_t o, double lam,
+                                            double (&out)[NS], bool* z) {
+  double v[FS];
+#pragma unroll
+  for (int s = 0; s < FS; ++s) v[s] = sigma_seg(tabf.t[s].shift[o] * lam, tabf.t[s], sg[s]);
+  if constexpr (NS == 1 && FS > 1) {
+    double Y = 0.0;
+    bool zz = false;
+#pragma unroll
+    for (int s = 0; s < FS; ++s) {
+      const double cv = tabf.t[s].chi * v[s];
+      zz = zz || !(cv > 0.0);
+      Y += cv;
+    }
+    out[0] = Y;
+    *z = zz;
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) out[s] = v[s];
+    *z = false;
+  }
+}
+
 // sigma_of for NS tables at once (the species of one wavelength): every table's directory load goes
 // out first, then every table's 4-node window (x and f, 64 B per target: the resampling kernel is bound
 // by the vector L1's bytes, so numpy.interp's slope is divided here rather than fetched), so a thread

@@ -264,6 +264,7 @@ struct TransitDev {
   // upper bounds of the normalised Q = sum_s sigma_s / c_s over every wavelength and phase (per species /
   // merged): k_order's always-tail threshold btail = tail epsilon / Q bound
   double qbound_v = 0.0, qbound_m = 0.0;
+  int taup_resident_f = 0;                  // resident workgroups of the fused planned tau kernel
   int32_t taup_resident = 0;                // k_tau_p wavefronts resident at once (set at the first run)
   // timed runs: k_tau_p stamps each workgroup's first and last device-clock tick into ts_out[2 b],
   // ts_out[2 b + 1] when it has at most ts_cap workgroups; ts_blocks reports the count (0: no stamps)
@@ -345,6 +346,9 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                        int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
                        int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start);
+// fused Doppler path: half-tile Q bounds from the table nodes instead of the sigma rows (prom_sigma.hip)
+void launch_qbounds(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav, int32_t n_rows,
+                    const SigSeg* seg, float4* tq, int32_t merge_sp, double nscale_m);
 // the fused tau kernels of the molecular and stellar-spectrum paths (prom_mol.hip, prom_rm.hip)
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev);

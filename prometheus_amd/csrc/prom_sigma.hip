@@ -67,37 +67,6 @@ __device__ __forceinline__ void sigma_row_out(int32_t orow, int32_t nse, const d
   if (lane == 0 && hw < n_halves) reinterpret_cast<float2*>(tq)[(int64_t)orow * n_halves + hw] = q_range(ql, qh);
 }
 
-// numpy.interp of one target from its bracket guess g (within one node of the bracket, SigSeg): x_g and
-// x_{g+1} decide between g - 1, g and g + 1, then the bracket's record {x, f, slope} gives the value --
-// two dependent reads, no branches on the common path.  X2(g) reads x_g and x_{g+1}, REC(k, ...) node k's
-// x, f and slope.
-template <class XF, class RF>
-__device__ __forceinline__ double interp_guess(double t, int32_t g, XF X2, RF REC) {
-  const double2 xg = X2(g);   // x_g, x_{g+1}
-  const int32_t k = t < xg.x ? g - 1 : (t >= xg.y ? g + 1 : g);
-  double xa, fa, sl;
-  REC(k, xa, fa, sl);
-  // numpy: an exact node hit returns f; with a finite slope sl (t - x) + f is that f already, so the
-  // test is only needed where the interpolation is NaN (non-finite slope), as is numpy's right-node retry
-  double rv = sl * (t - xa) + fa;
-  if (rv != rv) {
-    if (xa == t) rv = fa;
-    else {
-      double xb, fb, sb;
-      REC(k + 1, xb, fb, sb);
-      rv = sl * (t - xb) + fb;
-      if (rv != rv && fa == fb) rv = fa;
-    }
-  }
-  return rv;
-}
-
-__device__ __forceinline__ int32_t seg_guess(double t, double xs, double inv, int32_t m) {
-  // = (f < 0 ? 0 : f >= m - 2 ? m - 2 : (int)f), the host's verified map (NaN t never reaches here)
-  const double f = (t - xs) * inv;
-  return (int32_t)__builtin_fmin(__builtin_fmax(f, 0.0), (double)(m - 2));
-}
-
 // Workgroups [0, n_blk * n_rc): one per (256-wavelength block whose slices all fit in LDS, chunk of
 // kSigRowChunk rows).  Per species the block's node records go to LDS; a target's bracket comes from the
 // slice's verified linear guess (interp_guess), so the rows' lookups are independent and their LDS round
@@ -111,7 +80,7 @@ __device__ __forceinline__ int32_t seg_guess(double t, double xs, double inv, in
 template <int NSIG>
 __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
                                                  int32_t n_rows, const SigSeg* __restrict__ seg,
-                                                 const int32_t* __restrict__ fb, int32_t n_blk, int32_t n_rc,
+                                                 const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk, int32_t n_rc,
                                                  double* __restrict__ sig, float4* __restrict__ tq, int32_t merge_sp,
                                                  double nscale_m, uint8_t* __restrict__ zfl) {
   // the slice as three conflict-free arrays: x (bracket tests), (x, f) pairs and slopes (the value)
@@ -124,10 +93,15 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
   const int32_t nse = merge_sp ? 1 : NSIG;
   const int64_t n_main = (int64_t)((n_blk + 7) / 8) * 8 * n_rc;
   if ((int64_t)blockIdx.x >= n_main) {
+    // XCD-aware order as below: the row chunks of an oversize block are 8 workgroups apart, so its (large)
+    // slice is fetched into one XCD's L2 rather than all eight
     const int64_t item = (int64_t)blockIdx.x - n_main;
     const int32_t n_fc = (n_rows + kSigFbRows - 1) / kSigFbRows;
-    const int32_t f0 = (int32_t)(item % n_fc) * kSigFbRows;
-    const int64_t wb = fb[item / n_fc];
+    const int64_t fgrp = item / (8 * n_fc), frem = item % (8 * n_fc);
+    const int64_t fi = fgrp * 8 + frem % 8;
+    if (fi >= n_fb) return;
+    const int32_t f0 = (int32_t)(frem / 8) * kSigFbRows;
+    const int64_t wb = fb[fi];
     const int64_t w = wb * kBlock + tid;
     const bool live = w < n_wav;
     const double lam = wav[live ? w : n_wav - 1];
@@ -237,16 +211,104 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
 }
 
 
+// ---- half-tile Q bounds for the fused path (no sigma rows in HBM) -------------------------------------
+// k_order / k_windows pick each tile's tau window from a Q range that must enclose Q at every wavelength of
+// the half tile.  Without the sigma rows it is bounded from the table nodes the half tile's targets can
+// interpolate between: numpy.interp's value lies between its bracket nodes' values, so log10 sigma_s is
+// within [min, max] of f over the nodes bracketing the first to the last target (verified guess +- 1
+// node), and 10^f - offset is monotone (widened by 2^-50 against the last-ulp behaviour of exp10).  Blocks
+// without a verified guess take their whole slice's range; targets outside the table or non-finite give
+// the "bad" range (-1, 0): window = every record.  One thread per (row, half tile).
+__device__ __forceinline__ void node_range(const double* __restrict__ y, int64_t a, int64_t b, double* lo, double* hi) {
+  double mn = y[a], mx = y[a];
+  for (int64_t i = a + 1; i <= b; ++i) {
+    const double v = y[i];
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+  *lo = mn;
+  *hi = mx;
+}
+
+template <int NSIG>
+__global__ void __launch_bounds__(kBlock) k_qbounds(const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
+                                                  int32_t n_rows, const SigSeg* __restrict__ seg, float4* __restrict__ tq,
+                                                  int32_t merge_sp, double nscale_m) {
+  const int64_t n_halves = 2 * ((n_wav + kTW - 1) / kTW);
+  const int64_t item = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  if (item >= (int64_t)n_rows * n_halves) return;
+  const int32_t orow = (int32_t)(item / n_halves);
+  const int64_t hw = item - (int64_t)orow * n_halves;
+  const int64_t w0 = hw * 64, w1 = (w0 + 63 < n_wav ? w0 + 63 : n_wav - 1);
+  const int64_t wb = w0 / kBlock;   // the 256-wavelength block (segments) of this half tile
+  bool bad = !(w0 < n_wav);
+  double qlo = 0.0, qhi = 0.0, ylo = 0.0, yhi = 0.0;
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) {
+    const SigTabDev& tb = tabv.t[s];
+    const SigSeg sg = seg[wb * NSIG + s];
+    double flo, fhi;
+    if (sg.m <= 0) { bad = true; continue; }
+    const double ta = tb.shift[orow] * wav[w0 < n_wav ? w0 : n_wav - 1], tz = tb.shift[orow] * wav[w1];
+    if (sg.kind > 0) {
+      // first / last target's bracket within one node of the guess: the range [g_a - 1, g_z + 2] holds both
+      // brackets' nodes
+      const int32_t ga = seg_guess(ta, sg.xs, sg.inv, sg.m), gz = seg_guess(tz, sg.xs, sg.inv, sg.m);
+      const int64_t a = (int64_t)sg.lo + (ga > 0 ? ga - 1 : 0);
+      const int64_t b = (int64_t)sg.lo + (gz + 2 < sg.m ? gz + 2 : sg.m - 1);
+      node_range(tb.y, a, b, &flo, &fhi);
+    } else {
+      node_range(tb.y, sg.lo, (int64_t)sg.lo + sg.m - 1, &flo, &fhi);
+    }
+    const double slo = (exp10(flo) - tb.offset) * (1.0 - 0x1p-50), shi = (exp10(fhi) - tb.offset) * (1.0 + 0x1p-50);
+    if (merge_sp) {
+      ylo += tb.chi * slo;
+      yhi += tb.chi * shi;
+    } else {
+      const double a = slo * tb.nscale, b = shi * tb.nscale;
+      qlo += a > 0.0 ? a : 0.0;
+      qhi += b > 0.0 ? b : 0.0;
+    }
+  }
+  if (merge_sp) {
+    const double a = ylo * nscale_m, b = yhi * nscale_m;
+    qlo = a > 0.0 ? a : 0.0;
+    qhi = b > 0.0 ? b : 0.0;
+  }
+  // sums of NSIG terms: relative rounding below 2^-45
+  qlo *= 1.0 - 0x1p-45;
+  qhi *= 1.0 + 0x1p-45;
+  bad = bad || !(qhi <= 1.0e100) || !(qlo == qlo);
+  reinterpret_cast<float2*>(tq)[(int64_t)orow * n_halves + hw] =
+      bad ? make_float2(-1.0f, 0.0f) : q_range((float)qlo, (float)qhi);
+}
+
+void launch_qbounds(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav, int32_t n_rows,
+                    const SigSeg* seg, float4* tq, int32_t merge_sp, double nscale_m) {
+  const int64_t n_halves = 2 * ((n_wav + kTW - 1) / kTW);
+  const unsigned nb = grid_for((int64_t)n_rows * n_halves);
+#define PROM_QB(NS) \
+  hipLaunchKernelGGL((k_qbounds<NS>), dim3(nb), dim3(kBlock), 0, s, tabv, wav, n_wav, n_rows, seg, tq, merge_sp, nscale_m)
+  switch (nsig) {
+    case 1: PROM_QB(1); break;
+    case 2: PROM_QB(2); break;
+    case 3: PROM_QB(3); break;
+    default: PROM_QB(4); break;
+  }
+#undef PROM_QB
+  PROM_HIP(hipGetLastError());
+}
+
 void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                        int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
                        int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start) {
   const int32_t n_blk = (int32_t)grid_for(n_wav);
   const int32_t n_rc = (n_rows + kSigRowChunk - 1) / kSigRowChunk;
   const int32_t n_fc = (n_rows + kSigFbRows - 1) / kSigFbRows;
-  const unsigned nb = (unsigned)((int64_t)((n_blk + 7) / 8) * 8 * n_rc + (int64_t)n_fb * n_fc);
+  const unsigned nb = (unsigned)((int64_t)((n_blk + 7) / 8) * 8 * n_rc + (int64_t)((n_fb + 7) / 8) * 8 * n_fc);
 #define PROM_SIGR(NS)                                                                                        \
   hipExtLaunchKernelGGL((k_sigma_rows<NS>), dim3(nb), dim3(kBlock), 0, s, ev_start, nullptr, 0, tabv, wav, n_wav, \
-                        n_rows, seg, fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl)
+                        n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl)
   switch (nsig) {
     case 1: PROM_SIGR(1); break;
     case 2: PROM_SIGR(2); break;

@@ -1665,18 +1665,26 @@ __device__ __forceinline__ void tau_count(unsigned long long* __restrict__ evals
 
 // One heavy entry {half tile, h, t, flags | phase << 8}: this lane's wavelength, its cross-sections (row of
 // the entry's phase when PH), the record source, the first chunk `first` preloaded into nx.
-template <int NS, bool PH>
+template <int NS, bool PH, int FS>
 __device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const double* __restrict__ sig,
                                             const double* __restrict__ recs, const double* __restrict__ mrecs,
                                             int32_t n_pr, int64_t n_wav, int lane, int64_t* w, bool* live,
-                                            double (&sg)[1][NS], const double** src, double (&nx)[1 + NS]) {
+                                            double (&sg)[1][NS], const double** src, double (&nx)[1 + NS],
+                                            const SigTabs4& tabf, const SigSeg* __restrict__ fseg,
+                                            const double* __restrict__ wav) {
   constexpr int ST = 1 + NS;
   const int32_t o = en.w >> 8;
   *w = (int64_t)en.x * 64 + lane;
   *live = *w < n_wav;
-  const double* so = sig + (PH ? (int64_t)o * NS * n_wav : 0);
+  if constexpr (FS > 0) {
+    const int64_t wc = *live ? *w : n_wav - 1;
+    bool z;
+    fused_sigma<FS, NS>(tabf, fseg + ((int64_t)en.x * 64 / kBlock) * FS, o, wav[wc], sg[0], &z);
+  } else {
+    const double* so = sig + (PH ? (int64_t)o * NS * n_wav : 0);
 #pragma unroll
-  for (int s = 0; s < NS; ++s) sg[0][s] = so[(int64_t)s * n_wav + (*live ? *w : n_wav - 1)];
+    for (int s = 0; s < NS; ++s) sg[0][s] = so[(int64_t)s * n_wav + (*live ? *w : n_wav - 1)];
+  }
   *src = (((en.w & 1) ? mrecs : recs)) + ((int64_t)o * n_pr + en.y) * ST;
   const int32_t nel = (en.z - en.y) * ST;
 #pragma unroll
@@ -1690,7 +1698,7 @@ __device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const 
 // blockIdx.x * 4 + wid < n_static): tile sw % n_tiles, phases 4 (sw / n_tiles) ...; round trip 1 = its
 // phases' tile records {h, t, flags, tail moments} (k_order), sigma at its 128 wavelengths (2 per lane), the
 // exp table; a second round trip only for the packed records of non-empty light windows.
-template <int NS, bool PH>
+template <int NS, bool PH, int FS>
 __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs4 tabv, const double* __restrict__ sig,
                                                                    const double* __restrict__ recs,
                                                                    const double* __restrict__ mrecs,
@@ -1707,7 +1715,11 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
                                                                    int32_t n_static, const uint8_t* __restrict__ zfl,
                                                                    unsigned long long* __restrict__ evals,
                                                                    unsigned long long* __restrict__ tstamp,
-                                                                   double* __restrict__ R) {
+                                                                   double* __restrict__ R, const SigTabs4 tabf,
+                                                                   const SigSeg* __restrict__ fseg,
+                                                                   const double* __restrict__ wav) {
+  // FS > 0 (fused Doppler path): the cross sections of the FS table species are looked up here
+  // (fused_sigma) instead of read from sigma rows; merged absorbers also get their zero flags here
   constexpr int K = Monos<NS>::K;
   constexpr int ST = 1 + NS;
   constexpr int PQ = (4 * kHeavy * ST + 63) / 64;   // packed record loads per lane
@@ -1740,15 +1752,36 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
   const int4 tv = lane < np ? trec[(int64_t)(o0 + lane) * n_tiles + tile] : make_int4(0, 0, 0, 0);
   bool live[2];
   double sg[SR][2][NS];
+  bool zb[SR][2];
+  if constexpr (FS > 0) {
+    const SigSeg* fs_tile = fseg + ((int64_t)tile * kTW / kBlock) * FS;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
-    live[j] = w < n_wav;
+    for (int j = 0; j < 2; ++j) {
+      const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
+      live[j] = w < n_wav;
+      const double lam = wav[live[j] ? w : n_wav - 1];
 #pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      const double* so = sig + (PH ? (int64_t)(o0 + r) * NS * n_wav : 0);
+      for (int r = 0; r < SR; ++r) {
+        if (r < np) fused_sigma<FS, NS>(tabf, fs_tile, o0 + r, lam, sg[r][j], &zb[r][j]);
+        else {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) sg[r][j][s] = r < np ? so[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)] : 0.0;
+          for (int s = 0; s < NS; ++s) sg[r][j][s] = 0.0;
+          zb[r][j] = false;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
+      live[j] = w < n_wav;
+#pragma unroll
+      for (int r = 0; r < SR; ++r) {
+        const double* so = sig + (PH ? (int64_t)(o0 + r) * NS * n_wav : 0);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) sg[r][j][s] = r < np ? so[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)] : 0.0;
+        zb[r][j] = false;
+      }
     }
   }
   double tfv[4];
@@ -1768,8 +1801,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
     bool lv;
     double sgh[1][NS], nx[ST];
     const double* src;
-    heavy_setup<NS, PH>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), wid, sig, recs, mrecs, n_pr,
-                        n_wav, lane, &w, &lv, sgh, &src, nx);
+    heavy_setup<NS, PH, FS>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), wid, sig, recs, mrecs, n_pr,
+                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav);
     double mm[K];
     if (wid == 0 && (f4 & 2)) {
       const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;   // t <= G <= n_pr: the row exists
@@ -1813,8 +1846,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
     bool lv;
     double sgh[1][NS], nx[ST];
     const double* src;
-    heavy_setup<NS, PH>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), 0, sig, recs, mrecs, n_pr,
-                        n_wav, lane, &w, &lv, sgh, &src, nx);
+    heavy_setup<NS, PH, FS>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), 0, sig, recs, mrecs, n_pr,
+                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav);
     const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
     double mm[K];
 #pragma unroll
@@ -1936,8 +1969,11 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
             double tau = rr[1] * sg[r][j][0];
 #pragma unroll
             for (int s = 1; s < NS; ++s) tau = tau + rr[1 + s] * sg[r][j][s];
-            if (NS == 1 && zo)
+            if constexpr (FS > 1 && NS == 1) {
+              if (!__builtin_isfinite(rr[1]) && zb[r][j]) tau = __builtin_nan("");
+            } else if (NS == 1 && zo) {
               tau = exact_tau_merged(rr[1], sg[r][j][0], zo, live[j] ? (int64_t)tile * kTW + 64 * j + lane : n_wav - 1);
+            }
             acc[j] = acc[j] + F * exp(-tau);
           }
         }
@@ -1978,6 +2014,13 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // species merging (TransitDev::species_merge_ok) on the resampled fast path: downstream of the
   // column kernel there is one effective absorber
   const bool msp = pre_sigma && tr.species_merge_ok;
+  // fused Doppler path (opt-in, PROM_FUSED=1): no sigma rows in HBM; the planned tau kernel looks the cross
+  // sections up itself (per-lane gathers from the global tables) and k_order / k_windows take node-range Q
+  // bounds (k_qbounds).  Correct (test_fused_sigma) but slower on C3: 122 us for the fused tau kernel and
+  // 1 ms for the bounds' node scans against 48 + 28 us for k_sigma_rows + k_tau_p (DESIGN.md "Tried").
+  const char* fenv = std::getenv("PROM_FUSED");
+  const bool fused = pre_sigma && sig_rows > 1 && tr.sig_seg_ok && tr.plan && tr.n_atoms <= 4 &&
+                     fenv && std::atoi(fenv) != 0;
   const int32_t nsig = tr.n_atoms;                 // species the column kernel resamples
   const int32_t na = msp ? 1 : tr.n_atoms;         // species the ordering and tau kernels see
   const ColArgs& cargs = msp ? tr.colargs_m : tr.colargs;
@@ -2003,23 +2046,31 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
     // orbital Doppler shift with sigma segments: the rows come from their own kernel (k_sigma_rows)
     const bool rows_seg = pre_sigma && sig_rows > 1 && tr.sig_seg_ok;
-    const bool sig_fork = rows_seg && rs.aux && rs.ev_fork && rs.ev_join;
+    const bool sig_fork = rows_seg && !fused && rs.aux && rs.ev_fork && rs.ev_join;
     const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
     const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
-    if (rows_seg) {
-      // the sigma rows do not depend on the columns or the ordering: with a second stream for the slot they
-      // run beside k_columns8 / k_order (VALU-bound full chip beside latency-bound per-phase workgroups) and
-      // join before the tile windows
-      if (sig_fork) {
-        PROM_HIP(hipEventRecord(rs.ev_fork, s));
-        PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
-      }
+    // the sigma rows do not depend on the columns or the ordering: with a second stream for the slot they
+    // run beside k_columns8 / k_order (VALU-bound full chip beside latency-bound per-phase workgroups) and
+    // join before the tile windows.  The fork point is taken before the column kernel is queued (the rows
+    // wait only for the slot's previous run); PROM_SIGMA_FIRST=1 queues them before the column kernel.
+    const bool sig_first = !sig_fork || (std::getenv("PROM_SIGMA_FIRST") && std::atoi(std::getenv("PROM_SIGMA_FIRST")));
+    if (sig_fork) {
+      PROM_HIP(hipEventRecord(rs.ev_fork, s));
+      PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
+    }
+    auto sigma_rows = [&]() {
       launch_sigma_rows(sig_fork ? rs.aux : s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
                         tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(),
                         rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(),
                         sig_fork ? nullptr : ev0);
       if (sig_fork) PROM_HIP(hipEventRecord(rs.ev_join, rs.aux));
       else ev0 = nullptr;
+    };
+    if (fused) {
+      launch_qbounds(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
+                     rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale);
+    } else if (rows_seg && sig_first) {
+      sigma_rows();
     }
 #define PROM_COLS(SV, NSV)                                                                               \
   hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
@@ -2045,6 +2096,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #undef PROM_COLS_L
 #undef PROM_COLS
     PROM_HIP(hipGetLastError());
+    if (rows_seg && !fused && !sig_first) sigma_rows();
   } else {
     if (ev0) PROM_HIP(hipEventRecord(ev0, s));
     for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
@@ -2111,7 +2163,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #undef PROM_CHW
     if (pre_sigma) {
       // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
-      if (sig_rows > 1 && tr.sig_seg_ok && rs.aux && rs.ev_join) PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
+      if (sig_rows > 1 && tr.sig_seg_ok && !fused && rs.aux && rs.ev_join) PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
       const dim3 gw((unsigned)((n_wtiles + kBlock - 1) / kBlock), (unsigned)tr.n_orb);
 #define PROM_WIN(NSV)                                                                                    \
   hipExtLaunchKernelGGL(k_windows<NSV>, gw, dim3(kBlock), 0, s, nullptr, ev_ord, 0, rs.tq.as<float4>(),      \
@@ -2191,41 +2243,63 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       // planned: big and small heavy entries from k_order's lists over the whole grid, then one static
       // wavefront per (tile, 4 phases)
       const bool ph = sig_rows > 1;
-      if (tr.taup_resident == 0) {
+      const int fsv = fused ? nsig : 0;   // table species the tau kernel looks up (0: reads sigma rows)
+      int& resident = fused ? tr.taup_resident_f : tr.taup_resident;
+      if (resident == 0) {
         int cus = 0, nb = 0;
         int dev = 0;
         PROM_HIP(hipGetDevice(&dev));
         PROM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-#define PROM_OCC(NSV)                                                                                        \
-  (ph ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, true>, kBlock, 0)                     \
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, false>, kBlock, 0))
-        switch (na) {
-          case 1: PROM_HIP(PROM_OCC(1)); break;
-          case 2: PROM_HIP(PROM_OCC(2)); break;
-          case 3: PROM_HIP(PROM_OCC(3)); break;
-          default: PROM_HIP(PROM_OCC(4)); break;
+#define PROM_OCC(NSV, PHV, FSV) PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, PHV, FSV>, kBlock, 0))
+        if (fused) {
+          if (na == 1) {
+            switch (fsv) { case 1: PROM_OCC(1, true, 1); break; case 2: PROM_OCC(1, true, 2); break;
+                           case 3: PROM_OCC(1, true, 3); break; default: PROM_OCC(1, true, 4); break; }
+          } else {
+            switch (na) { case 2: PROM_OCC(2, true, 2); break; case 3: PROM_OCC(3, true, 3); break;
+                          default: PROM_OCC(4, true, 4); break; }
+          }
+        } else {
+          switch (na) {
+            case 1: if (ph) { PROM_OCC(1, true, 0); } else { PROM_OCC(1, false, 0); } break;
+            case 2: if (ph) { PROM_OCC(2, true, 0); } else { PROM_OCC(2, false, 0); } break;
+            case 3: if (ph) { PROM_OCC(3, true, 0); } else { PROM_OCC(3, false, 0); } break;
+            default: if (ph) { PROM_OCC(4, true, 0); } else { PROM_OCC(4, false, 0); } break;
+          }
         }
 #undef PROM_OCC
-        tr.taup_resident = std::max(1, cus) * std::max(1, nb);   // workgroups resident at once
+        resident = std::max(1, cus) * std::max(1, nb);   // workgroups resident at once
       }
       const int64_t n_static = (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
-      const int64_t blocks = std::max<int64_t>((n_static + kTP - 1) / kTP, tr.taup_resident);
+      const int64_t blocks = std::max<int64_t>((n_static + kTP - 1) / kTP, resident);
       *variant = 30 + (na <= 4 ? na : 0);
       unsigned long long* tsp = (tr.ts_out && blocks <= tr.ts_cap) ? tr.ts_out : nullptr;
       tr.ts_blocks = tsp ? (int32_t)blocks : 0;
-#define PROM_TAUP(NSV, PHV)                                                                             \
-  hipExtLaunchKernelGGL((k_tau_p<NSV, PHV>), dim3((unsigned)blocks), dim3(kBlock), 0, s,                \
+#define PROM_TAUP(NSV, PHV, FSV)                                                                        \
+  hipExtLaunchKernelGGL((k_tau_p<NSV, PHV, FSV>), dim3((unsigned)blocks), dim3(kBlock), 0, s,           \
                         ev_tau0, ev ? ev[3] : nullptr, 0, tabs4, rs.sig.as<double>(),                     \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
                         rs.wmom.as<double>(), rs.trec.as<int4>(), n_wtiles, rs.hlist.as<int4>(),        \
                         hcap, rs.hcnt.as<int32_t>(), (int32_t)n_static,                                 \
-                        msp ? rs.zfl.as<uint8_t>() : nullptr,                                            \
-                        tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tsp, R)
-      switch (na) {
-        case 1: if (ph) { PROM_TAUP(1, true); } else { PROM_TAUP(1, false); } break;
-        case 2: if (ph) { PROM_TAUP(2, true); } else { PROM_TAUP(2, false); } break;
-        case 3: if (ph) { PROM_TAUP(3, true); } else { PROM_TAUP(3, false); } break;
-        default: if (ph) { PROM_TAUP(4, true); } else { PROM_TAUP(4, false); } break;
+                        (msp && !fused) ? rs.zfl.as<uint8_t>() : nullptr,                                \
+                        tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tsp, R,           \
+                        tr.sigtab_v, tr.sig_seg.as<prom::SigSeg>(), tr.wav.as<double>())
+      if (fused) {
+        if (na == 1) {
+          switch (fsv) { case 1: PROM_TAUP(1, true, 1); break; case 2: PROM_TAUP(1, true, 2); break;
+                         case 3: PROM_TAUP(1, true, 3); break; default: PROM_TAUP(1, true, 4); break; }
+        } else {
+          switch (na) { case 2: PROM_TAUP(2, true, 2); break; case 3: PROM_TAUP(3, true, 3); break;
+                        default: PROM_TAUP(4, true, 4); break; }
+        }
+        *variant = 50 + (na <= 4 ? na : 0);
+      } else {
+        switch (na) {
+          case 1: if (ph) { PROM_TAUP(1, true, 0); } else { PROM_TAUP(1, false, 0); } break;
+          case 2: if (ph) { PROM_TAUP(2, true, 0); } else { PROM_TAUP(2, false, 0); } break;
+          case 3: if (ph) { PROM_TAUP(3, true, 0); } else { PROM_TAUP(3, false, 0); } break;
+          default: if (ph) { PROM_TAUP(4, true, 0); } else { PROM_TAUP(4, false, 0); } break;
+        }
       }
 #undef PROM_TAUP
     } else if (pre_sigma) { PROM_TAUW_NS(8, true) } else { PROM_TAUW_NS(2, false) }

@@ -342,6 +342,7 @@ def test_planned_tau_bitwise(dev, name, monkeypatch):
     else:
         cfg = json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
+    monkeypatch.setenv("PROM_FUSED", "0")   # both read the same sigma rows (test_fused_sigma: the fused path)
     monkeypatch.setenv("PROM_TAU_PLAN", "1")
     R_p = tr.sumOverChords(devices=[0])
     st_p = tr.last_stats[-1]
@@ -353,6 +354,28 @@ def test_planned_tau_bitwise(dev, name, monkeypatch):
     bound = 2 * (2.0 ** -40 / 24 + np.exp(-40.0)) + 1e-14
     assert np.max(np.abs(R_p - R_w)) <= bound
     assert st_p["exp_evals"] <= st_w["exp_evals"]
+
+
+@pytest.mark.parametrize("name", ["C3r", "C4r", "exomoon", "C3"])
+def test_fused_sigma(dev, name, monkeypatch):
+    """The fused Doppler path (PROM_FUSED, default: the planned tau kernel looks sigma up itself, windows from
+    node-range Q bounds, no sigma rows in HBM) against the sigma-row path: both within the windowed
+    integration's bound of the full evaluation, so within 1e-13 of each other; and the reference's R."""
+    from prometheus_amd import configs
+    cfg = configs.get(name) if name == "C3" else json.loads(str(load("transit_" + name)["config"]))
+    tr = _product_transit(cfg)
+    monkeypatch.setenv("PROM_FUSED", "1")
+    R_f = tr.sumOverChords(devices=[0])
+    st_f = tr.last_stats[-1]
+    monkeypatch.setenv("PROM_FUSED", "0")
+    R_r = tr.sumOverChords(devices=[0])
+    st_r = tr.last_stats[-1]
+    print(name, "variants", st_f["tau_kernel_variant"], st_r["tau_kernel_variant"], "exp evals", st_f["exp_evals"],
+          st_r["exp_evals"])
+    assert st_f["tau_kernel_variant"] // 10 == 5 and st_r["tau_kernel_variant"] // 10 == 3
+    assert np.max(np.abs(R_f - R_r)) <= 1e-13
+    if name != "C3":
+        assert rel(R_f, load("transit_" + name)["R"]) < R_TOL
 
 
 @pytest.mark.parametrize("name", ["C2r", "C2"])
@@ -377,7 +400,7 @@ def test_species_merge(dev, name, monkeypatch):
         assert rel(R_m, load("transit_" + name)["R"]) < R_TOL
 
 
-@pytest.mark.parametrize("plan", ["1", "0"])
+@pytest.mark.parametrize("plan", ["1", "0", "doppler"])
 def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     """A user density plugin (host-tabulated n(c, x)) with one infinite sample: that chord's column is
     inf, its phase takes the exact chord-order path (ocml exp, no windows), e^{-inf sigma} = 0 and
@@ -385,9 +408,12 @@ def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     Both the planned (k_tau_p) and the k_tau_w fast path."""
     import copy
     from prometheus_amd import configs
-    monkeypatch.setenv("PROM_TAU_PLAN", plan)
+    # "doppler": orbital Doppler shift on, so the merged Na + K absorber takes the fused path (the tau kernel
+    # looks sigma and the zero flags up itself)
+    monkeypatch.setenv("PROM_TAU_PLAN", "1" if plan == "doppler" else plan)
     cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
                           res_low=5e-9, res_high=1e-10)
+    cfg["Fundamentals"]["DopplerOrbitalMotion"] = plan == "doppler"
     tr = _product_transit(cfg)
     scen, dop, grids = O.from_setup(cfg)
     base = scen[0]
@@ -461,6 +487,7 @@ def test_sigma_rows_bitwise(dev, name, merge, monkeypatch):
     cfg = configs.get(name) if name in ("C3", "C4") else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
     monkeypatch.setenv("PROM_SPECIES_MERGE", merge)
+    monkeypatch.setenv("PROM_FUSED", "0")   # the sigma-row kernel itself (the fused path: test_fused_sigma)
     monkeypatch.setenv("PROM_SIGMA_ROWS", "1")
     R_a = tr.sumOverChords(devices=[0])
     monkeypatch.setenv("PROM_SIGMA_ROWS", "0")
