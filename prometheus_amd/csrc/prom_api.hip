@@ -906,11 +906,13 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     const int si = (tr.last + 1) % tr.depth;
     const hipStream_t st = ctx->streams[si];
     prom::RunSlot& rs = tr.slot[si];
-    // the slot's second stream: the one kMaxSlots / 2 away (free when depth <= kMaxSlots / 2); PROM_SIGMA_FORK=0
-    // keeps every kernel of a run on one stream
+    // the slot's second stream: the one `depth` away (free when depth <= kMaxSlots / 2).  The fork shortens
+    // one run (sigma rows beside k_columns8 / k_order) but costs pipelined throughput (C4 7.3e10 -> 3.8e10
+    // pts/s, C3 unchanged: profiles/r02w_pipeline_sweep.txt), so it is the default for unpipelined
+    // problems only; PROM_SIGMA_FORK=0/1 forces it off/on
     const char* fk = std::getenv("PROM_SIGMA_FORK");
-    const bool fork_ok = tr.depth <= prom::kMaxSlots / 2 && !(fk && std::atoi(fk) == 0);
-    rs.aux = fork_ok ? ctx->streams[si + prom::kMaxSlots / 2] : nullptr;
+    const bool fork_ok = tr.depth <= prom::kMaxSlots / 2 && (fk ? std::atoi(fk) != 0 : tr.depth == 1);
+    rs.aux = fork_ok ? ctx->streams[si + tr.depth] : nullptr;
     rs.ev_fork = fork_ok ? ctx->fork_ev[si] : nullptr;
     rs.ev_join = fork_ok ? ctx->join_ev[si] : nullptr;
     if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
