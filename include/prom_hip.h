@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PROM_ABI_VERSION 3
+#define PROM_ABI_VERSION 4
 
 typedef struct prom_ctx prom_ctx;
 
@@ -222,8 +222,18 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* problem);
  * work-buffer slots, so one run's column / ordering kernels overlap earlier runs' tau kernels;
  * prom_transit_result, prom_synchronize and prom_transit_set wait for all of them. */
 int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats);
-/* Copy R[n_orb][n_wav] (row-major) of the last run to a host buffer. */
+/* Copy R[n_orb][n_wav] (row-major) of the last run to a host buffer.  A buffer from prom_host_alloc
+ * takes one DMA at the link rate; any other buffer is filled through the context's pinned staging. */
 int32_t prom_transit_result(prom_ctx* ctx, double* R_out);
+
+/* Page-locked host memory for results (ABI 4).  Process-wide pool, independent of contexts: a freed
+ * buffer is kept for the next request of a similar size (size <= capacity <= 2 size), so a caller that
+ * takes a fresh output array per call pays neither hipHostMalloc nor page faults.  Pinned bytes (in use +
+ * cached) are capped at PROM_PINNED_CAP_MB (default 4096): past the cap PROM_E_NOMEM, and the caller falls
+ * back to ordinary memory.  Replaces the reference's np.zeros result arrays (gasProperties.py:1165-1166). */
+int32_t prom_host_alloc(int64_t bytes, void** out);
+/* Return a prom_host_alloc buffer to the pool (PROM_E_ARG for any other pointer). */
+int32_t prom_host_free(void* p);
 /* Column densities N[s][o][ip] of the last run (atomic constituents in scenario order); testing aid. */
 int32_t prom_transit_columns(prom_ctx* ctx, double* N_out);
 

@@ -63,7 +63,7 @@ class TransitProblem(C.Structure):
                 ("chord_rho", _dp), ("chord_clv", _dp), ("chord_star_shift", _dp)]
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
 OPT_NO_WINDOW = 4
@@ -113,6 +113,8 @@ SIGNATURES = {
     "prom_timing_begin": (C.c_int32, [C.c_void_p]),
     "prom_timing_end": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _ip]),
     "prom_timing_stride": (C.c_int32, [C.c_void_p, C.c_int32]),
+    "prom_host_alloc": (C.c_int32, [C.c_int64, C.POINTER(C.c_void_p)]),
+    "prom_host_free": (C.c_int32, [C.c_void_p]),
 }
 
 _lib = None
@@ -149,6 +151,31 @@ def device_count() -> int:
     n = C.c_int32(0)
     lib.prom_device_count(C.byref(n))
     return int(n.value)
+
+
+class _PinnedBuffer:
+    """A prom_host_alloc buffer exposed to numpy; returned to the pool when the last array over it dies."""
+
+    def __init__(self, lib, ptr: int, shape):
+        self._lib, self._ptr = lib, ptr
+        self.__array_interface__ = {"shape": tuple(shape), "typestr": "<f8", "data": (ptr, False), "version": 3}
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self._lib.prom_host_free(C.c_void_p(self._ptr))
+        except Exception:
+            pass
+
+
+def host_array(shape) -> Optional[np.ndarray]:
+    """A float64 array of ``shape`` in page-locked memory from the library's pool (prom_host_alloc), or None
+    when the pool's cap (PROM_PINNED_CAP_MB) is reached.  Device results copy into it with one DMA."""
+    lib = load_library()
+    n = int(np.prod(shape, dtype=np.int64)) * 8
+    p = C.c_void_p()
+    if lib.prom_host_alloc(n, C.byref(p)) != PROM_OK or not p.value:
+        return None
+    return np.asarray(_PinnedBuffer(lib, p.value, shape))
 
 
 def _d(a: np.ndarray):

@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstring>
 #include <exception>
+#include <map>
+#include <mutex>
 #include <thread>
 
 #include "prom_internal.h"
@@ -81,9 +83,85 @@ bool table_ok(const std::vector<T>& v, int32_t id) {
   return id >= 0 && id < (int32_t)v.size() && v[id].live;
 }
 
+// Pinned host pool behind prom_host_alloc / prom_host_free: buffers keyed by address, each either in use
+// or cached for reuse; the total (in use + cached) stays under the cap, idle buffers are released first
+struct PinnedPool {
+  struct Buf {
+    size_t cap;
+    bool used;
+  };
+  std::mutex mu;
+  std::map<char*, Buf> bufs;
+  size_t total = 0;
+  size_t cap_bytes() const {
+    const char* e = std::getenv("PROM_PINNED_CAP_MB");
+    const long long mb = e ? std::atoll(e) : 4096;
+    return (size_t)std::max(0LL, mb) << 20;
+  }
+  // in-use buffer holding [p, p + n)
+  bool holds(const void* p, size_t n) {
+    std::lock_guard<std::mutex> g(mu);
+    const char* c = static_cast<const char*>(p);
+    auto it = bufs.upper_bound(const_cast<char*>(c));
+    if (it == bufs.begin()) return false;
+    --it;
+    return it->second.used && c >= it->first && c + n <= it->first + it->second.cap;
+  }
+};
+
+PinnedPool& pinned_pool() {
+  static PinnedPool* pool = new PinnedPool();   // never destroyed: buffers may outlive static teardown
+  return *pool;
+}
+
 }  // namespace
 
 extern "C" {
+
+int32_t prom_host_alloc(int64_t bytes, void** out) {
+  if (!out || bytes < 0) return PROM_E_ARG;
+  *out = nullptr;
+  PinnedPool& pp = pinned_pool();
+  const size_t want = std::max<size_t>(((size_t)bytes + ((size_t)1 << 21) - 1) & ~(((size_t)1 << 21) - 1),
+                                       (size_t)1 << 21);
+  std::lock_guard<std::mutex> g(pp.mu);
+  char* best = nullptr;
+  for (auto& kv : pp.bufs)
+    if (!kv.second.used && kv.second.cap >= want && kv.second.cap <= 2 * want &&
+        (!best || kv.second.cap < pp.bufs[best].cap))
+      best = kv.first;
+  if (best) {
+    pp.bufs[best].used = true;
+    *out = best;
+    return PROM_OK;
+  }
+  const size_t cap = pp.cap_bytes();
+  for (auto it = pp.bufs.begin(); pp.total + want > cap && it != pp.bufs.end();) {
+    if (!it->second.used) {
+      (void)hipHostFree(it->first);
+      pp.total -= it->second.cap;
+      it = pp.bufs.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  if (pp.total + want > cap) return PROM_E_NOMEM;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess || !p) return PROM_E_NOMEM;
+  pp.bufs[static_cast<char*>(p)] = PinnedPool::Buf{want, true};
+  pp.total += want;
+  *out = p;
+  return PROM_OK;
+}
+
+int32_t prom_host_free(void* p) {
+  PinnedPool& pp = pinned_pool();
+  std::lock_guard<std::mutex> g(pp.mu);
+  auto it = pp.bufs.find(static_cast<char*>(p));
+  if (!p || it == pp.bufs.end() || !it->second.used) return PROM_E_ARG;
+  it->second.used = false;
+  return PROM_OK;
+}
 
 int32_t prom_abi_version(void) { return PROM_ABI_VERSION; }
 
@@ -208,6 +286,7 @@ int32_t prom_table_upload(prom_ctx* ctx, int64_t n, const double* x, const doubl
     t.ymax = m;
     build_directory(ctx, t, x, n);
     PROM_HIP(hipStreamSynchronize(ctx->stream));
+    t.gen = ++ctx->table_gen;
     *table_id = store_table(ctx->tables, std::move(t));
   });
 }
@@ -246,6 +325,7 @@ int32_t prom_table_build_voigt(prom_ctx* ctx, int64_t n, const double* x, int32_
       download(log_sigma_out, t.y, n, ctx->stream);
       PROM_HIP(hipStreamSynchronize(ctx->stream));
     }
+    t.gen = ++ctx->table_gen;
     *table_id = store_table(ctx->tables, std::move(t));
   });
 }
@@ -654,7 +734,20 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       // [lo, hi] with X[lo] <= fl(s_min lambda_first) and fl(s_max lambda_last) < X[hi] (numpy's bracket j of
       // a target: the largest j <= n-2 with X[j] <= t), and a linear bracket guess verified over the slice
       tr.sig_seg_ok = false;
-      if (!tr.uniform_shift && n_atoms >= 1 && n_atoms <= 4) {
+      std::vector<double> key_sh;
+      std::vector<uint64_t> key_gen;
+      for (const auto& t : tr.terms) {
+        if (t.is_molecule) continue;
+        key_gen.push_back(ctx->tables[t.table].gen);
+        key_sh.insert(key_sh.end(), sh.begin() + t.scenario * n_orb, sh.begin() + (t.scenario + 1) * n_orb);
+      }
+      const bool seg_reuse = !tr.uniform_shift && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
+                             key_sh == tr.seg_key_sh && (int64_t)tr.seg_key_wav.size() == tr.n_wav &&
+                             std::memcmp(tr.seg_key_wav.data(), pb->wavelength, sizeof(double) * tr.n_wav) == 0;
+      if (seg_reuse) {
+        tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
+      } else if (!tr.uniform_shift && n_atoms >= 1 && n_atoms <= 4) {
+        tr.seg_key_valid = false;
         const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
         std::vector<prom::SigSeg> seg(nb * n_atoms, prom::SigSeg{0, 0, 0, 0, 0.0, 0.0});
         int32_t ia = 0;
@@ -740,6 +833,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         if (fbl.empty()) fbl.push_back(0);
         upload(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
         tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
+        tr.seg_key_wav.assign(pb->wavelength, pb->wavelength + tr.n_wav);
+        tr.seg_key_sh = std::move(key_sh);
+        tr.seg_key_gen = std::move(key_gen);
+        tr.seg_key_valid = true;
       }
     }
     tr.star = pb->has_star != 0;
@@ -990,10 +1087,22 @@ int32_t prom_transit_result(prom_ctx* ctx, double* R_out) {
     if (!tr.ran) throw Error(PROM_E_STATE, "prom_transit_result: no completed run");
     PROM_REQUIRE(R_out, "prom_transit_result: null output");
     for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
+    const size_t bytes = sizeof(double) * (size_t)tr.n_orb * (size_t)tr.n_wav;
+    const char* src = static_cast<const char*>(tr.slot[tr.last].R.p);
+    if (pinned_pool().holds(R_out, bytes)) {
+      // page-locked destination (prom_host_alloc): DMA straight into it, split over PROM_D2H_SPLIT streams
+      const char* e = std::getenv("PROM_D2H_SPLIT");
+      const size_t k = (size_t)std::max(1, std::min(prom::kMaxSlots, e ? std::atoi(e) : 1));
+      const size_t part = ((bytes + k - 1) / k + 4095) & ~(size_t)4095;
+      for (size_t i = 0; i < k && i * part < bytes; ++i)
+        PROM_HIP(hipMemcpyAsync(reinterpret_cast<char*>(R_out) + i * part, src + i * part,
+                                std::min(part, bytes - i * part), hipMemcpyDeviceToHost, ctx->streams[i]));
+      for (size_t i = 0; i < k; ++i) PROM_HIP(hipStreamSynchronize(ctx->streams[i]));
+      return;
+    }
     // D2H in chunks into pinned staging (one DMA per chunk, full link rate) while host threads copy the
     // finished chunks out to the caller's (pageable) array: the copy-out overlaps the transfer and runs on
     // several cores instead of one
-    const size_t bytes = sizeof(double) * (size_t)tr.n_orb * (size_t)tr.n_wav;
     constexpr size_t kChunk = (size_t)2 << 20;
     const size_t n_chunks = (bytes + kChunk - 1) / kChunk;
     if (ctx->pin_cap < bytes) {
@@ -1008,7 +1117,6 @@ int32_t prom_transit_result(prom_ctx* ctx, double* R_out) {
       PROM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       ctx->pin_ev.push_back(e);
     }
-    const char* src = static_cast<const char*>(tr.slot[tr.last].R.p);
     char* pin = static_cast<char*>(ctx->pin);
     for (size_t c = 0; c < n_chunks; ++c) {
       const size_t off = c * kChunk, len = std::min(kChunk, bytes - off);

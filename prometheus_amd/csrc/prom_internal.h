@@ -177,6 +177,7 @@ struct AtomTable {
   std::vector<double> hx;   // host copy of x (stellar-spectrum slice bounds)
   int32_t n_dir = 0;
   double dir_x0 = 0.0, dir_inv_h = 0.0;
+  uint64_t gen = 0;         // upload number within the context (ids are reused, generations are not)
 };
 
 struct MolTable {
@@ -290,6 +291,11 @@ struct TransitDev {
   DevBuf sig_fb;                            // blocks with an oversize slice (m = 0 for some species)
   int32_t n_sig_fb = 0;
   bool sig_seg_ok = false;
+  // inputs the sigma segments were built from (wavelengths, per-slot table generation and Doppler factors):
+  // a later problem with the same ones reuses sig_seg / sig_fb instead of rebuilding them
+  std::vector<double> seg_key_wav, seg_key_sh;
+  std::vector<uint64_t> seg_key_gen;
+  bool seg_key_valid = false;
   RunSlot slot[kMaxSlots];
   // PROM_GRAPH=1: a fast-path run is one hipGraph per slot, captured at the slot's first untimed run
   // and replayed (one host call instead of three launches; slower on ROCm 7.2, so off by default)
@@ -324,6 +330,7 @@ struct prom_ctx {
   size_t pin_cap = 0;
   std::vector<hipEvent_t> pin_ev;
   hipEvent_t fork_ev[prom::kMaxSlots] = {}, join_ev[prom::kMaxSlots] = {};
+  uint64_t table_gen = 0;        // uploads so far (AtomTable::gen)
 };
 
 namespace prom {

@@ -726,7 +726,14 @@ class Transit:
                       if not c.isMolecule)
         per_wav = 8 * n_orb * (2 + max(1, n_atoms))
         chunk = max(4096, int(max_memory_gb * 1e9) // per_wav) // WAVE_ALIGN * WAVE_ALIGN
-        R = np.empty((n_orb, n_wav)) if want_R else None
+        R = None
+        if want_R:
+            # one chunk on one device: R lands in page-locked memory from the library's pool in one DMA
+            # (transit_result(out=R) below); otherwise (or past the pool's cap) ordinary memory
+            if len(devices) == 1 and n_wav <= chunk:
+                R = _native.host_array((n_orb, n_wav))
+            if R is None:
+                R = np.empty((n_orb, n_wav))
         acc = None
         if bounds is not None:
             from .lightcurve import BandAccumulator

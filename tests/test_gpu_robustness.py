@@ -164,3 +164,62 @@ def test_band_lightcurve_array_centres(dev):
     a = tr.bandLightcurve(devices=[0])
     b = tr.bandLightcurve(line_centers=np.array([lc.NA_D2, lc.NA_D1]), devices=[0])
     assert np.array_equal(a, b)
+
+
+def test_pinned_result_arrays(dev):
+    """sumOverChords returns R in page-locked memory from the library's pool (one DMA, prom_host_alloc):
+    the values are bitwise those copied into ordinary memory, a dropped array's buffer is reused, and past
+    the pool's cap (PROM_PINNED_CAP_MB) R falls back to ordinary memory with the same values."""
+    from prometheus_amd import _native, configs, setupfile
+    cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
+                          res_low=5e-9, res_high=1e-10)
+    tr = setupfile.build_transit(cfg)
+    R1 = tr.sumOverChords(devices=[0])
+    assert isinstance(R1.base, _native._PinnedBuffer) and R1.flags.writeable and R1.flags.c_contiguous
+    with dev.lock:
+        Rp = dev.transit_result(out=np.empty_like(R1))   # pageable: staged path
+    assert np.array_equal(R1, Rp)
+    addr = R1.__array_interface__["data"][0]
+    del R1
+    gc.collect()
+    R2 = tr.sumOverChords(devices=[0])
+    assert R2.__array_interface__["data"][0] == addr    # the freed buffer came back
+    view = R2[1:]
+    del R2
+    gc.collect()
+    assert np.array_equal(view, Rp[1:])                  # a view keeps its buffer alive
+    old = os.environ.get("PROM_PINNED_CAP_MB")
+    os.environ["PROM_PINNED_CAP_MB"] = "0"
+    try:
+        R3 = tr.sumOverChords(devices=[0])
+    finally:
+        if old is None:
+            del os.environ["PROM_PINNED_CAP_MB"]
+        else:
+            os.environ["PROM_PINNED_CAP_MB"] = old
+    assert not isinstance(R3.base, _native._PinnedBuffer)
+    assert np.array_equal(R3, Rp)
+    assert rel(Rp, _oracle_R(cfg, tr.wavelength)) < R_TOL
+
+
+def test_sigma_segments_reused_across_problems(dev):
+    """prom_transit_set keeps the Doppler sigma segments of the previous problem when the wavelengths, tables
+    and Doppler factors are unchanged, and rebuilds them when any of them changes: every run of a problem is
+    bitwise its first run, and each problem matches the oracle."""
+    from prometheus_amd import configs, setupfile
+    cfg = configs.reduced(configs.get("C4"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
+                          res_low=5e-9, res_high=1e-10)
+    tr = setupfile.build_transit(cfg)
+    cfg2 = json.loads(json.dumps(cfg))
+    cfg2["Grids"]["orbphase_border"] = 0.07    # other phases: other Doppler factors, same wavelengths
+    tr2 = setupfile.build_transit(cfg2)
+    assert np.array_equal(tr.wavelength, tr2.wavelength)
+    seq = [tr, tr, tr2, tr, tr2, tr2]
+    got = [t.sumOverChords(devices=[0]).copy() for t in seq]
+    for i in (1, 3):
+        assert np.array_equal(got[i], got[0])
+    for i in (4, 5):
+        assert np.array_equal(got[i], got[2])
+    assert not np.array_equal(got[0], got[2])
+    assert rel(got[0], _oracle_R(cfg, tr.wavelength)) < R_TOL
+    assert rel(got[2], _oracle_R(cfg2, tr2.wavelength)) < R_TOL

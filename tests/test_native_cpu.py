@@ -31,7 +31,7 @@ def test_library_exports_header():
 def test_abi_version_and_no_device_here():
     from prometheus_amd import _native
     lib = _native.load_library()
-    assert lib.prom_abi_version() == _native.ABI_VERSION == 3
+    assert lib.prom_abi_version() == _native.ABI_VERSION == 4
     if _native.device_count() == 0:
         with pytest.raises(_native.NativeUnavailable):
             _native.Device(0)
@@ -50,3 +50,18 @@ def test_missing_library_is_an_error(tmp_path):
     from prometheus_amd import _native
     with pytest.raises(_native.NativeUnavailable):
         _native.load_library(str(tmp_path / "nope.so"))
+
+
+def test_pinned_pool_argument_errors():
+    """prom_host_alloc / prom_host_free reject bad arguments without touching a device."""
+    import ctypes as C
+    from prometheus_amd import _native
+    lib = _native.load_library()
+    p = C.c_void_p()
+    E_ARG = -1
+    assert _native.STATUS[E_ARG] == "PROM_E_ARG"
+    assert lib.prom_host_alloc(-1, C.byref(p)) == E_ARG
+    assert lib.prom_host_alloc(8, None) == E_ARG
+    assert lib.prom_host_free(None) == E_ARG
+    buf = np.zeros(4)
+    assert lib.prom_host_free(C.c_void_p(buf.ctypes.data)) == E_ARG   # not a pool buffer
