@@ -178,6 +178,26 @@ def host_array(shape) -> Optional[np.ndarray]:
     return np.asarray(_PinnedBuffer(lib, p.value, shape))
 
 
+_pinned_usable: Optional[bool] = None
+
+
+def pinned_copy(a) -> np.ndarray:
+    """``a`` as a C-contiguous float64 array in the pinned pool (inputs re-sent on every call, such as the
+    wavelength grid, then reach the device in one DMA), or an ordinary copy without a GPU or past the cap."""
+    global _pinned_usable
+    a = np.asarray(a, dtype=np.float64)
+    if _pinned_usable is None:
+        try:
+            _pinned_usable = device_count() > 0
+        except NativeUnavailable:
+            _pinned_usable = False
+    out = host_array(a.shape) if _pinned_usable and a.size else None
+    if out is None:
+        return np.array(a, dtype=np.float64, order="C")
+    out[...] = a
+    return out
+
+
 def _d(a: np.ndarray):
     return a.ctypes.data_as(_dp)
 

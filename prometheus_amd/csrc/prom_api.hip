@@ -114,6 +114,57 @@ PinnedPool& pinned_pool() {
   return *pool;
 }
 
+// prom_transit_set's inputs: small arrays are appended to a host image at add() (the callers' temporaries
+// may die before the flush) and reach the device as one DMA of [descriptors | data] plus one scatter kernel,
+// instead of a pageable copy each; large arrays are copied directly (one DMA when they sit in the pinned
+// pool, e.g. the wavelength grid of a Transit)
+struct Stager {
+  static constexpr size_t kSmall = (size_t)256 << 10;
+  std::vector<char> img;
+  std::vector<std::pair<DevBuf*, int64_t>> ent;   // destination, offset in img
+  std::vector<int64_t> len;
+  template <class T>
+  void add(DevBuf& b, const T* h, int64_t n, hipStream_t s) {
+    b.ensure(sizeof(T) * (size_t)std::max<int64_t>(n, 1));
+    if (n <= 0) return;
+    const size_t bytes = sizeof(T) * (size_t)n;
+    if (bytes > kSmall) {
+      PROM_HIP(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, s));
+      return;
+    }
+    const size_t off = (img.size() + 15) & ~(size_t)15;
+    img.resize(off + bytes);
+    std::memcpy(img.data() + off, h, bytes);
+    ent.push_back({&b, (int64_t)off});
+    len.push_back((int64_t)bytes);
+  }
+  void flush(prom_ctx* ctx, hipStream_t s) {
+    if (ent.empty()) return;
+    const size_t n = ent.size();
+    const size_t head = (sizeof(prom::ScatterDesc) * n + 255) & ~(size_t)255;
+    const size_t total = head + img.size();
+    if (ctx->upin_cap < total) {
+      // nothing reads the old staging: every set ends with a stream synchronisation
+      if (ctx->upin) PROM_HIP(hipHostFree(ctx->upin));
+      ctx->upin = nullptr;
+      ctx->upin_cap = 0;
+      const size_t cap = std::max<size_t>(total * 2, (size_t)1 << 20);
+      PROM_HIP(hipHostMalloc(&ctx->upin, cap, hipHostMallocDefault));
+      ctx->upin_cap = cap;
+    }
+    ctx->ustage.ensure(ctx->upin_cap);
+    char* dbase = static_cast<char*>(ctx->ustage.p);
+    auto* d = static_cast<prom::ScatterDesc*>(ctx->upin);
+    for (size_t i = 0; i < n; ++i) d[i] = prom::ScatterDesc{ent[i].first->p, (int64_t)head + ent[i].second, len[i]};
+    std::memcpy(static_cast<char*>(ctx->upin) + head, img.data(), img.size());
+    PROM_HIP(hipMemcpyAsync(dbase, ctx->upin, total, hipMemcpyHostToDevice, s));
+    prom::launch_scatter(s, dbase, reinterpret_cast<const prom::ScatterDesc*>(dbase), (int32_t)n);
+    img.clear();
+    ent.clear();
+    len.clear();
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -232,6 +283,7 @@ void prom_destroy(prom_ctx* ctx) {
     if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
   }
   if (ctx->pin) (void)hipHostFree(ctx->pin);
+  if (ctx->upin) (void)hipHostFree(ctx->upin);
   for (auto& st : ctx->streams)
     if (st) {
       (void)hipStreamSynchronize(st);
@@ -554,6 +606,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.atom_sigma_max.clear();
     tr.tab_off.assign(tr.n_sc, -1);
     const hipStream_t s = ctx->stream;
+    Stager stg;
     const int64_t n_orb = tr.n_orb;
     std::vector<double> bx(tr.n_sc * n_orb), by(tr.n_sc * n_orb), sh(tr.n_sc * n_orb);
     int64_t tab_total = 0;
@@ -615,24 +668,24 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.n_mol = n_mol;
     tr.n_terms = (int32_t)tr.terms.size();
     // uploads
-    upload(tr.wav, pb->wavelength, tr.n_wav, s);
-    upload(tr.cy, pb->chord_y, tr.n_pr, s);
-    upload(tr.cz, pb->chord_z, tr.n_pr, s);
-    upload(tr.cfout, pb->chord_fout, tr.n_pr, s);
-    upload(tr.x, pb->x, tr.n_x, s);
-    upload(tr.planet_y, pb->planet_y, n_orb, s);
-    upload(tr.moon_y, pb->moon_y, (int64_t)tr.n_moons * n_orb, s);
-    upload(tr.moon_R, pb->moon_R, tr.n_moons, s);
-    upload(tr.body_x, bx.data(), (int64_t)bx.size(), s);
-    upload(tr.body_y, by.data(), (int64_t)by.size(), s);
-    upload(tr.shift, sh.data(), (int64_t)sh.size(), s);
-    upload(tr.terms_dev, tr.terms.data(), (int64_t)tr.terms.size(), s);
-    upload(tr.sigma_max_dev, tr.atom_sigma_max.data(), (int64_t)tr.atom_sigma_max.size(), s);
+    stg.add(tr.wav, pb->wavelength, tr.n_wav, s);
+    stg.add(tr.cy, pb->chord_y, tr.n_pr, s);
+    stg.add(tr.cz, pb->chord_z, tr.n_pr, s);
+    stg.add(tr.cfout, pb->chord_fout, tr.n_pr, s);
+    stg.add(tr.x, pb->x, tr.n_x, s);
+    stg.add(tr.planet_y, pb->planet_y, n_orb, s);
+    stg.add(tr.moon_y, pb->moon_y, (int64_t)tr.n_moons * n_orb, s);
+    stg.add(tr.moon_R, pb->moon_R, tr.n_moons, s);
+    stg.add(tr.body_x, bx.data(), (int64_t)bx.size(), s);
+    stg.add(tr.body_y, by.data(), (int64_t)by.size(), s);
+    stg.add(tr.shift, sh.data(), (int64_t)sh.size(), s);
+    stg.add(tr.terms_dev, tr.terms.data(), (int64_t)tr.terms.size(), s);
+    stg.add(tr.sigma_max_dev, tr.atom_sigma_max.data(), (int64_t)tr.atom_sigma_max.size(), s);
     for (auto& md : tr.mslots) {
       md.k_B = pb->k_B > 0.0 ? pb->k_B : 1.381 * std::pow(10.0, -16);
       md.shift = tr.shift.as<double>() + (int64_t)md.scenario * n_orb;
     }
-    upload(tr.molslot, tr.mslots.data(), (int64_t)tr.mslots.size(), s);
+    stg.add(tr.molslot, tr.mslots.data(), (int64_t)tr.mslots.size(), s);
     {
       // per-scenario density bound n_ref (every built-in model peaks at p[0] = n_0 on its domain;
       // tabulated: the largest finite value) -> column normalisation c_s = 1 / (chi_s n_ref n_x dx)
@@ -716,10 +769,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         tm.table = -1;
         tm.chi = 1.0;
         tr.colargs_m.t[0] = tm;
-        upload(tr.sigma_max_m, &smax_m, 1, s);
+        stg.add(tr.sigma_max_m, &smax_m, 1, s);
         tr.qbound_m = smax_m * tr.sigtab_m.t[0].nscale;
       }
-      upload(tr.sigtab, st.data(), (int64_t)st.size(), s);
+      stg.add(tr.sigtab, st.data(), (int64_t)st.size(), s);
       tr.qbound_v = 0.0;
       for (size_t i = 0; i < st.size(); ++i) tr.qbound_v += tr.atom_sigma_max[i] * st[i].nscale;
       tr.uniform_shift = true;
@@ -822,7 +875,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
           for (auto& th : pool) th.join();
           ++ia;
         }
-        upload(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
+        stg.add(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
         std::vector<int32_t> fbl;
         for (int64_t b = 0; b < nb; ++b) {
           bool lds = true;
@@ -831,7 +884,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         }
         tr.n_sig_fb = (int32_t)fbl.size();
         if (fbl.empty()) fbl.push_back(0);
-        upload(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
+        stg.add(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
         tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
         tr.seg_key_wav.assign(pb->wavelength, pb->wavelength + tr.n_wav);
         tr.seg_key_sh = std::move(key_sh);
@@ -854,9 +907,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       tr.star_tab = prom::SigTabDev{sb.x.as<double>(), sb.y.as<double>(), sb.n, sb.offset, nullptr,
                                     sb.dir.as<int32_t>(), sb.n_dir, 0, sb.dir_x0, sb.dir_inv_h, 0.0, 0.0, 0.0,
                                     sb.hx.front(), sb.hx.back(), sb.rec.as<double4>()};
-      upload(tr.crho, pb->chord_rho, tr.n_pr, s);
-      upload(tr.cclv, pb->chord_clv, tr.n_pr, s);
-      upload(tr.cshift, pb->chord_star_shift, tr.n_pr, s);
+      stg.add(tr.crho, pb->chord_rho, tr.n_pr, s);
+      stg.add(tr.cclv, pb->chord_clv, tr.n_pr, s);
+      stg.add(tr.cshift, pb->chord_star_shift, tr.n_pr, s);
       double smin = INFINITY, smax = -INFINITY;
       bool ok = sb.n >= 2 && (int64_t)sb.hx.size() == sb.n;
       for (int32_t i = 0; i < tr.n_pr; ++i) {
@@ -897,7 +950,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         sl[3 * tl + 1] = (int32_t)m;
         sl[3 * tl + 2] = P / 2;
       }
-      upload(tr.rm_slices, sl.data(), (int64_t)sl.size(), s);
+      stg.add(tr.rm_slices, sl.data(), (int64_t)sl.size(), s);
     }
     tr.tab.ensure(sizeof(double) * std::max<int64_t>(tab_total, 1));
     {
@@ -906,7 +959,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         sd[sc].m = tr.dens[sc];
         sd[sc].tab = tr.tab_off[sc] >= 0 ? tr.tab.as<double>() + tr.tab_off[sc] : nullptr;
       }
-      upload(tr.scdev, sd.data(), (int64_t)sd.size(), s);
+      stg.add(tr.scdev, sd.data(), (int64_t)sd.size(), s);
       tr.colargs = prom::ColArgs{};
       for (int32_t i = 0; i < tr.n_sc && i < 4; ++i) tr.colargs.sc[i] = sd[i];
       for (int32_t i = 0; i < tr.n_sc && i < 4; ++i) tr.colargs_m.sc[i] = sd[i];
@@ -966,6 +1019,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);
     }
     tr.last = 0;
+    stg.flush(ctx, s);
     PROM_HIP(hipStreamSynchronize(s));
     tr.ready = true;
   });

@@ -135,6 +135,28 @@ __global__ void k_table_recs(const double* __restrict__ x, const double* __restr
   rec[i] = make_double4(xv, yv, sl, 0.0);
 }
 
+// prom_transit_set's small inputs arrive in one DMA (descriptors + data, prom_api.hip Stager); a workgroup
+// per descriptor scatters its bytes to the destination buffer (8-byte words, then the byte tail)
+__global__ void __launch_bounds__(kBlock) k_scatter(const char* __restrict__ base, const ScatterDesc* __restrict__ d) {
+  const ScatterDesc e = d[blockIdx.x];
+  const char* src = base + e.src_off;
+  char* dst = static_cast<char*>(e.dst);
+  const int64_t words = e.bytes >> 3;
+  if ((reinterpret_cast<uintptr_t>(dst) & 7) == 0) {
+    for (int64_t i = threadIdx.x; i < words; i += kBlock)
+      reinterpret_cast<uint64_t*>(dst)[i] = reinterpret_cast<const uint64_t*>(src)[i];
+    for (int64_t i = (words << 3) + threadIdx.x; i < e.bytes; i += kBlock) dst[i] = src[i];
+  } else {
+    for (int64_t i = threadIdx.x; i < e.bytes; i += kBlock) dst[i] = src[i];
+  }
+}
+
+void launch_scatter(hipStream_t s, const char* base, const ScatterDesc* d, int32_t n) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)n), dim3(kBlock), 0, s, base, d);
+  PROM_HIP(hipGetLastError());
+}
+
 void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_table_recs, dim3(grid_for(n, kBlock, (int64_t)1 << 31)), dim3(kBlock), 0, s, x, y, n, rec);

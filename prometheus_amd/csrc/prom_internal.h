@@ -125,6 +125,13 @@ struct SigTabDev {
   const double4* rec;    // [n] {x_i, y_i, slope_i = (y_{i+1} - y_i) / (x_{i+1} - x_i), 0} (AtomTable::rec)
 };
 
+// one destination of prom_transit_set's staged upload: bytes at src_off of the staging buffer -> dst
+struct ScatterDesc {
+  void* dst;
+  int64_t src_off;
+  int64_t bytes;
+};
+
 // Per 256-wavelength block and atomic slot of a Doppler-row problem (prom_api.hip sigma segments): the
 // table nodes [lo, lo + m) every row's targets fall between, and, for kind > 0, a linear bracket guess
 // g(t) = clamp((int)((t - xs) * inv), 0, m - 2) that the host verified to be within one node of numpy's
@@ -331,6 +338,10 @@ struct prom_ctx {
   std::vector<hipEvent_t> pin_ev;
   hipEvent_t fork_ev[prom::kMaxSlots] = {}, join_ev[prom::kMaxSlots] = {};
   uint64_t table_gen = 0;        // uploads so far (AtomTable::gen)
+  // prom_transit_set: its small inputs staged in page-locked memory, copied in one DMA and scattered
+  void* upin = nullptr;
+  size_t upin_cap = 0;
+  prom::DevBuf ustage;
 };
 
 namespace prom {
@@ -365,6 +376,7 @@ void launch_gridded(hipStream_t s, const double* g, int32_t nx, int32_t ny, int3
                     const double* px, const double* py, const double* pz, double* out);
 // AtomTable::rec from a table's x and y (prom_fn.hip)
 void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec);
+void launch_scatter(hipStream_t s, const char* base, const ScatterDesc* d, int32_t n);
 // per phase: sum / count of R over the band-selected wavelengths, max of R over all (prom_transit_band_stats)
 void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,
                        int32_t n_bands, const double* bounds, double* sum, int64_t* count, double* mx);

@@ -585,9 +585,15 @@ class Transit:
         self.spatialGrid = spatialGrid
         self.planet = self.atmosphere.densityDistributionList[0].planet
         self.last_stats: List[dict] = []
+        # per-run device statistics in last_stats (stage times, chord counts, exp evaluations): they time
+        # the run with events and count in the kernels, ~0.1 ms per call, so off unless asked for
+        # (this attribute, or PROM_COLLECT_STATS=1 in the environment)
+        self.collect_stats = os.environ.get("PROM_COLLECT_STATS", "0") not in ("", "0")
 
     def addWavelength(self) -> None:
-        self.wavelength = self.wavelengthGrid.constructWavelengthGrid(self.atmosphere.densityDistributionList)
+        # page-locked copy (_native.pinned_copy): the grid is sent to the device on every call
+        self.wavelength = _native.pinned_copy(
+            self.wavelengthGrid.constructWavelengthGrid(self.atmosphere.densityDistributionList))
 
     def checkBlock(self, phi: float, rho: float, orbphase: float) -> bool:
         """Scalar blocking test (gasProperties.py:1107-1130; the moon test uses R_moon^2 here,
@@ -601,21 +607,36 @@ class Transit:
         return False
 
     # ---- host-side set-up: O(n_phase + n_chord-positions) scalars, numpy as in the reference ----
-    def _host_inputs(self) -> dict:
-        g = self.spatialGrid
-        star = self.planet.hostStar
+    def _chord_geometry(self, g, star) -> tuple:
+        """(phi, rho, y, z, clv, fout, orbphase, x) of the chord grid: a function of the grid's and the
+        star's scalars only, so it is kept and rebuilt when any of them changes (retrieval loops call
+        sumOverChords with the same geometry and new densities)."""
+        key = (g.x_midpoint, g.x_border, g.x_steps, g.rho_border, g.rho_steps, g.phi_steps, g.orbphase_border,
+               g.orbphase_steps, star.R, star.CLV_u1, star.CLV_u2)
+        cached = getattr(self, "_geo_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
         phi, rho = g.getChordPositions()
         y, z = rho * np.sin(phi), rho * np.cos(phi)
         mu = np.sqrt(np.clip(1. - rho ** 2 / star.R ** 2, 0, 1))
         clv = 1. - star.CLV_u1 * (1. - mu) - star.CLV_u2 * (1. - mu) ** 2
         fout = rho * (np.ones_like(clv) * clv)
+        geo = (phi, rho, y, z, clv, fout, g.constructOrbphaseAxis(), g.constructXaxis())
+        for a in geo:
+            a.flags.writeable = False
+        self._geo_cache = (key, geo)
+        return geo
+
+    def _host_inputs(self) -> dict:
+        g = self.spatialGrid
+        star = self.planet.hostStar
+        phi, rho, y, z, clv, fout, orb, xaxis = self._chord_geometry(g, star)
         stellar = None
         if star.Fstar_function is not None:
             # gasProperties.py:1183-1184: the Rossiter-McLaughlin shift of each chord's stellar spectrum
             v_star = star.vsiniStarrot * rho / star.R * np.cos(phi - star.phiStarrot)
             stellar = {"rho": rho, "clv": clv, "shift": const.calculateDopplerShift(v_star),
                        "table": self._star_table(star.Fstar_function)}
-        orb = g.constructOrbphaseAxis()
         moons = [d.moon for d in self.atmosphere.densityDistributionList if d.hasMoon]
         scen = []
         need_tab = []
@@ -624,7 +645,7 @@ class Transit:
             try:
                 kind, params, body = d.densityModel()
                 if kind == _native.DENSITY_GRIDDED:
-                    d.checkBounds(g.constructXaxis()[None, :], y[:, None], z[:, None])
+                    d.checkBounds(xaxis[None, :], y[:, None], z[:, None])
                     entry.update(kind=kind, params=params, n_tabulated=d._packed)
                 else:
                     bx, by = body.getPosition(orb)
@@ -640,7 +661,7 @@ class Transit:
             for e in need_tab:
                 e["n_tabulated"] = np.asarray(e["dist"].calculateNumberDensity(x, cg[:, 0], cg[:, 1], cg[:, 2]),
                                               dtype=np.float64).reshape(len(cg), len(x))
-        return {"y": y, "z": z, "fout": fout, "orb": orb, "x": g.constructXaxis(), "dx": g.getDeltaX(),
+        return {"y": y, "z": z, "fout": fout, "orb": orb, "x": xaxis, "dx": g.getDeltaX(),
                 "planet_y": self.planet.a * np.sin(orb), "planet_R": self.planet.R,
                 "moon_y": np.array([m.getPosition(orb)[1] for m in moons]).reshape(len(moons), len(orb)),
                 "moon_R": np.array([m.R for m in moons], dtype=np.float64), "scenarios": scen,
@@ -750,7 +771,7 @@ class Transit:
                     for a in range(lo, hi, chunk):
                         b = min(hi, a + chunk)
                         dev.transit_set(self._problem(dev, host, a, b, cull_tau, options))
-                        st = dev.transit_run(stats=True)
+                        st = dev.transit_run(stats=True) if self.collect_stats else dev.transit_run() or {}
                         if R is not None:
                             if a == 0 and b == n_wav:   # one chunk: straight into the result
                                 dev.transit_result(out=R)

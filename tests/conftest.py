@@ -8,6 +8,8 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
+# the tests read Transit.last_stats (per-run chord counts, kernel variants, exp evaluations)
+os.environ.setdefault("PROM_COLLECT_STATS", "1")
 
 
 def pytest_configure(config):

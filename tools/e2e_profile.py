@@ -17,9 +17,9 @@ tr = setupfile.build_transit(configs.get(name))
 dev = _native.get_device(0)
 for _ in range(3):
     tr.sumOverChords(devices=[0])
-Rbuf = np.empty((len(tr.spatialGrid.constructOrbphaseAxis()), len(tr.wavelength)))
+Rbuf = _native.host_array((len(tr.spatialGrid.constructOrbphaseAxis()), len(tr.wavelength)))
 Rbuf[:] = 0.0
-st = {k: [] for k in ("host_inputs", "problem", "set", "run", "result", "total", "sumOverChords")}
+st = {k: [] for k in ("host_inputs", "problem", "set", "run_stats", "result_pinned", "total", "sumOverChords")}
 for _ in range(20):
     t0 = time.perf_counter()
     host = tr._host_inputs()
@@ -28,8 +28,7 @@ for _ in range(20):
     t2 = time.perf_counter()
     dev.transit_set(prob)
     t3 = time.perf_counter()
-    dev.transit_run()
-    dev.synchronize()
+    dev.transit_run(stats=True)
     t4 = time.perf_counter()
     R = dev.transit_result(out=Rbuf)
     t5 = time.perf_counter()
@@ -37,6 +36,6 @@ for _ in range(20):
     t6 = time.perf_counter()
     for k, v in zip(st, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t5 - t0, t6 - t5)):
         st[k].append(v * 1e3)
-print(name, "R", R.shape, "%.1f MB" % (R.nbytes / 1e6), "(result: into a reused array; sumOverChords: a new one)")
+print(name, "R", R.shape, "%.1f MB" % (R.nbytes / 1e6), "(result: into a reused pinned array; sumOverChords: a new one from the pool)")
 for k, v in st.items():
     print("  %-14s median %7.3f ms" % (k, float(np.median(v))))

@@ -25,6 +25,7 @@ def main():
     a = ap.parse_args()
     cfg = configs.get(a.config)
     tr = setupfile.build_transit(cfg)
+    tr.collect_stats = True
     g = cfg["Grids"]
     n_pts = None
     for mode in ("flat", "star"):
