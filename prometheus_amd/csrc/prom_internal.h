@@ -78,7 +78,10 @@ inline int n_tail_moments(int S) { return S == 1 ? 8 : (S + 1) * (S + 2) * (S + 
 
 // Doppler cross-section rows: table nodes a resampling workgroup stages in LDS per species (prom_api.hip
 // sigma segments; larger slices gather from the global table).
-constexpr int kSigSeg = 512;
+#ifndef PROM_SIG_SEG
+#define PROM_SIG_SEG 512
+#endif
+constexpr int kSigSeg = PROM_SIG_SEG;
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
 constexpr int kSigRowChunk = 8;   // rows per resampling workgroup
 

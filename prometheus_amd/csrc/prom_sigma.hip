@@ -5,7 +5,10 @@
 namespace prom {
 
 static_assert(kSigBlockW == kBlock, "sigma segments are built per kBlock wavelengths");
-constexpr int kSigFbRows = 1;   // rows per gathering workgroup (independent lookups in flight per lane)
+#ifndef PROM_SIG_FB_ROWS
+#define PROM_SIG_FB_ROWS 1
+#endif
+constexpr int kSigFbRows = PROM_SIG_FB_ROWS;   // rows per gathering workgroup (independent lookups in flight per lane)
 
 // ---- Doppler-shifted cross-section rows (orbital Doppler shift: one row per phase) ----------------
 // The host (prom_api.hip sigma segments) gives, per 256-wavelength block and atomic slot, the table nodes
