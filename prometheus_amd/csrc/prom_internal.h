@@ -83,7 +83,10 @@ inline int n_tail_moments(int S) { return S == 1 ? 8 : (S + 1) * (S + 2) * (S + 
 #endif
 constexpr int kSigSeg = PROM_SIG_SEG;
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
-constexpr int kSigRowChunk = 8;   // rows per resampling workgroup
+#ifndef PROM_SIG_ROWS
+#define PROM_SIG_ROWS 8
+#endif
+constexpr int kSigRowChunk = PROM_SIG_ROWS;   // rows per resampling workgroup (4, 8 or 16)
 
 // Stellar-spectrum path: star-table nodes a tau workgroup stages in LDS (prom_api.hip rm_slices).
 constexpr int kRmStarMax = 1024;

@@ -184,8 +184,9 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
   }
   // rows' outputs; their Q values go through LDS (over the slice, no longer read) so that the half-tile
   // ranges of all rows take one pass: thread (r, h, p) reduces 8 values, then 8 lanes combine by DPP
-  float* sq = reinterpret_cast<float*>(sxf);   // [kSigRowChunk][kBlock]
-  static_assert(sizeof(sxf) >= sizeof(float) * kSigRowChunk * kBlock, "Q staging fits the slice");
+  constexpr bool kSqAlias = sizeof(double2) * kSigSeg >= sizeof(float) * kSigRowChunk * kBlock;
+  __shared__ float sqx[kSqAlias ? 1 : kSigRowChunk * kBlock];
+  float* sq = kSqAlias ? reinterpret_cast<float*>(sxf) : sqx;   // [kSigRowChunk][kBlock]
   float qv[kSigRowChunk];
 #pragma unroll
   for (int r = 0; r < kSigRowChunk; ++r) {
@@ -198,15 +199,18 @@ __global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, cons
   for (int r = 0; r < kSigRowChunk; ++r) sq[r * kBlock + tid] = qv[r];
   __syncthreads();
   {
-    static_assert(kSigRowChunk * 4 * 8 == kBlock, "one thread per (row, half tile, eighth)");
-    const int r = tid >> 5, h = (tid >> 3) & 3, pp = tid & 7;
-    const float* q8 = sq + r * kBlock + h * 64 + pp * 8;
+    // TPH threads per (row, half tile), VPT values each, then log2(TPH) DPP steps
+    constexpr int TPH = kBlock / (kSigRowChunk * 4), VPT = 64 / TPH;
+    static_assert(TPH >= 4 && TPH <= 16 && TPH * VPT == 64, "4 to 16 threads per (row, half tile)");
+    const int r = tid / (4 * TPH), h = (tid / TPH) & 3, pp = tid % TPH;
+    const float* q8 = sq + r * kBlock + h * 64 + pp * VPT;
     float mn = q8[0], mx = q8[0];
 #pragma unroll
-    for (int i = 1; i < 8; ++i) { mn = fminf(mn, q8[i]); mx = fmaxf(mx, q8[i]); }
+    for (int i = 1; i < VPT; ++i) { mn = fminf(mn, q8[i]); mx = fmaxf(mx, q8[i]); }
     mn = fminf(mn, dpp_movf<0xB1>(mn)); mx = fmaxf(mx, dpp_movf<0xB1>(mx));     // quad_perm [1,0,3,2]
     mn = fminf(mn, dpp_movf<0x4E>(mn)); mx = fmaxf(mx, dpp_movf<0x4E>(mx));     // quad_perm [2,3,0,1]
-    mn = fminf(mn, dpp_movf<0x141>(mn)); mx = fmaxf(mx, dpp_movf<0x141>(mx));   // row_half_mirror
+    if (TPH >= 8) { mn = fminf(mn, dpp_movf<0x141>(mn)); mx = fmaxf(mx, dpp_movf<0x141>(mx)); }   // row_half_mirror
+    if (TPH >= 16) { mn = fminf(mn, dpp_movf<0x140>(mn)); mx = fmaxf(mx, dpp_movf<0x140>(mx)); }  // row_mirror
     const int64_t hw2 = wb * (kBlock / 64) + h;
     if (pp == 0 && r0 + r < n_rows && hw2 < n_halves)
       reinterpret_cast<float2*>(tq)[(int64_t)(r0 + r) * n_halves + hw2] = q_range(mn, mx);

@@ -1333,7 +1333,6 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
                                                   const uint8_t* __restrict__ zfl, int32_t sig_rows,
                                                   unsigned long long* __restrict__ evals,
                                                   double* __restrict__ R) {
-  constexpr Monos<NS> M{};
   constexpr int K = Monos<NS>::K;
   constexpr int ST = 1 + NS;
   __shared__ double srec[kTP][2 * 64 * ST];   // per wavefront: two chunks of 64 records
