@@ -603,6 +603,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
 #pragma unroll
       for (int s = 0; s < NS; ++s) nv[k][s] = in ? nc0[s * nstride + ip] : 0.0;
     }
+    PROM_TS(o * 16 + 7);
     double fp = 0.0, tp = 0.0;
     int32_t c[5] = {0, 0, 0, 0, 0};   // active (not tail), transparent, blocked, nonfinite, tail
     uint32_t tailbits = 0;
@@ -884,6 +885,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         for (int m = 0; m < K; ++m) msum[m] += Fv[k] * mono_eval<NS>(M, m, pw);
       }
     }
+    PROM_TS(o * 16 + 5);
     // ---- 5. combined workgroup scan (DPP): group ids (prefix sum of heads), A (prefix min of a),
     //         suffix moments; the B envelope needs no scan: records are sorted by 2^-30 buckets of
     //         b, so every later record has b_j <= b_i (1 + 2^-29) (b >= 1 only ahead of b < 1)
@@ -904,6 +906,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     if (lane == 63) { pg_[wid] = hinc; pm_[wid][K] = ainc; }
     if (lane == 0) pm_[wid][K + 1] = bw;
     __syncthreads();
+    PROM_TS(o * 16 + 6);
     int32_t gb = hinc - nheads, gtot = 0;
     double ball = 0.0;
     for (int w = 0; w < NW; ++w) {
