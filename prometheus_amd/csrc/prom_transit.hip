@@ -631,14 +631,16 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         else ++c[0];
       }
     }
-    // combined: prefixes of the candidate and tail counts, wavefront totals of everything (DPP scans)
-    const int32_t inc = wave_prefix<int32_t>(c[0], OpAdd());
-    const int32_t inct = wave_prefix<int32_t>(c[4], OpAdd());
+    // combined: prefixes of the candidate and tail counts, wavefront totals of everything (DPP scans); the
+    // five counts (<= kLD per lane, <= 64 kLD = 512 per wavefront) travel as 10-bit fields of two scans
+    static_assert(64 * kLD < 1024, "10-bit count fields");
+    const int32_t pa = wave_prefix<int32_t>(c[0] | (c[4] << 10) | (c[1] << 20), OpAdd());
+    const int32_t pb = lane_read(wave_prefix<int32_t>(c[2] | (c[3] << 10), OpAdd()), 63);
+    const int32_t pa63 = lane_read(pa, 63);
+    const int32_t inc = pa & 1023, inct = (pa >> 10) & 1023;
     const double fpw = lane_read(wave_prefix<double>(fp, OpAdd()), 63);
     const double tpw = lane_read(wave_prefix<double>(tp, OpAdd()), 63);
-    const int32_t c1w = lane_read(wave_prefix<int32_t>(c[1], OpAdd()), 63);
-    const int32_t c2w = lane_read(wave_prefix<int32_t>(c[2], OpAdd()), 63);
-    const int32_t c3w = lane_read(wave_prefix<int32_t>(c[3], OpAdd()), 63);
+    const int32_t c1w = (pa63 >> 20) & 1023, c2w = pb & 1023, c3w = (pb >> 10) & 1023;
     __syncthreads();
     if (lane == 63) { pi_[wid][0] = inc; pi_[wid][4] = inct; }
     if (lane == 0) {
