@@ -296,6 +296,15 @@ def main():
         flops_unit += 6 * len(host["x"])
     flops = evals * flops_unit
     traffic = latest_profile_traffic("prom::" + tau_kernel, cfg_name)
+    # latency of one run alone on an idle device (host clock: submit, kernels, synchronize; no stats
+    # instrumentation), median of 20 -- what one retrieval sample waits for with inputs resident; not `value`
+    lat = []
+    for _ in range(20):
+        t_l = time.perf_counter()
+        dev.transit_run()
+        dev.synchronize()
+        lat.append(time.perf_counter() - t_l)
+    single_run_ms = float(np.median(lat)) * 1e3
     # end-to-end (host prep + H2D + run + D2H) for reference: median of 7 sumOverChords calls after one
     # warm-up call (first-call costs: pinned pool, host threads, page faults)
     R, e2e_s = None, None
@@ -339,6 +348,7 @@ def main():
                               "achieved_tflops": flops / (tau_ms * 1e-3) / 1e12,
                               "peak_tflops": FP64_VALU_PEAK_TFLOPS}},
         "stage_ms_single_run": {"columns_order": st["ms_density"], "tau": st["ms_tau"], "total": st["ms_total"]},
+        "single_run_ms": single_run_ms,
         "chords": {"active": st["active_chords"], "transparent": st["transparent_chords"],
                    "blocked": st["blocked_chords"], "integrated_records": st["tau_records"]},
         "setup_s": setup_s,

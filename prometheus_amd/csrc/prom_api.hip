@@ -1066,6 +1066,10 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     rs.aux = fork_ok ? ctx->streams[si + tr.depth] : nullptr;
     rs.ev_fork = fork_ok ? ctx->fork_ev[si] : nullptr;
     rs.ev_join = fork_ok ? ctx->join_ev[si] : nullptr;
+    // staggered kernel order on alternate slots (PROM_SIG_STAGGER=1): odd slots queue the Doppler sigma
+    // rows after k_order, so their latency-bound ordering overlaps the even slots' full-chip kernels
+    const char* sg = std::getenv("PROM_SIG_STAGGER");
+    rs.sig_late = tr.depth > 1 && (si & 1) && sg && std::atoi(sg) != 0;
     if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
     if (!stats && !timed && tr.graphs && tr.depth > 1) {
       // untimed fast-path run: replay the slot's graph (captured here the first time)

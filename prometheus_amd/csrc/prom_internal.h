@@ -233,6 +233,9 @@ struct RunSlot {
   // and ordering kernels); set per run by prom_transit_run, null: one stream
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // one stream, Doppler sigma rows queued after k_order instead of before k_columns8 (set per run by
+  // prom_transit_run on alternate slots of a pipelined problem: staggers the slots' kernel order)
+  bool sig_late = false;
 };
 
 // Everything the transit kernels need, as device pointers.

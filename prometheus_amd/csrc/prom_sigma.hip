@@ -9,6 +9,15 @@ static_assert(kSigBlockW == kBlock, "sigma segments are built per kBlock wavelen
 #define PROM_SIG_FB_ROWS 1
 #endif
 constexpr int kSigFbRows = PROM_SIG_FB_ROWS;   // rows per gathering workgroup (independent lookups in flight per lane)
+// minimum waves per SIMD the register allocation must allow (0: the compiler's choice, 70 VGPRs = 7 waves)
+#ifndef PROM_SIG_WPE
+#define PROM_SIG_WPE 0
+#endif
+#if PROM_SIG_WPE > 0
+#define PROM_SIG_ATTR __attribute__((amdgpu_waves_per_eu(PROM_SIG_WPE)))
+#else
+#define PROM_SIG_ATTR
+#endif
 
 // ---- Doppler-shifted cross-section rows (orbital Doppler shift: one row per phase) ----------------
 // The host (prom_api.hip sigma segments) gives, per 256-wavelength block and atomic slot, the table nodes
@@ -81,7 +90,7 @@ __device__ __forceinline__ void sigma_row_out(int32_t orow, int32_t nse, const d
 // reads the global records) or no verified guess (slices straddling a change of node spacing, targets
 // outside the table: sigma_of's directory lookup).
 template <int NSIG>
-__global__ void __launch_bounds__(kBlock) k_sigma_rows(const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
+__global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_rows(const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
                                                  int32_t n_rows, const SigSeg* __restrict__ seg,
                                                  const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk, int32_t n_rc,
                                                  double* __restrict__ sig, float4* __restrict__ tq, int32_t merge_sp,

@@ -2044,6 +2044,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   hipEvent_t ev_tau0 = (ev && stage_events) ? ev[2] : nullptr;
   // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
+  bool sig_after_order = false;   // Doppler sigma rows still to queue, after k_order (rs.sig_late)
   if (cols8) {
     // with resampling: chord workgroups padded to a multiple of 8, sigma workgroups rounded up to one
     const unsigned chord_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
@@ -2058,6 +2059,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // join before the tile windows.  The fork point is taken before the column kernel is queued (the rows
     // wait only for the slot's previous run); PROM_SIGMA_FIRST=1 queues them before the column kernel.
     const bool sig_first = !sig_fork || (std::getenv("PROM_SIGMA_FIRST") && std::atoi(std::getenv("PROM_SIGMA_FIRST")));
+    sig_after_order = rows_seg && !fused && !sig_fork && rs.sig_late && wpath;
     if (sig_fork) {
       PROM_HIP(hipEventRecord(rs.ev_fork, s));
       PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
@@ -2073,7 +2075,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     if (fused) {
       launch_qbounds(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
                      rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale);
-    } else if (rows_seg && sig_first) {
+    } else if (rows_seg && sig_first && !sig_after_order) {
       sigma_rows();
     }
 #define PROM_COLS(SV, NSV)                                                                               \
@@ -2101,6 +2103,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #undef PROM_COLS
     PROM_HIP(hipGetLastError());
     if (rows_seg && !fused && !sig_first) sigma_rows();
+    ev0 = nullptr;
   } else {
     if (ev0) PROM_HIP(hipEventRecord(ev0, s));
     for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
@@ -2165,6 +2168,11 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       default: PROM_CHW(4); break;
     }
 #undef PROM_CHW
+    if (sig_after_order) {
+      launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
+                        tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0,
+                        tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(), nullptr);
+    }
     if (pre_sigma) {
       // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
       if (sig_rows > 1 && tr.sig_seg_ok && !fused && rs.aux && rs.ev_join) PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
