@@ -104,6 +104,29 @@ def test_pipelined_runs_bitwise(dev, x_steps):
     assert rel(R1, _oracle_R(cfg, tr.wavelength)) < R_TOL
 
 
+@pytest.mark.parametrize("stagger", ["0", "1"])
+def test_pipelined_doppler_runs_bitwise(dev, stagger, monkeypatch):
+    """Orbital Doppler shift (sigma rows per phase), eight back-to-back runs over the pipeline slots, with
+    and without the staggered kernel order (PROM_SIG_STAGGER=1: odd slots queue k_sigma_rows after
+    k_order): every run's R is bitwise the R of a single synchronised run."""
+    from prometheus_amd import setupfile
+    d = np.load(os.path.join(G, "transit_C3r.npz"))
+    tr = setupfile.build_transit(json.loads(str(d["config"])))
+    R1 = tr.sumOverChords(devices=[0])
+    monkeypatch.setenv("PROM_SIG_STAGGER", stagger)
+    host = tr._host_inputs()
+    with dev.lock:
+        dev.transit_set(tr._problem(dev, host, 0, len(tr.wavelength), 0.0))
+        for _ in range(8):
+            dev.transit_run()
+        R8 = dev.transit_result()
+        dev.transit_run()
+        dev.synchronize()
+        R9 = dev.transit_result()
+    assert np.array_equal(R1, R8) and np.array_equal(R1, R9)
+    assert rel(R1, d["R"]) < R_TOL
+
+
 def test_more_active_chords_than_window_limit(dev):
     """100 x 50 = 5,000 chords per phase, nearly all active (power law q = 6): more than the sorted
     window limit (4,096), so the phases take the unsorted compaction and the heavy tau units; checked

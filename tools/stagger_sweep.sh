@@ -5,7 +5,3 @@ for c in C3 C4 C2; do for sv in 0 1; do
 done; done
 PROM_SIG_STAGGER=1 timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread -k "pipelin or C3 or c3 or doppler or Doppler" > gpurun_out/stag/pytest.log 2>&1; tail -2 gpurun_out/stag/pytest.log
 
-for c in C3 C4; do
-  PROMETHEUS_AMD_LIB=prometheus_amd/libprom_hip_w8.so timeout -k 10 200 python -u bench.py --config $c --no-cpu-baseline --steps 200 --warmup 20 > gpurun_out/stag/w8_${c}.log 2>&1 || exit 1
-  echo "$c w8 $(tail -1 gpurun_out/stag/w8_${c}.log | cut -c1-200 | grep -o '"value": [0-9.e+]*, .*"ms_per_step": [0-9.]*')"
-done
