@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PROM_ABI_VERSION 4
+#define PROM_ABI_VERSION 5
 
 typedef struct prom_ctx prom_ctx;
 
@@ -245,6 +245,18 @@ int32_t prom_transit_columns(prom_ctx* ctx, double* N_out);
  * maxima combine with max; the light curve is (sum / count) / max. */
 int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bounds, double* sum_out,
                                 int64_t* count_out, double* max_out);
+
+/* Disk-integrated stellar flux of a rotating star (ABI 5).  Replaces the rotating branch of
+ * Star.getFstarIntegrated (celestialBodies.py:299-311, through calculateRM :226-240 and calculateCLV
+ * :212-224): for every wavelength, the n_cells disk cells in the reference's loop order (phi outer, rho
+ * inner) are accumulated one after the other,
+ *   out[w] += (((10^interp(wavelength[w] / shift[c]) * clv[c]) * dphi) * drho) * rho[c],
+ * interp = numpy.interp over the star table (offset 0).  The caller gives each cell's Doppler factor
+ * (calculateDopplerShift of the surface velocity) and CLV factor.  A target outside the table is an
+ * error (PROM_E_ARG), as the reference's interp1d(bounds_error=True) raises. */
+int32_t prom_star_disk_flux(prom_ctx* ctx, int32_t star_table, int32_t n_cells, const double* shift,
+                            const double* clv, const double* rho, double dphi, double drho, int64_t n_wav,
+                            const double* wavelength, double* out);
 
 /* Live per-run timing of the tau kernel without per-run synchronisation: between prom_timing_begin
  * and prom_timing_end every timed prom_transit_run carries a HIP event pair (the ordering kernel's

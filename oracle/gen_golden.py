@@ -183,6 +183,63 @@ def gen_stars():
               fstar_sha=np.array(_sha(np.concatenate([x, np.log10(F)]))))
 
 
+def gen_star_methods():
+    """Star.round_to_grid / calculateRM / getFstar / getFstarIntegrated (celestialBodies.py:113-333) of the
+    reference, on WASP-49's star with CLV coefficients, a synthetic spectrum installed as the reference's
+    interp1d Fstar_function, and a small disk grid: the closed form (vsini = 0) and the rotating branch."""
+    from scipy.interpolate import interp1d
+    from oracle.prom_oracle import synthetic_star_spectrum
+    planet = bodies.AvailablePlanets().findPlanet("WASP-49b")
+    st = planet.hostStar
+    lo, hi = 5886e-8, 5896e-8
+    x, F = synthetic_star_spectrum(lo, hi)
+    wav = np.linspace(lo, hi, 301)
+    grid = geom.Grid(planet.a, 5. * planet.R, 10, 0.8 * st.R, 6, 7, 0.1, 3)
+    pts = np.array([[0.3, 0.2 * st.R], [2.1, 0.55 * st.R], [4.0, 0.9 * st.R], [5.9, 0.05 * st.R]])
+    out = {"wavelength": wav, "spec_x": x, "spec_logF": np.log10(F), "points": pts, "R_star": np.array(st.R),
+           "grid": np.array([grid.x_midpoint, grid.x_border, grid.x_steps, grid.rho_border, grid.rho_steps,
+                             grid.phi_steps, grid.orbphase_border, grid.orbphase_steps])}
+    cases = {"static": (0.31, 0.22, 0.0, 0.0), "rot": (0.31, 0.22, 5e6, 0.4), "rot_noclv": (0.0, 0.0, 3e6, -1.1)}
+    for name, (u1, u2, vsini, phi_rot) in cases.items():
+        st.addCLVparameters(u1, u2)
+        st.addRMparameters(vsini, phi_rot)
+        st.Fstar_function = interp1d(x, np.log10(F))
+        try:
+            FI, FU = st.getFstarIntegrated(wav, grid)
+            out[name + "_integrated"] = FI
+            out[name + "_upper"] = FU
+            out[name + "_getFstar"] = np.array([st.getFstar(p[0], p[1], wav) for p in pts])
+            if vsini != 0.0:
+                out[name + "_calculateRM"] = np.array([st.calculateRM(p[0], p[1], wav) for p in pts])
+            out[name + "_params"] = np.array([u1, u2, vsini, phi_rot])
+        finally:
+            st.addCLVparameters(0., 0.)
+            st.addRMparameters(0., 0.)
+            st.Fstar_function = None
+    # round_to_grid on getSpectrum's PHOENIX parameter grids (celestialBodies.py:146-156), ties included
+    T_grid = np.concatenate((np.arange(2300, 7100, 100), np.arange(7200, 12200, 200)))
+    log_g_grid = np.arange(0, 6.5, 0.5)
+    Z_grid = np.concatenate((np.arange(-4, -1, 1), np.arange(-1.5, 1.5, 0.5)))
+    alpha_grid = np.arange(0, 1.6, 0.2) - 0.2
+    vals = {"T": [2000., 5600., 5650., 7150., 7300., 12500., st.T_eff], "log_g": [-1., 4.25, 4.3, 7.],
+            "Z": [-5., -2.5, -1.25, 0.1, 0.25, 2.], "alpha": [-1., 0.1, 0.5, 2.]}
+    for key, g in (("T", T_grid), ("log_g", log_g_grid), ("Z", Z_grid), ("alpha", alpha_grid)):
+        out["rtg_%s_grid" % key] = g.astype(np.float64)
+        out["rtg_%s_values" % key] = np.array(vals[key], dtype=np.float64)
+        out["rtg_%s_out" % key] = np.array([bodies.Star.round_to_grid(g, v) for v in vals[key]], dtype=np.float64)
+    try:
+        st.Fstar_function = interp1d(x, np.log10(F))
+        st.addRMparameters(5e6, 0.)
+        st.calculateRM(0.0, 0.5 * st.R, np.array([x[0] * 0.9]))
+        out["rm_out_of_range_raises"] = np.array(False)
+    except ValueError:
+        out["rm_out_of_range_raises"] = np.array(True)
+    finally:
+        st.addRMparameters(0., 0.)
+        st.Fstar_function = None
+    _save("star_methods", **out)
+
+
 def gen_wavelength_grids():
     """Full-size lambda grids C1..C5 (hash + samples; C1 stored whole)."""
     out = {}
@@ -438,7 +495,7 @@ def gen_lightcurve():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["interp", "tables", "density", "grids", "molecular", "transits", "stars",
-                             "serpens", "tidal", "harness", "lightcurve"]
+                             "star_methods", "serpens", "tidal", "harness", "lightcurve"]
     if "interp" in which:
         gen_interp_kats()
     if "tables" in which:
@@ -453,6 +510,8 @@ if __name__ == "__main__":
         gen_transits()
     if "stars" in which:
         gen_stars()
+    if "star_methods" in which:
+        gen_star_methods()
     if "serpens" in which:
         gen_serpens()
     if "tidal" in which:

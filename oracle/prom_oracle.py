@@ -629,6 +629,26 @@ def apply_star(planet: Body, star: Optional[dict]) -> None:
     planet.fstar = star.get("fstar")
 
 
+def star_disk_flux(x, logF, R_star, u1, u2, vsini, phi_rot, phi_axis, rho_axis, dphi, drho, wavelength):
+    """Star.getFstarIntegrated, rotating branch (celestialBodies.py:299-311): cells in the reference's loop
+    order (phi outer, rho inner), F = 10**interp1d(x, logF)(lambda / shift) (calculateRM :226-240, interp1d
+    linear = numpy.interp in range), times calculateCLV (:212-224), accumulated one cell after the other."""
+    wavelength = np.asarray(wavelength, dtype=np.float64)
+    acc = np.zeros_like(wavelength)
+    for phi in phi_axis:
+        for rho in rho_axis:
+            v = vsini * rho / R_star * np.cos(phi - phi_rot)
+            shift = doppler_shift(v)
+            t = wavelength / shift
+            if np.any(t < x[0]) or np.any(t > x[-1]):
+                raise ValueError("target outside the stellar spectrum (interp1d bounds_error)")
+            F = 10. ** np.interp(t, x, logF)
+            arg = 1. - np.sqrt(1. - rho ** 2 / R_star ** 2)
+            F *= 1. - u1 * arg - u2 * arg ** 2
+            acc += F * dphi * drho * rho
+    return acc
+
+
 def synthetic_star_spectrum(lower_w, upper_w, step=1e-10, margin=3e-8, seed=7):
     """Seeded stand-in for a PHOENIX HiRes slice (the reference fetches it over FTP,
     celestialBodies.py:128-209; no network here): x = arange(lower_w - margin, upper_w + margin, step)

@@ -63,7 +63,7 @@ class TransitProblem(C.Structure):
                 ("chord_rho", _dp), ("chord_clv", _dp), ("chord_star_shift", _dp)]
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
 OPT_NO_WINDOW = 4
@@ -110,6 +110,8 @@ SIGNATURES = {
     "prom_transit_result": (C.c_int32, [C.c_void_p, _dp]),
     "prom_transit_columns": (C.c_int32, [C.c_void_p, _dp]),
     "prom_transit_band_stats": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _dp, C.POINTER(C.c_int64), _dp]),
+    "prom_star_disk_flux": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, _dp, _dp, _dp, C.c_double, C.c_double,
+                                        C.c_int64, _dp, _dp]),
     "prom_timing_begin": (C.c_int32, [C.c_void_p]),
     "prom_timing_end": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _ip]),
     "prom_timing_stride": (C.c_int32, [C.c_void_p, C.c_int32]),
@@ -396,6 +398,18 @@ class Device:
                                                      c.ctypes.data_as(C.POINTER(C.c_int64)), _d(m)),
                     "prom_transit_band_stats")
         return s, c, m
+
+
+    # ---- stellar disk -----------------------------------------------------------------------
+    def star_disk_flux(self, table_id: int, shift, clv, rho, dphi: float, drho: float, wavelength) -> np.ndarray:
+        """prom_star_disk_flux: sum over disk cells (in order) of 10^interp(lambda / shift) clv dphi drho rho."""
+        sh, cl, rh, w = _f64(shift), _f64(clv), _f64(rho), _f64(wavelength)
+        if not (len(sh) == len(cl) == len(rh)):
+            raise ValueError("shift, clv and rho need one value per disk cell")
+        out = np.empty(w.shape)
+        self._check(self.lib.prom_star_disk_flux(self.h, int(table_id), len(sh), _d(sh), _d(cl), _d(rh), float(dphi),
+                                                 float(drho), w.size, _d(w), _d(out)), "prom_star_disk_flux")
+        return out
 
 
 class TransitInputs:

@@ -43,9 +43,68 @@ class Star:
     def getSurfaceVelocity(self, phi, rho):
         return self.vsiniStarrot * rho / self.R * np.cos(phi - self.phiStarrot)
 
+    @staticmethod
+    def round_to_grid(grid, value):
+        """The grid point closest to value, the first one on a tie (celestialBodies.py:113-126)."""
+        diff = np.subtract(value, grid)
+        return grid[np.argmin(np.abs(diff))]
+
     def calculateCLV(self, rho):
         arg = 1. - np.sqrt(1. - rho ** 2 / self.R ** 2)
         return 1. - self.CLV_u1 * arg - self.CLV_u2 * arg ** 2
+
+    def calculateRM(self, phi, rho, wavelength):
+        """Stellar flux of the surface point (phi, rho), Doppler-shifted by the star's rotation:
+        10**Fstar_function(wavelength / shift) (celestialBodies.py:226-240).  O(n_wavelength) for one
+        point, as in the reference; the disk integral runs on the GPU (getFstarIntegrated)."""
+        shift = const.calculateDopplerShift(self.getSurfaceVelocity(phi, rho))
+        return 10. ** self.Fstar_function(wavelength / shift)
+
+    def getFstar(self, phi, rho, wavelength):
+        """Flux of one disk point: CLV only without rotation, else calculateRM * CLV
+        (celestialBodies.py:313-332)."""
+        if self.vsiniStarrot == 0.:
+            return np.ones_like(wavelength) * self.calculateCLV(rho)
+        Fstar = self.calculateRM(phi, rho, wavelength)
+        Fstar *= self.calculateCLV(rho)
+        return Fstar
+
+    def getFstarIntegrated(self, wavelength, grid, device: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """(disk-integrated flux, flux of the disk outside rho_border) (celestialBodies.py:267-311).
+
+        Without rotation both are the reference's closed forms (scalars broadcast over the wavelengths).
+        With rotation the disk integral sum_phi sum_rho F(lambda / s) clv dphi drho rho over the grid's
+        cells runs on the GPU (prom_star_disk_flux; the per-cell Doppler and CLV factors are formed here
+        exactly as the reference forms them), and the second value is zeros, as in the reference."""
+        if self.vsiniStarrot == 0.:
+            FstarIntegrated = np.pi * self.R ** 2 * (1. - self.CLV_u1 / 3. - self.CLV_u2 / 6.) * \
+                np.ones_like(wavelength)
+            upperTerm = 0.5 * (-self.CLV_u2 * self.R ** 2 - self.CLV_u1 * self.R ** 2 + self.R ** 2)
+            rb = grid.rho_border
+            term1 = -4. * self.R ** 2 * self.CLV_u1 * (1. - rb ** 2 / self.R ** 2) ** 1.5
+            term2 = self.R ** 2 * self.CLV_u2 * (6 * rb ** 2 / self.R ** 2 + 8. * (1. - rb ** 2 / self.R ** 2) ** 1.5 -
+                                                 3. * (self.R ** 2 - rb ** 2) ** 2 / self.R ** 4)
+            lowerTerm = 1. / 12. * (term1 - term2 - 6. * self.CLV_u1 * rb ** 2 + 6. * rb ** 2)
+            FstarUpper = 2. * np.pi * (upperTerm - lowerTerm) * np.ones_like(wavelength)
+            return FstarIntegrated, FstarUpper
+        from . import _native
+        from .gasProperties import _star_lookup_table
+        phiArray, rhoArray = grid.constructPhiAxis(), grid.constructRhoAxis()
+        if len(phiArray) == 0 or len(rhoArray) == 0:
+            raise UnboundLocalError("getFstarIntegrated: empty disk grid (the reference's FstarUpper is unset)")
+        shift, clv, rho = [], [], []
+        for phi in phiArray:          # the reference's loop order: phi outer, rho inner
+            for r in rhoArray:
+                shift.append(const.calculateDopplerShift(self.getSurfaceVelocity(phi, r)))
+                clv.append(self.calculateCLV(r))
+                rho.append(r)
+        w = np.asarray(wavelength, dtype=np.float64)
+        dev = _native.get_device(_native.default_device() if device is None else device)
+        tab = _star_lookup_table(self.Fstar_function)
+        with dev.lock:
+            out = dev.star_disk_flux(tab.table_id(dev), shift, clv, rho, grid.getDeltaPhi(), grid.getDeltaRho(),
+                                     w.ravel())
+        return out.reshape(w.shape), np.zeros_like(w)
 
     def getSpectrum(self):
         raise NotImplementedError("PHOENIX spectra are fetched over FTP by the reference "
@@ -72,6 +131,13 @@ class StellarSpectrum:
         self.y = np.ascontiguousarray(y, dtype=np.float64)
 
     def __call__(self, w):
+        """interp1d(x, y, kind='linear') evaluation: numpy.interp inside [x_0, x_{n-1}], ValueError outside
+        (bounds_error, scipy's default for the reference's Fstar_function)."""
+        w = np.asarray(w, dtype=np.float64)
+        if np.any(w < self.x[0]):
+            raise ValueError("A value in x_new is below the interpolation range's minimum value (%r)." % self.x[0])
+        if np.any(w > self.x[-1]):
+            raise ValueError("A value in x_new is above the interpolation range's maximum value (%r)." % self.x[-1])
         return np.interp(w, self.x, self.y)
 
 

@@ -449,7 +449,7 @@ int32_t prom_table_count(prom_ctx* ctx, int32_t* n_atomic, int32_t* n_molecular,
     for (const auto& t : ctx->tables)
       if (t.live) {
         ++a;
-        b += (int64_t)(t.x.cap + t.y.cap + t.dir.cap);
+        b += (int64_t)(t.x.cap + t.y.cap + t.dir.cap + t.rec.cap);
       }
     for (const auto& t : ctx->mtables)
       if (t.live) {
@@ -565,6 +565,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     prom::TransitDev& tr = ctx->tr;
     tr.ready = false;
     tr.ran = false;
+    // sigma-segment cache key of this set (committed at the end, after the device copy succeeded)
+    bool seg_key_new = false, seg_key_keep = false;
+    std::vector<double> new_key_sh;
+    std::vector<uint64_t> new_key_gen;
     PROM_REQUIRE(pb->n_wav >= 1 && pb->wavelength, "transit: need >= 1 wavelength");
     PROM_REQUIRE(pb->n_pr >= 1 && pb->n_orb >= 1 && pb->chord_y && pb->chord_z && pb->chord_fout,
                  "transit: need chords and phases");
@@ -797,6 +801,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       const bool seg_reuse = !tr.uniform_shift && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
                              key_sh == tr.seg_key_sh && (int64_t)tr.seg_key_wav.size() == tr.n_wav &&
                              std::memcmp(tr.seg_key_wav.data(), pb->wavelength, sizeof(double) * tr.n_wav) == 0;
+      // reused segments stay valid only if this set completes; a throw below must not leave the key
+      // pointing at buffers a later (failed) set may have reallocated
+      tr.seg_key_valid = false;
+      seg_key_keep = seg_reuse;   // the stored key stays as it is (re-validated at the end)
       if (seg_reuse) {
         tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
       } else if (!tr.uniform_shift && n_atoms >= 1 && n_atoms <= 4) {
@@ -886,10 +894,11 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         if (fbl.empty()) fbl.push_back(0);
         stg.add(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
         tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
-        tr.seg_key_wav.assign(pb->wavelength, pb->wavelength + tr.n_wav);
-        tr.seg_key_sh = std::move(key_sh);
-        tr.seg_key_gen = std::move(key_gen);
-        tr.seg_key_valid = true;
+        // the key is committed only after the segments have reached the device (end of this call):
+        // a set that throws later must not leave a key that a retry would reuse
+        seg_key_new = true;
+        new_key_sh = std::move(key_sh);
+        new_key_gen = std::move(key_gen);
       }
     }
     tr.star = pb->has_star != 0;
@@ -1021,6 +1030,14 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.last = 0;
     stg.flush(ctx, s);
     PROM_HIP(hipStreamSynchronize(s));
+    if (seg_key_new) {
+      tr.seg_key_wav.assign(pb->wavelength, pb->wavelength + tr.n_wav);
+      tr.seg_key_sh = std::move(new_key_sh);
+      tr.seg_key_gen = std::move(new_key_gen);
+      tr.seg_key_valid = true;
+    } else if (seg_key_keep) {
+      tr.seg_key_valid = true;
+    }
     tr.ready = true;
   });
 }
@@ -1231,6 +1248,50 @@ int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bo
     download(count_out, ctx->scratch[2], n_orb, st);
     download(max_out, ctx->scratch[3], n_orb, st);
     PROM_HIP(hipStreamSynchronize(st));
+  });
+}
+
+int32_t prom_star_disk_flux(prom_ctx* ctx, int32_t star_table, int32_t n_cells, const double* shift,
+                            const double* clv, const double* rho, double dphi, double drho, int64_t n_wav,
+                            const double* wavelength, double* out) {
+  return guarded(ctx, [&] {
+    PROM_REQUIRE(table_ok(ctx->tables, star_table), "prom_star_disk_flux: unknown star table");
+    PROM_REQUIRE(n_cells >= 0 && n_wav >= 0 && (n_cells == 0 || (shift && clv && rho)) &&
+                     (n_wav == 0 || (wavelength && out)),
+                 "prom_star_disk_flux: bad arguments");
+    const prom::AtomTable& sb = ctx->tables[star_table];
+    PROM_REQUIRE(sb.offset == 0.0, "prom_star_disk_flux: the star table must have offset 0 (10**Fstar_function)");
+    // interp1d(bounds_error=True) semantics of the reference's Fstar_function: every target lambda / shift
+    // inside [x_0, x_{n-1}] (IEEE division is monotone: the extremes decide)
+    double smin = INFINITY, smax = -INFINITY, lmin = INFINITY, lmax = -INFINITY;
+    for (int32_t c = 0; c < n_cells; ++c) {
+      PROM_REQUIRE(shift[c] > 0.0 && std::isfinite(shift[c]), "prom_star_disk_flux: Doppler factors must be positive");
+      smin = std::min(smin, shift[c]);
+      smax = std::max(smax, shift[c]);
+    }
+    for (int64_t w = 0; w < n_wav; ++w) {
+      PROM_REQUIRE(std::isfinite(wavelength[w]), "prom_star_disk_flux: non-finite wavelength");
+      lmin = std::min(lmin, wavelength[w]);
+      lmax = std::max(lmax, wavelength[w]);
+    }
+    if (n_cells > 0 && n_wav > 0) {
+      PROM_REQUIRE(lmin / smax >= sb.hx.front(), "prom_star_disk_flux: a target is below the interpolation range");
+      PROM_REQUIRE(lmax / smin <= sb.hx.back(), "prom_star_disk_flux: a target is above the interpolation range");
+    }
+    const prom::SigTabDev tb{sb.x.as<double>(), sb.y.as<double>(), sb.n, sb.offset, nullptr, sb.dir.as<int32_t>(),
+                             sb.n_dir, 0, sb.dir_x0, sb.dir_inv_h, 0.0, 0.0, 0.0, sb.hx.front(), sb.hx.back(),
+                             sb.rec.as<double4>()};
+    const hipStream_t s = ctx->stream;
+    upload(ctx->scratch[0], shift, n_cells, s);
+    upload(ctx->scratch[1], clv, n_cells, s);
+    upload(ctx->scratch[2], rho, n_cells, s);
+    upload(ctx->scratch[3], wavelength, n_wav, s);
+    ctx->scratch[4].ensure(sizeof(double) * std::max<int64_t>(n_wav, 1));
+    prom::launch_star_disk(s, tb, ctx->scratch[0].as<double>(), ctx->scratch[1].as<double>(),
+                           ctx->scratch[2].as<double>(), n_cells, dphi, drho, ctx->scratch[3].as<double>(), n_wav,
+                           ctx->scratch[4].as<double>());
+    download(out, ctx->scratch[4], n_wav, s);
+    PROM_HIP(hipStreamSynchronize(s));
   });
 }
 

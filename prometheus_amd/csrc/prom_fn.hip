@@ -247,4 +247,38 @@ void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_
   PROM_HIP(hipGetLastError());
 }
 
+// Star.getFstarIntegrated, rotating branch (celestialBodies.py:299-311): per wavelength, the disk cells in
+// the reference's loop order (phi outer, rho inner) accumulated one after the other,
+//   acc += (((F * clv_c) * dphi) * drho) * rho_c,   F = 10^interp(lambda / shift_c)  (calculateRM :226-240),
+// with the products rounded where numpy rounds them (-ffp-contract=off).  Four cells' lookups go out
+// together (independent directory + window loads); the sum stays sequential.
+__global__ void __launch_bounds__(kBlock) k_star_disk(const SigTabDev tb, const double* __restrict__ shift,
+                                                       const double* __restrict__ clv, const double* __restrict__ rho,
+                                                       int32_t n_cells, double dphi, double drho,
+                                                       const double* __restrict__ wav, int64_t n_wav,
+                                                       double* __restrict__ out) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_wav; w += (int64_t)gridDim.x * blockDim.x) {
+    const double lam = wav[w];
+    double acc = 0.0;
+    int32_t c = 0;
+    for (; c + 4 <= n_cells; c += 4) {
+      double F[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) F[k] = sigma_of(lam / shift[c + k], tb);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = acc + (((F[k] * clv[c + k]) * dphi) * drho) * rho[c + k];
+    }
+    for (; c < n_cells; ++c) acc = acc + (((sigma_of(lam / shift[c], tb) * clv[c]) * dphi) * drho) * rho[c];
+    out[w] = acc;
+  }
+}
+
+void launch_star_disk(hipStream_t s, const SigTabDev& tb, const double* shift, const double* clv, const double* rho,
+                      int32_t n_cells, double dphi, double drho, const double* wav, int64_t n_wav, double* out) {
+  if (n_wav == 0) return;
+  hipLaunchKernelGGL(k_star_disk, dim3(grid_for(n_wav)), dim3(kBlock), 0, s, tb, shift, clv, rho, n_cells, dphi,
+                     drho, wav, n_wav, out);
+  PROM_HIP(hipGetLastError());
+}
+
 }  // namespace prom

@@ -389,5 +389,8 @@ void launch_scatter(hipStream_t s, const char* base, const ScatterDesc* d, int32
 // per phase: sum / count of R over the band-selected wavelengths, max of R over all (prom_transit_band_stats)
 void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,
                        int32_t n_bands, const double* bounds, double* sum, int64_t* count, double* mx);
+// Star.getFstarIntegrated with rotation: the disk-integrated stellar flux per wavelength (prom_fn.hip)
+void launch_star_disk(hipStream_t s, const SigTabDev& tb, const double* shift, const double* clv, const double* rho,
+                      int32_t n_cells, double dphi, double drho, const double* wav, int64_t n_wav, double* out);
 
 }  // namespace prom

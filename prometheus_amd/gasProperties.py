@@ -576,6 +576,34 @@ class WavelengthGrid:
 
 
 # ============================================================================== transit
+_STAR_TABLES: "weakref.WeakKeyDictionary" = None
+
+
+def _star_lookup_table(fn) -> "LookupTable":
+    """Device copies of an Fstar_function's (x, log10 F) (offset 0: n_interp_log(..., 0.0),
+    gasProperties.py:1212-1219; 10**Fstar_function(...), celestialBodies.py:239), kept per function object."""
+    global _STAR_TABLES
+    import weakref
+    if isinstance(fn, LookupTable):
+        return fn
+    if _STAR_TABLES is None:
+        _STAR_TABLES = weakref.WeakKeyDictionary()
+    try:
+        tab = _STAR_TABLES.get(fn)
+    except TypeError:   # not weak-referenceable: no cache
+        tab = None
+    if tab is None:
+        x = np.ascontiguousarray(np.asarray(fn.x, dtype=np.float64))
+        if np.any(x[1:] < x[:-1]):
+            raise ValueError("Fstar_function.x must be ascending (np.interp, gasProperties.py:1214)")
+        tab = LookupTable(x, np.ascontiguousarray(np.asarray(fn.y, dtype=np.float64)), 0.0)
+        try:
+            _STAR_TABLES[fn] = tab
+        except TypeError:
+            pass
+    return tab
+
+
 class Transit:
     """Transit depth R(orbital phase, wavelength) (gasProperties.py:1074-1258)."""
 
@@ -668,20 +696,7 @@ class Transit:
                 "stellar": stellar}
 
     def _star_table(self, fn) -> "LookupTable":
-        """Device copies of Fstar_function's (x, log10 F) (offset 0: n_interp_log(..., 0.0)), cached
-        per function object."""
-        cached = getattr(self, "_star_cache", None)
-        if cached is not None and cached[0] is fn:
-            return cached[1]
-        if isinstance(fn, LookupTable):
-            tab = fn
-        else:
-            x = np.ascontiguousarray(np.asarray(fn.x, dtype=np.float64))
-            if np.any(x[1:] < x[:-1]):
-                raise ValueError("Fstar_function.x must be ascending (np.interp, gasProperties.py:1214)")
-            tab = LookupTable(x, np.ascontiguousarray(np.asarray(fn.y, dtype=np.float64)), 0.0)
-        self._star_cache = (fn, tab)
-        return tab
+        return _star_lookup_table(fn)
 
     def _problem(self, dev, host: dict, w0: int, w1: int, cull_tau: float,
                  options: int = 0) -> "_native.TransitInputs":

@@ -330,12 +330,12 @@ def test_many_los_samples_generic_columns(dev):
 
 
 @pytest.mark.parametrize("name", ["C1", "C2r", "C3r", "C4r", "exomoon", "C2", "C3"])
-def test_planned_tau_bitwise(dev, name, monkeypatch):
+def test_planned_tau_within_window_bound(dev, name, monkeypatch):
     """The planned tau kernel (k_tau_p: static (tile, 4-phase) wavefronts for light windows, heavy entries
     per 64-wavelength half with their own windows, long ones split into 64-record chunks over a workgroup)
     against k_tau_w (PROM_TAU_PLAN=0: one window per 128-wavelength tile, records summed in order).  Light
-    tiles are bitwise equal; heavy halves differ by at most the two windows' truncation bounds plus the
-    chunked summation's rounding, and never evaluate more exponentials."""
+    tiles are bitwise equal (most points); heavy halves differ by at most the two windows' truncation bounds
+    plus the chunked summation's rounding, and never evaluate more exponentials."""
     from prometheus_amd import configs
     if name in ("C2", "C3"):
         cfg = configs.get(name)
@@ -354,6 +354,10 @@ def test_planned_tau_bitwise(dev, name, monkeypatch):
     bound = 2 * (2.0 ** -40 / 24 + np.exp(-40.0)) + 1e-14
     assert np.max(np.abs(R_p - R_w)) <= bound
     assert st_p["exp_evals"] <= st_w["exp_evals"]
+    # light tiles (windows of <= kHeavy records, nearly every tile) take the same records in the same order
+    # on both kernels and are bitwise equal; only heavy halves (line cores) may differ
+    diff = R_p != R_w
+    assert np.count_nonzero(diff) <= diff.size // 2
 
 
 @pytest.mark.parametrize("name", ["C3r", "C4r", "exomoon", "C3"])

@@ -59,7 +59,10 @@ def test_table_free_keeps_memory_flat(dev):
     with dev.lock:
         dev._drain_frees()
         after = dev.table_count()
-    assert after[0] <= base[0] + 1 and after[2] <= base[2] + 3 * 8 * 20000 + 8 * (4 * 20000 + 1)
+    # one live table at most: x, y (8 B per node), the bucket directory (4 B per bucket, 4 n + 1 buckets)
+    # and the interval records (32 B per node)
+    one = 8 * 20000 * 2 + 4 * (4 * 20000 + 1) + 32 * 20000
+    assert after[0] <= base[0] + 1 and after[2] <= base[2] + one
 
 
 def test_freed_table_invalidates_problem(dev):
@@ -249,3 +252,28 @@ def test_sigma_segments_reused_across_problems(dev):
     assert not np.array_equal(got[0], got[2])
     assert rel(got[0], _oracle_R(cfg, tr.wavelength)) < R_TOL
     assert rel(got[2], _oracle_R(cfg2, tr2.wavelength)) < R_TOL
+
+
+def test_failed_set_does_not_commit_sigma_segments(dev):
+    """A prom_transit_set that builds new Doppler sigma segments and then fails (here: a stellar table with
+    a non-zero offset, rejected after the segments are built) must not leave its segment key behind: the
+    same problem without the star rebuilds the segments instead of reusing ones that never reached the
+    device, and matches the oracle (prom_api.hip seg_key_valid)."""
+    from prometheus_amd import configs, setupfile, _native
+    cfg = configs.reduced(configs.get("C4"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
+                          res_low=5e-9, res_high=1e-10)
+    tr = setupfile.build_transit(cfg)
+    R_a = tr.sumOverChords(devices=[0]).copy()
+    cfg2 = json.loads(json.dumps(cfg))
+    cfg2["Grids"]["orbphase_border"] = 0.07    # other Doppler factors: the segments are rebuilt
+    tr2 = setupfile.build_transit(cfg2)
+    host = tr2._host_inputs()
+    con = host["scenarios"][0]["dist"].constituents[0].lookupFunction   # offset 1e-50: not a star table
+    n_pr = len(host["y"])
+    host_bad = dict(host, stellar={"rho": np.ones(n_pr), "clv": np.ones(n_pr), "shift": np.ones(n_pr), "table": con})
+    with dev.lock:
+        with pytest.raises(_native.NativeError):
+            dev.transit_set(tr2._problem(dev, host_bad, 0, len(tr2.wavelength), 0.0))
+    R_c = tr2.sumOverChords(devices=[0])
+    assert rel(R_c, _oracle_R(cfg2, tr2.wavelength)) < R_TOL
+    assert rel(R_a, _oracle_R(cfg, tr.wavelength)) < R_TOL

@@ -31,7 +31,7 @@ def test_library_exports_header():
 def test_abi_version_and_no_device_here():
     from prometheus_amd import _native
     lib = _native.load_library()
-    assert lib.prom_abi_version() == _native.ABI_VERSION == 4
+    assert lib.prom_abi_version() == _native.ABI_VERSION == 5
     if _native.device_count() == 0:
         with pytest.raises(_native.NativeUnavailable):
             _native.Device(0)
