@@ -16,6 +16,13 @@ the data path (torch.distributed carries only the timing barrier and the max-ove
       (resolutionLow/N, resolutionHigh/N: ~N x the wavelengths); rank r integrates shard r.
   --scaling strong: the global spectrum is the config's grid as it stands (e.g. --config C4x10,
       C5), split into N contiguous shards.
+  --shard r/N (one process): only shard r of N of the config's grid, timed alone on one GPU -- one rank's
+      work under an N-way strong split.
+
+The N=1 line also carries, per kernel of the step, its device duration (prom_transit_kernel_ms: one run in
+flight, dispatch-packet events) with its algorithmic bytes and roofline fraction, the path-level fraction
+(compulsory bytes / ms_per_step), a live HBM read peak, and the strong-scaling projection of the two
+8-GPU configurations (C4x10, C5): T(full grid) / T(shard 0 of 8), each timed on this GPU.
 
 Prints one JSON line (rank 0).
 """
@@ -46,6 +53,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--shard", default=None, metavar="r/N",
+                    help="time only shard r of an N-way split of the config's grid (strong scaling, one process)")
+    ap.add_argument("--no-projection", action="store_true",
+                    help="skip the strong-scaling projection (C4x10 and C5, full grid vs shard 0 of 8)")
+    ap.add_argument("--kernel-runs", type=int, default=20,
+                    help="serialized runs for the per-kernel durations (prom_transit_kernel_ms)")
     ap.add_argument("--cpu-workers", type=int, default=None,
                     help="processes of the multi-core CPU baseline leg (default: this process's CPU share, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -187,11 +200,86 @@ def cpu_baseline(cfg: dict, n_sample: int, workers: int):
 CPU_SAMPLE = {"C1": 219, "C2": 12288, "C3": 6144, "C4": 12288, "C4x10": 12288, "C5": 16}
 
 
+def measured_read_peak():
+    """The measured STREAM-like HBM read peak of an MI355X (SURVEY.md 8d rule (i)): the newest committed
+    tools/microbench/hbm_peak result (profiles/r*_hbm_peak.json: 4 GiB streamed with 16-byte loads per lane,
+    best of 20 launches), as (GB/s, source) or (None, None)."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_hbm_peak.json")), reverse=True):
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+            return float(d["read_gbs_best"]), os.path.relpath(path, REPO)
+        except Exception:
+            continue
+    return None, None
+
+
+def table_nodes_in_range(tr, host, w0: int, w1: int) -> int:
+    """Refined-table nodes the shifted targets of wavelengths [w0, w1) can bracket, summed over the atomic
+    constituents (each node's x and log10 sigma: 16 algorithmic bytes)."""
+    lo, hi = float(tr.wavelength[w0]), float(tr.wavelength[w1 - 1])
+    total = 0
+    for e in host["scenarios"]:
+        sh = np.asarray(e["shift"], dtype=np.float64)
+        for con in e["dist"].constituents:
+            if con.isMolecule:
+                continue
+            x = np.asarray(con.lookupFunction.x)
+            a = np.searchsorted(x, lo * sh.min(), side="right") - 1
+            b = np.searchsorted(x, hi * sh.max(), side="left") + 1
+            total += int(max(0, min(len(x), b) - max(0, a)))
+    return total
+
+
+def time_runs(dev, prob, steps: int, warmup: int) -> float:
+    """ms per run of a problem in the pipelined loop (inputs resident; set outside the timed region)."""
+    dev.transit_set(prob)
+    dev.transit_run()
+    dev.synchronize()
+    for _ in range(warmup):
+        dev.transit_run()
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dev.transit_run()
+    dev.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def strong_projection(dev_id: int, names=("C4x10", "C5"), parts: int = 8):
+    """Strong scaling measured on one GPU: each configuration's full grid, then shard 0 of
+    `parts` (the rank with the most wavelengths: shards are equal to 256 wavelengths), both in the pipelined
+    loop.  T(full) / T(shard) is the speedup `parts` GPUs give at best (no collective, host gather only)."""
+    from prometheus_amd import _native, configs, setupfile, sharding, gasProperties
+    out = {}
+    for name in names:
+        cfg = configs.get(name)
+        if any(sp not in ("NaI", "KI", "CaII", "MgI") for sc in cfg["Species"].values() for sp in sc):
+            gasProperties.register_molecular_table("H2O", configs.synthetic_molecular_table())
+        tr = setupfile.build_transit(cfg)
+        dev = _native.get_device(dev_id)
+        host = tr._host_inputs()
+        n = len(tr.wavelength)
+        steps, warm = (10, 3) if name == "C5" else (60, 10)
+        t_full = time_runs(dev, tr._problem(dev, host, 0, n, 0.0), steps, warm)
+        shards = sharding.split(n, parts)
+        a, b = max(shards, key=lambda ab: ab[1] - ab[0])
+        k_full = dev.transit_kernel_ms(5)
+        t_shard = time_runs(dev, tr._problem(dev, host, a, b, 0.0), steps, warm)
+        k_shard = dev.transit_kernel_ms(5)
+        out[name] = {"wavelengths": n, "phases": len(host["orb"]), "shard": [a, b], "shards": parts,
+                     "ms_full": t_full, "ms_shard": t_shard, "projected_speedup": t_full / t_shard,
+                     "projected_efficiency": t_full / t_shard / parts,
+                     "kernel_ms_full": k_full, "kernel_ms_shard": k_shard}
+        del tr
+    return out
+
+
 def main():
     args = parse()
     rank, local_rank, world = dist_env()
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard:
         # before anything touches the GPU: the multi-core leg forks worker processes
         cfgc = global_config(args.config, 1)
         cfgc["_name"] = args.config
@@ -209,7 +297,8 @@ def main():
     dev_id = local_rank % max(1, _native.device_count())
     _native.set_default_device(dev_id)
 
-    cfg = global_config(args.config, world, args.scaling)
+    scaling = "strong" if args.shard else args.scaling
+    cfg = global_config(args.config, world, scaling)
     cfg_name = args.config
     if any(sp not in ("NaI", "KI", "CaII", "MgI") for sc in cfg["Species"].values() for sp in sc):
         from prometheus_amd.configs import synthetic_molecular_table
@@ -218,7 +307,13 @@ def main():
     tr = setupfile.build_transit(cfg)   # lambda grid + device Voigt tables on this rank's GPU
     dev = _native.get_device(dev_id)
     n_wav_global = len(tr.wavelength)
-    w0, w1 = sharding.shard_for_rank(n_wav_global, world, rank)   # tile-aligned contiguous shards
+    if args.shard:
+        sr, sn = (int(v) for v in args.shard.split("/"))
+        if not (0 <= sr < sn):
+            raise SystemExit("--shard r/N needs 0 <= r < N")
+        w0, w1 = sharding.shard_for_rank(n_wav_global, sn, sr)
+    else:
+        w0, w1 = sharding.shard_for_rank(n_wav_global, world, rank)   # tile-aligned contiguous shards
     host = tr._host_inputs()
     prob = tr._problem(dev, host, w0, w1, 0.0)
     dev.transit_set(prob)
@@ -262,42 +357,83 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_pts * args.steps / elapsed
 
-    # dominant kernel: k_tau_p (planned windowed tau/exp/disk-sum; k_tau_w when the planned path does
-    # not apply); mean launch duration from the start/stop events carried on its own dispatch packets
-    # over the timed runs
-    # (molecular species: the fused molecular kernel k_tau_mol)
     # variant // 10: 3 planned tau kernel on sigma rows, 5 planned with the Doppler sigma fused in
     tv = st.get("tau_kernel_variant", 0) // 10
     fused = tv == 5
-    tau_kernel = ("k_tau_mol" if getattr(prob, "n_molecules", 0) else
-                  "k_tau_p" if tv in (3, 5) else "k_tau_w")
-    # k_tau_p: its span on the device clock (first workgroup start -> last workgroup end), which is what
-    # rocprofv3's dispatch durations measure; the HIP event pair (ordering kernel done -> tau kernel
-    # done) also holds the tau kernel's dispatch behind the ordering kernel and is reported beside it
+    mol = bool(getattr(prob, "n_molecules", 0))
+    tau_kernel = "k_tau_mol" if mol else ("k_tau_p" if tv in (3, 5) else "k_tau_w")
+    # k_tau_p in the pipelined loop: its span on the device clock (first workgroup start -> last workgroup end)
     tau_ms_events = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
     dev_ms = ms_runs[:, 3][np.isfinite(ms_runs[:, 3])] if len(ms_runs) else np.zeros(0)
-    tau_ms = float(np.mean(dev_ms)) if len(dev_ms) else tau_ms_events
-    tau_clock = "device clock" if len(dev_ms) else "hip events"
+    tau_ms_loop = float(np.mean(dev_ms)) if len(dev_ms) else tau_ms_events
 
-    # species the tau kernel integrates: variant = 10 * path + effective species (merged species: 1)
+    # per-kernel device durations, one run in flight (what rocprofv3 reports at PROM_PIPELINE=1)
+    kms = dev.transit_kernel_ms(args.kernel_runs)
     n_atoms = st["tau_kernel_variant"] % 10 or prob.n_atoms
     cle = st["chord_lambda_evals"]
     evals = st["exp_evals"]
-    # one sigma row per phase unless every phase has the same Doppler factor (prom_api.hip uniform_shift)
     same_shift = all(np.all(np.asarray(e["shift"]) == np.asarray(e["shift"])[0]) for e in host["scenarios"])
     sigma_rows = 1 if same_shift else n_orb
-    # fused: no sigma rows are read (the kernel looks the cross sections up in the tables itself)
-    tau_bytes = tau_bytes_per_launch(w1 - w0, n_orb, 0 if fused else n_atoms, sigma_rows) + (8 * (w1 - w0) if fused else 0)
-    achieved_gbs = tau_bytes / (tau_ms * 1e-3) / 1e9
-    flops_unit = flops_per_eval(n_atoms)
-    if tau_kernel == "k_tau_mol":
-        # SURVEY.md 8(d) molecular count: per chord-wavelength, n_x x (P lerp + 10^v + FMA) = 6 n_x flops,
-        # on top of the atomic exp evaluation
-        flops_unit += 6 * len(host["x"])
-    flops = evals * flops_unit
-    traffic = latest_profile_traffic("prom::" + tau_kernel, cfg_name)
+    n_w = w1 - w0
+    n_pr = len(host["y"])
+    n_x = len(host["x"])
+    merged = n_atoms == 1 and prob.n_atoms > 1
+    peak_meas, peak_src = measured_read_peak()
+
+    def hbm(nbytes, ms):
+        if not ms:
+            return None
+        a = nbytes / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
+                "frac_of_measured_read_peak": (a / peak_meas) if peak_meas else None, "algorithmic_bytes": nbytes}
+
+    kernels = {}
+    # tau kernel: R written, the resampled cross-section rows read (8 B per species row and wavelength)
+    tau_bytes = tau_bytes_per_launch(n_w, n_orb, 0 if fused else n_atoms, sigma_rows) + (8 * n_w if fused else 0)
+    flops_unit = flops_per_eval(n_atoms) + (6 * n_x if mol else 0)
+    tau_ms_iso = kms.get("tau")
+    kernels[tau_kernel] = dict(hbm(tau_bytes, tau_ms_iso) or {}, ms=tau_ms_iso, ms_pipelined_loop=tau_ms_loop,
+                               exp_evals=evals, exp_per_s=(evals / (tau_ms_iso * 1e-3)) if tau_ms_iso else None,
+                               valu_tflops=(evals * flops_unit / (tau_ms_iso * 1e-3) / 1e12) if tau_ms_iso else None)
+    if mol:
+        # SURVEY.md 8d rule (ii): per chord-wavelength n_x table lookups (P-lerp + 10^v + FMA) against the
+        # measured table-exp rate (profiles/r02u_fp64_exp_peak.json: 2.8e12/s)
+        pow10 = st["active_chords"] * n_w * n_x
+        kernels[tau_kernel].update(bound="fp64-exp", pow10_evals=pow10,
+                                   pow10_per_s=pow10 / (tau_ms_iso * 1e-3) if tau_ms_iso else None,
+                                   pow10_peak_per_s=2.815e12,
+                                   frac=(pow10 / (tau_ms_iso * 1e-3) / 2.815e12) if tau_ms_iso else None)
+    if kms.get("sigma"):
+        # Doppler sigma rows: one row per phase and wavelength (Y for merged species, else sigma per species)
+        # and their zero flags written, the wavelengths and the refined tables' nodes (x, log10 sigma) read
+        out_rows = 1 if merged else prob.n_atoms
+        nodes = table_nodes_in_range(tr, host, w0, w1)
+        sig_bytes = 8 * sigma_rows * out_rows * n_w + (sigma_rows * n_w if merged else 0) + 8 * n_w + 16 * nodes
+        lookups = sigma_rows * n_w * prob.n_atoms
+        kernels["k_sigma"] = dict(hbm(sig_bytes, kms["sigma"]), ms=kms["sigma"], lookups=lookups, table_nodes=nodes,
+                                  lookups_per_s=lookups / (kms["sigma"] * 1e-3))
+    if kms.get("columns"):
+        dens = n_orb * n_pr * n_x * len(host["scenarios"])
+        col_bytes = 8 * n_orb * n_pr * prob.n_atoms + 4 * n_orb * n_pr + 8 * (3 * n_pr + n_x)
+        kernels["k_columns"] = dict(hbm(col_bytes, kms["columns"]), bound="latency", ms=kms["columns"],
+                                    density_evals=dens, density_evals_per_s=dens / (kms["columns"] * 1e-3))
+    for k, name in (("order", "k_order"), ("windows", "k_windows")):
+        if kms.get(k):
+            kernels[name] = {"bound": "latency", "ms": kms[k],
+                             "workgroups": n_orb if k == "order" else None}
+    # path level: what any implementation must move -- R written, wavelengths and table nodes read -- over
+    # the measured step
+    path_bytes = 8 * n_orb * n_w + 8 * n_w + (16 * table_nodes_in_range(tr, host, w0, w1) if prob.n_atoms else 0)
+    path = hbm(path_bytes, ms_step)
+    # the dominant kernel of the step (longest device duration) carries the top-level roofline
+    dom = max(kernels, key=lambda k: kernels[k].get("ms") or 0.0)
+    dk = kernels[dom]
+    traffic = latest_profile_traffic("prom::" + dom, cfg_name)
     # latency of one run alone on an idle device (host clock: submit, kernels, synchronize; no stats
     # instrumentation), median of 20 -- what one retrieval sample waits for with inputs resident; not `value`
+    dev.transit_set(prob)
+    dev.transit_run()
+    dev.synchronize()
     lat = []
     for _ in range(20):
         t_l = time.perf_counter()
@@ -308,7 +444,7 @@ def main():
     # end-to-end (host prep + H2D + run + D2H) for reference: median of 7 sumOverChords calls after one
     # warm-up call (first-call costs: pinned pool, host threads, page faults)
     R, e2e_s = None, None
-    if world == 1:
+    if world == 1 and not args.shard:
         R = tr.sumOverChords(devices=[dev_id])
         calls = []
         for _ in range(7):
@@ -317,6 +453,14 @@ def main():
             R = tr.sumOverChords(devices=[dev_id])
             calls.append(time.perf_counter() - t_e2e)
         e2e_s = float(np.median(calls))
+    proj = None
+    if world == 1 and not args.shard and not args.no_projection:
+        del tr
+        proj = strong_projection(dev_id)
+    workload = "%s (%s), %d wavelengths x %d phases x %d chords x %d samples" % (
+        cfg_name, describe(cfg), n_wav_global, n_orb, n_pr, n_x)
+    if args.shard:
+        workload += ", shard %s: wavelengths [%d, %d)" % (args.shard, w0, w1)
     result = {
         "metric": "spectrum points/sec (phase x wavelength)",
         "value": value,
@@ -326,35 +470,34 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (WASP-49b catalogue system, NIST line list bundled from the reference)",
-        "config": {"workload": "%s (%s), %d wavelengths x %d phases x %d chords x %d samples"
-                               % (cfg_name, describe(cfg), n_wav_global, n_orb, len(host["y"]), len(host["x"])),
+        "config": {"workload": workload,
                    "global_wavelengths": n_wav_global, "orbital_phases": n_orb,
-                   "chords_per_phase": len(host["y"]), "los_samples": len(host["x"]),
+                   "chords_per_phase": n_pr, "los_samples": n_x,
                    "parallelism": "wavelength shards x%d (no collective)" % world},
-        "roofline": {"bound": "hbm", "kernel": tau_kernel, "achieved": achieved_gbs,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic, "algorithmic_bytes": tau_bytes, "sigma_rows": sigma_rows,
-                     "tau_ms": tau_ms,
-                     "tau_ms_source": tau_clock, "tau_ms_hip_events": tau_ms_events,
-                     "tau_ms_sampled_runs": int(len(ms_runs)),
-                     "fused_sigma": fused,
-                     "sigma_lookups": (n_orb * (w1 - w0) * prob.n_atoms) if fused else 0,
-                     "exp_evals": evals, "chord_lambda_evals": cle,
-                     "valu": {"flops": flops, "flops_per_exp_eval": flops_unit,
-                              "achieved_tflops": flops / (tau_ms * 1e-3) / 1e12,
-                              "peak_tflops": FP64_VALU_PEAK_TFLOPS}},
+        "roofline": {"bound": dk.get("bound", "hbm"), "kernel": dom, "achieved": dk.get("achieved"),
+                     "peak": dk.get("peak", HBM_PEAK_GBS), "unit": dk.get("unit", "GB/s"), "frac": dk.get("frac"),
+                     "traffic": traffic, "algorithmic_bytes": dk.get("algorithmic_bytes"),
+                     "kernel_ms": dk.get("ms"), "kernel_ms_source": "prom_transit_kernel_ms: one run in flight, "
+                     "dispatch-packet events, mean of %d runs" % args.kernel_runs,
+                     "measured_read_peak_gbs": peak_meas, "measured_read_peak_source": peak_src,
+                     "sigma_rows": sigma_rows,
+                     "kernels": kernels, "path": dict(path or {}, ms_per_step=ms_step),
+                     "tau_ms_pipelined_loop": tau_ms_loop, "tau_ms_hip_events": tau_ms_events,
+                     "chord_lambda_evals": cle, "fused_sigma": fused},
         "stage_ms_single_run": {"columns_order": st["ms_density"], "tau": st["ms_tau"], "total": st["ms_total"]},
         "single_run_ms": single_run_ms,
         "chords": {"active": st["active_chords"], "transparent": st["transparent_chords"],
                    "blocked": st["blocked_chords"], "integrated_records": st["tau_records"]},
         "setup_s": setup_s,
-        "end_to_end_s": e2e_s if R is not None else None,
-        "end_to_end_points_per_s": (n_wav_global * n_orb / e2e_s) if R is not None else None,
+        "end_to_end_s": e2e_s,
+        "end_to_end_points_per_s": (n_wav_global * n_orb / e2e_s) if e2e_s else None,
     }
+    if proj is not None:
+        result["strong_scaling_projection"] = proj
     if cpu is not None:
         result["cpu_baseline"] = cpu
     if dist:

@@ -246,6 +246,21 @@ int32_t prom_transit_columns(prom_ctx* ctx, double* N_out);
 int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bounds, double* sum_out,
                                 int64_t* count_out, double* max_out);
 
+/* Per-kernel device durations of the transit path (ABI 5): n_runs runs of the current problem, one at a
+ * time (one slot, no second stream; the stream waits after every run), each kernel timed by start/stop
+ * events on its own dispatch packet (groups of kernels: the first start to the last stop).  ms_out[k] is
+ * the mean duration in milliseconds of kernel k (prom_kernel_id), NaN when the path does not launch it.
+ * What rocprofv3 --kernel-trace reports for one slot in flight; measurement aid for bench.py. */
+enum prom_kernel_id {
+  PROM_K_COLUMNS = 0,   /* column densities + culling: k_columns8 (k_ntot + k_mol_prep + k_columns)   */
+  PROM_K_SIGMA = 1,     /* Doppler cross-section rows: k_sigma_poly / k_sigma_rows                     */
+  PROM_K_ORDER = 2,     /* per-phase ordering and windows: k_order (k_chords)                          */
+  PROM_K_WINDOWS = 3,   /* tile windows and heavy-entry lists: k_windows                               */
+  PROM_K_TAU = 4,       /* the fused tau kernel: k_tau_p / k_tau_w / k_tau / k_tau_mol / k_tau_rm      */
+  PROM_K_COUNT = 5
+};
+int32_t prom_transit_kernel_ms(prom_ctx* ctx, int32_t n_runs, double* ms_out);
+
 /* Disk-integrated stellar flux of a rotating star (ABI 5).  Replaces the rotating branch of
  * Star.getFstarIntegrated (celestialBodies.py:299-311, through calculateRM :226-240 and calculateCLV
  * :212-224): for every wavelength, the n_cells disk cells in the reference's loop order (phi outer, rho

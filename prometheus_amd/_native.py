@@ -110,6 +110,7 @@ SIGNATURES = {
     "prom_transit_result": (C.c_int32, [C.c_void_p, _dp]),
     "prom_transit_columns": (C.c_int32, [C.c_void_p, _dp]),
     "prom_transit_band_stats": (C.c_int32, [C.c_void_p, C.c_int32, _dp, _dp, C.POINTER(C.c_int64), _dp]),
+    "prom_transit_kernel_ms": (C.c_int32, [C.c_void_p, C.c_int32, _dp]),
     "prom_star_disk_flux": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, _dp, _dp, _dp, C.c_double, C.c_double,
                                         C.c_int64, _dp, _dp]),
     "prom_timing_begin": (C.c_int32, [C.c_void_p]),
@@ -381,6 +382,15 @@ class Device:
         n = C.c_int32(0)
         self._check(self.lib.prom_timing_end(self.h, max_runs, _d(ms), C.byref(n)), "prom_timing_end")
         return ms[:min(int(n.value), max_runs)]
+
+    KERNEL_IDS = ("columns", "sigma", "order", "windows", "tau")   # prom_kernel_id order
+
+    def transit_kernel_ms(self, n_runs: int = 20) -> dict:
+        """prom_transit_kernel_ms: mean device duration [ms] of each kernel of the current problem over
+        n_runs serialized runs (one slot; dispatch-packet events), None for kernels the path does not launch."""
+        ms = np.empty(len(self.KERNEL_IDS))
+        self._check(self.lib.prom_transit_kernel_ms(self.h, int(n_runs), _d(ms)), "prom_transit_kernel_ms")
+        return {k: (float(v) if np.isfinite(v) else None) for k, v in zip(self.KERNEL_IDS, ms)}
 
     def transit_columns(self) -> np.ndarray:
         out = np.empty((self._n_atoms, self._shape[0], self._n_pr))

@@ -32,9 +32,11 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(os.path.join(HERE, f)) <= t for f in SOURCES + HEADERS + ["build.py"])
 
 
-def build(force: bool = False, verbose: bool = False, extra=(), out: str = OUT, objdir: str = OBJDIR) -> str:
+def build(force: bool = False, verbose: bool = False, extra=(), out: str = OUT, objdir: str = OBJDIR,
+          only=None) -> str:
     """One object per translation unit, compiled in parallel, then linked into the shared library
-    (``extra``/``out``/``objdir``: variant builds such as the -DPROM_TRACE library of tools/trace_kernels.py)."""
+    (``extra``/``out``/``objdir``: variant builds such as the -DPROM_TRACE library of tools/trace_kernels.py;
+    ``only``: compile just these sources with ``extra`` and link them with the default build's other objects)."""
     if not force and out == OUT and up_to_date() and not extra:
         return OUT
     from concurrent.futures import ThreadPoolExecutor
@@ -42,6 +44,8 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = OUT, 
     cc = hipcc()
 
     def compile_one(src: str) -> str:
+        if only is not None and src not in only:
+            return os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
         obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
         cmd = [cc] + FLAGS + list(extra) + ["-c", os.path.join(HERE, src), "-o", obj]
         if verbose:

@@ -1,6 +1,7 @@
 // C-ABI layer of libprom_hip.so (declared in include/prom_hip.h).  Host code only: argument checks,
 // device memory owned by the context, H2D/D2H copies and kernel launches on the context's stream.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -315,7 +316,11 @@ static void build_directory(prom_ctx* ctx, prom::AtomTable& t, const double* x, 
   }
   upload(t.dir, d.data(), nd + 1, ctx->stream);
   t.rec.ensure(sizeof(double4) * n);
-  prom::launch_table_recs(ctx->stream, t.x.as<double>(), t.y.as<double>(), n, t.rec.as<double4>());
+  ctx->scratch[5].ensure(sizeof(double) * std::max<int64_t>(n, 1));
+  ctx->scratch[4].ensure(sizeof(double) * 1024);
+  prom::launch_table_recs(ctx->stream, t.x.as<double>(), t.y.as<double>(), n, t.rec.as<double4>(),
+                          ctx->scratch[5].as<double>());
+  t.amax = prom::reduce_max(ctx->stream, ctx->scratch[5].as<double>(), n, ctx->scratch[4].as<double>());
   t.hx.assign(x, x + n);
   t.n_dir = (int32_t)nd;
   t.dir_x0 = x0;
@@ -854,9 +859,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
             // bracket are monotone step functions, and the bracket is constant inside an interval)
             const double xs = X[lo], span = X[hi] - X[lo];
             const double inv = span > 0.0 ? (double)(m - 1) / span : 0.0;
-            bool lin = span > 0.0 && std::isfinite(inv);
+            const double b0 = -(xs * inv);
+            bool lin = span > 0.0 && std::isfinite(inv) && std::isfinite(b0);
             auto guess = [&](double v) -> int64_t {
-              const double f = (v - xs) * inv;
+              const double f = std::fma(v, inv, b0);   // the device's seg_guess
               int64_t g = f < 0.0 ? 0 : (f >= (double)(m - 2) ? m - 2 : (int64_t)f);
               return g;
             };
@@ -870,7 +876,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
             }
             if (lin) {
               e.kind = m <= prom::kSigSeg ? 1 : 2;
-              e.xs = xs;
+              e.xs = b0;
               e.inv = inv;
             }
           }
@@ -899,6 +905,27 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         seg_key_new = true;
         new_key_sh = std::move(key_sh);
         new_key_gen = std::move(key_gen);
+      }
+    }
+    // polynomial sigma rows: the smallest even degree D with amax^(D+1)/(D+1)! <= 2^-53 over the problem's
+    // atomic tables (AtomTable::amax bounds |ln10 slope| h on every interval); 0 (exp10 rows) when a table
+    // has non-finite values or |a| is too large for D <= 14
+    tr.sig_deg = 0;
+    {
+      const char* e = std::getenv("PROM_SIG_POLY");
+      bool fin = !(e && std::atoi(e) == 0);
+      double am = 0.0;
+      for (const auto& t : tr.terms) {
+        if (t.is_molecule) continue;
+        const double a = ctx->tables[t.table].amax;
+        if (!(a == a)) fin = false;
+        else am = std::max(am, a);
+      }
+      am *= 1.0 + 1e-6;
+      for (int D = 4; fin && D <= 14; D += 2) {
+        double term = 1.0;   // am^(D+1) / (D+1)!
+        for (int i = 1; i <= D + 1; ++i) term *= am / (double)i;
+        if (term <= std::ldexp(1.0, -53)) { tr.sig_deg = D; break; }
       }
     }
     tr.star = pb->has_star != 0;
@@ -1029,6 +1056,24 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     }
     tr.last = 0;
     stg.flush(ctx, s);
+    if (seg_key_new) {
+      // segments built by this call: mark those whose guess is numpy's bracket for every target
+      const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
+      tr.sig_flags.ensure(sizeof(int32_t) * nb * n_atoms);
+      prom::launch_seg_exact(s, n_atoms, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, (int32_t)n_orb,
+                             tr.sig_seg.as<prom::SigSeg>(), tr.sig_flags.as<int32_t>());
+      if (std::getenv("PROM_DEBUG")) {
+        std::vector<prom::SigSeg> hs(nb * n_atoms);
+        PROM_HIP(hipMemcpyAsync(hs.data(), tr.sig_seg.p, sizeof(prom::SigSeg) * hs.size(), hipMemcpyDeviceToHost, s));
+        PROM_HIP(hipStreamSynchronize(s));
+        int64_t cnt[8] = {};
+        for (const auto& e : hs) ++cnt[e.kind & 7];
+        std::fprintf(stderr, "[prom] sigma segments: %lld blocks x %d species, %d oversize blocks, kinds: none %lld, lds %lld, "
+                     "global %lld, lds exact %lld, global exact %lld; poly degree %d\n", (long long)nb, n_atoms,
+                     tr.n_sig_fb, (long long)cnt[0], (long long)cnt[1], (long long)cnt[2], (long long)cnt[5],
+                     (long long)cnt[6], tr.sig_deg);
+      }
+    }
     PROM_HIP(hipStreamSynchronize(s));
     if (seg_key_new) {
       tr.seg_key_wav.assign(pb->wavelength, pb->wavelength + tr.n_wav);
@@ -1153,6 +1198,49 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
       stats->exp_evals = counted + unwindowed * tr.n_wav;
       stats->tau_kernel_variant = variant;
     }
+  });
+}
+
+int32_t prom_transit_kernel_ms(prom_ctx* ctx, int32_t n_runs, double* ms_out) {
+  return guarded(ctx, [&] {
+    prom::TransitDev& tr = ctx->tr;
+    if (!tr.ready) throw Error(PROM_E_STATE, "prom_transit_kernel_ms: call prom_transit_set first");
+    PROM_REQUIRE(n_runs >= 1 && ms_out, "prom_transit_kernel_ms: bad arguments");
+    for (auto st : ctx->streams) PROM_HIP(hipStreamSynchronize(st));
+    std::vector<hipEvent_t> ev(2 * PROM_K_COUNT);
+    for (auto& e : ev) PROM_HIP(hipEventCreate(&e));
+    std::vector<double> sum(PROM_K_COUNT, 0.0);
+    std::vector<int32_t> cnt(PROM_K_COUNT, 0);
+    const hipStream_t st = ctx->streams[0];
+    prom::RunSlot& rs = tr.slot[0];
+    rs.aux = nullptr;
+    rs.ev_fork = rs.ev_join = nullptr;
+    rs.sig_late = false;
+    int variant = 0;
+    try {
+      for (int32_t r = 0; r < n_runs; ++r) {
+        tr.kprof = ev.data();
+        tr.kprof_mask = 0;
+        prom::launch_transit(st, tr, rs, ctx->tables, ctx->mtables, nullptr, &variant, false);
+        tr.kprof = nullptr;
+        PROM_HIP(hipStreamSynchronize(st));
+        for (int k = 0; k < PROM_K_COUNT; ++k) {
+          if (!(tr.kprof_mask & (1u << k))) continue;
+          float ms = 0.0f;
+          PROM_HIP(hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]));
+          sum[k] += ms;
+          ++cnt[k];
+        }
+      }
+    } catch (...) {
+      tr.kprof = nullptr;
+      for (auto e : ev) (void)hipEventDestroy(e);
+      throw;
+    }
+    for (auto e : ev) PROM_HIP(hipEventDestroy(e));
+    tr.last = 0;
+    tr.ran = true;
+    for (int k = 0; k < PROM_K_COUNT; ++k) ms_out[k] = cnt[k] ? sum[k] / cnt[k] : std::nan("");
   });
 }
 

@@ -151,17 +151,19 @@ __device__ __forceinline__ double interp_guess(double t, int32_t g, XF X2, RF RE
   return rv;
 }
 
-__device__ __forceinline__ int32_t seg_guess(double t, double xs, double inv, int32_t m) {
-  // = (f < 0 ? 0 : f >= m - 2 ? m - 2 : (int)f), the host's verified map (NaN t never reaches here)
-  const double f = (t - xs) * inv;
-  return (int32_t)__builtin_fmin(__builtin_fmax(f, 0.0), (double)(m - 2));
+__device__ __forceinline__ int32_t seg_guess(double t, double b, double inv, int32_t m) {
+  // f = fma(t, inv, b) (b = -x_lo inv), g = (f < 0 ? 0 : f >= m - 2 ? m - 2 : (int)f): the host's verified
+  // map (prom_api.hip sigma segments).  Every target lies in the slice, so f is within rounding of
+  // [0, m - 1] and truncating first, clamping the integer after, gives the same g
+  const int32_t g = (int32_t)__builtin_fma(t, inv, b);
+  return g < 0 ? 0 : (g > m - 2 ? m - 2 : g);
 }
 
 // sigma_s(t) for the fused Doppler path (no sigma rows in HBM): the verified linear guess of the target's
 // 256-wavelength block (SigSeg, kind > 0) and two dependent reads of the global x / f arrays (numpy's slope
 // divided here), else the directory lookup.  Bit for bit the value k_sigma_rows would have stored.
 __device__ __forceinline__ double sigma_seg(double t, const SigTabDev& tb, const SigSeg& sg) {
-  if (sg.kind > 0) {
+  if ((sg.kind & 3) > 0) {
     const double* __restrict__ gx = tb.x + sg.lo;
     const double* __restrict__ gy = tb.y + sg.lo;
     const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);

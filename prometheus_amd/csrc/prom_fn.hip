@@ -124,15 +124,30 @@ void launch_gridded(hipStream_t s, const double* g, int32_t nx, int32_t ny, int3
 }
 
 // ------------------------------------------------------------------ interval records
-// rec[i] = {x_i, y_i, numpy.interp's slope of [x_i, x_{i+1}], 0}: the Doppler-row lookups read a bracket's
-// node and slope in one 32-byte record (the same IEEE division as sigma_of's)
+// rec[i] = {x_i, E_i = 10^y_i, L_i = ln10 slope_i, x_{i+1}} with numpy.interp's slope of [x_i, x_{i+1}] (the
+// same IEEE division as sigma_of's): on [x_i, x_{i+1}) numpy's 10^(y_i + slope_i (t - x_i)) is E_i e^a with
+// a = L_i (t - x_i), which the polynomial sigma rows evaluate (k_sigma_poly).  The last node has L = 0 and
+// x_{i+1} = +inf.  amax[i] = |L_i| (x_{i+1} - x_i), the largest |a| on the interval (0 for an empty one;
+// NaN when y_i or y_{i+1} is not finite, which keeps such tables on the exp10 path).
 __global__ void k_table_recs(const double* __restrict__ x, const double* __restrict__ y, int64_t n,
-                             double4* __restrict__ rec) {
+                             double4* __restrict__ rec, double* __restrict__ amax) {
   const int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x;
   if (i >= n) return;
   const double xv = x[i], yv = y[i];
-  const double sl = i + 1 < n ? (y[i + 1] - yv) / (x[i + 1] - xv) : 0.0;
-  rec[i] = make_double4(xv, yv, sl, 0.0);
+  double sl = 0.0, xn = __builtin_inf(), am = 0.0;
+  if (i + 1 < n) {
+    xn = x[i + 1];
+    const double yn = y[i + 1];
+    if (xn > xv) {
+      sl = (yn - yv) / (xn - xv);
+      am = fabs(sl * 2.302585092994046) * (xn - xv);
+    }
+    if (!__builtin_isfinite(yv) || !__builtin_isfinite(yn)) am = __builtin_nan("");
+  } else if (!__builtin_isfinite(yv)) {
+    am = __builtin_nan("");
+  }
+  rec[i] = make_double4(xv, exp10(yv), sl * 2.302585092994046, xn);
+  if (amax) amax[i] = am;
 }
 
 // prom_transit_set's small inputs arrive in one DMA (descriptors + data, prom_api.hip Stager); a workgroup
@@ -157,9 +172,10 @@ void launch_scatter(hipStream_t s, const char* base, const ScatterDesc* d, int32
   PROM_HIP(hipGetLastError());
 }
 
-void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec) {
+void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec, double* amax) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_table_recs, dim3(grid_for(n, kBlock, (int64_t)1 << 31)), dim3(kBlock), 0, s, x, y, n, rec);
+  hipLaunchKernelGGL(k_table_recs, dim3(grid_for(n, kBlock, (int64_t)1 << 31)), dim3(kBlock), 0, s, x, y, n, rec,
+                     amax);
   PROM_HIP(hipGetLastError());
 }
 

@@ -140,9 +140,10 @@ struct ScatterDesc {
 
 // Per 256-wavelength block and atomic slot of a Doppler-row problem (prom_api.hip sigma segments): the
 // table nodes [lo, lo + m) every row's targets fall between, and, for kind > 0, a linear bracket guess
-// g(t) = clamp((int)((t - xs) * inv), 0, m - 2) that the host verified to be within one node of numpy's
-// bracket for every target in the slice.  kind 0: no guess (general lookup); 1: the slice fits in LDS;
-// 2: too large for LDS, the guess indexes the global records.
+// g(t) = clamp((int)fma(t, inv, xs), 0, m - 2) (xs holds -x_lo inv) that the host verified to be within one node of numpy's
+// bracket for every target in the slice.  kind & 3: 0 no guess (general lookup); 1 the slice fits in LDS;
+// 2 too large for LDS, the guess indexes the global records.  kind & 4 (k_seg_exact, at prom_transit_set):
+// the guess IS numpy's bracket for every target of the block's rows (one record read, no compares).
 struct SigSeg {
   int32_t lo, m, kind, pad;
   double xs, inv;
@@ -186,7 +187,8 @@ struct AtomTable {
   // bucket directory for O(1) bracketing: dir[j] = #{i : x[i] <= x0 + j h}, j = 0 .. n_dir,
   // h = (x[n-1] - x0) / n_dir (prom_api.hip build_directory)
   DevBuf dir;
-  DevBuf rec;               // [n] double4 {x, y, slope, 0} (k_table_recs)
+  DevBuf rec;               // [n] double4 {x_i, 10^y_i, ln10 slope_i, x_{i+1}} (k_table_recs)
+  double amax = 0.0;        // max over intervals of |ln10 slope_i| (x_{i+1} - x_i) (NaN: non-finite y)
   std::vector<double> hx;   // host copy of x (stellar-spectrum slice bounds)
   int32_t n_dir = 0;
   double dir_x0 = 0.0, dir_inv_h = 0.0;
@@ -288,6 +290,9 @@ struct TransitDev {
   unsigned long long* ts_out = nullptr;
   int32_t ts_cap = 0;
   int32_t ts_blocks = 0;
+  // prom_transit_kernel_ms: start/stop events per kernel id (null: not profiling) and the ids launched
+  hipEvent_t* kprof = nullptr;
+  uint32_t kprof_mask = 0;
   DevBuf molslot;                           // [n_mol] MolSlotDev
   DevBuf mol_ip;                            // [n_mol][n_orb][n_pr][n_x] int32 P bracket (-1: out of table)
   DevBuf mol_wp;                            // [n_mol][n_orb][n_pr][n_x] P weight
@@ -307,6 +312,10 @@ struct TransitDev {
   DevBuf sig_fb;                            // blocks with an oversize slice (m = 0 for some species)
   int32_t n_sig_fb = 0;
   bool sig_seg_ok = false;
+  // polynomial sigma rows (k_sigma_poly): degree D of the e^a Taylor polynomial for this problem's tables
+  // (0: the exp10 path, k_sigma_rows; PROM_SIG_POLY=0 forces it)
+  int32_t sig_deg = 0;
+  DevBuf sig_flags;                         // [n_wav blocks][n_atoms] int32 (k_seg_exact)
   // inputs the sigma segments were built from (wavelengths, per-slot table generation and Doppler factors):
   // a later problem with the same ones reuses sig_seg / sig_fb instead of rebuilding them
   std::vector<double> seg_key_wav, seg_key_sh;
@@ -372,7 +381,14 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 // orbital Doppler shift: the per-phase cross-section rows, Y or sigma_s, and the Q ranges (prom_sigma.hip)
 void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                        int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
-                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start);
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop);
+// the same rows with e^a polynomials over the tables' {x, 10^y, ln10 slope, x_next} records (prom_sigma.hip)
+void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4& tabv, const double* wav, int64_t n_wav,
+                       int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop);
+// prom_transit_set: mark the sigma segments whose guess is numpy's bracket for every target (kind |= 4)
+void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
+                      int32_t n_rows, SigSeg* seg, int32_t* flags);
 // fused Doppler path: half-tile Q bounds from the table nodes instead of the sigma rows (prom_sigma.hip)
 void launch_qbounds(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav, int32_t n_rows,
                     const SigSeg* seg, float4* tq, int32_t merge_sp, double nscale_m);
@@ -383,8 +399,8 @@ double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev
 // prom_gridded_density (prom_fn.hip)
 void launch_gridded(hipStream_t s, const double* g, int32_t nx, int32_t ny, int32_t nz, int64_t n,
                     const double* px, const double* py, const double* pz, double* out);
-// AtomTable::rec from a table's x and y (prom_fn.hip)
-void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec);
+// AtomTable::rec from a table's x and y, and the per-interval |a| bounds (prom_fn.hip)
+void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec, double* amax);
 void launch_scatter(hipStream_t s, const char* base, const ScatterDesc* d, int32_t n);
 // per phase: sum / count of R over the band-selected wavelengths, max of R over all (prom_transit_band_stats)
 void launch_band_stats(hipStream_t s, const double* R, const double* wav, int32_t n_orb, int64_t n_wav,

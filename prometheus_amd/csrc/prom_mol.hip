@@ -150,8 +150,15 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
     for (const auto& m : tr.mslots) max_np = std::max(max_np, m.n_p);
     const size_t lds = PROM_EXP2_TABLE_N * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
     PROM_REQUIRE(lds <= 160 * 1024, "transit: molecular tables too large for the LDS staging (n_mol * n_p)");
+    // prom_transit_kernel_ms: the kernel's own dispatch-packet events
+    hipEvent_t kps = nullptr, kpe = nullptr;
+    if (tr.kprof) {
+      tr.kprof_mask |= 1u << PROM_K_TAU;
+      kps = tr.kprof[2 * PROM_K_TAU];
+      kpe = tr.kprof[2 * PROM_K_TAU + 1];
+    }
 #define PROM_TAUM(NSV, EK)                                                                                  \
-  hipLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
+  hipExtLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, kps, kpe, 0, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
                      max_np, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x,         \
                      tr.delta_x, tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(), R)
 #define PROM_TAUM_NS(EK)                \

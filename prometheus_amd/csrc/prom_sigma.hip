@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_rows(const SigTa
       for (int r = 0; r < kSigFbRows; ++r) {
         const int32_t orow = f0 + r < n_rows ? f0 + r : n_rows - 1;
         const double t = tb.shift[orow] * lam;
-        if (sg.kind > 0) {
+        if ((sg.kind & 3) > 0) {
           // the x and f arrays (16 bytes per lane and array: the high-resolution slices are sparse in the
           // targets, so bytes per lane decide), the slope divided here as numpy does
           const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_rows(const SigTa
   if (wb >= n_blk) return;
   bool lds_ok = true;
 #pragma unroll
-  for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && seg[wb * NSIG + s].kind == 1;
+  for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
   if (!lds_ok) return;   // its rows are the trailing workgroups'
   const int64_t w = wb * kBlock + tid;
   const bool live = w < n_wav;
@@ -227,6 +227,370 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_rows(const SigTa
 }
 
 
+// ---- polynomial sigma rows (prom_transit_set: sig_deg > 0) ---------------------------------------------
+// On numpy's bracket [x_k, x_{k+1}) of a target t,
+//   sigma_s(t) = 10^(f_k + slope_k (t - x_k)) - offset = E_k e^a - offset,   a = L_k (t - x_k),
+// with E_k = 10^f_k and L_k = ln10 slope_k kept per node (AtomTable::rec, k_table_recs).  e^a is a degree-D
+// Taylor polynomial: the tables bound |a| on every interval by amax (AtomTable::amax) and prom_transit_set
+// takes the smallest even D with amax^(D+1)/(D+1)! <= 2^-53, so the truncation is below one rounding of e^a.
+// Against numpy's 10^v (v rounded once) sigma moves by ~|v| ln10 2^-53 (about 1e-14 relative); at an exact
+// node hit a = 0 and sigma is 10^f_k - offset as numpy's node rule gives it, and a flat interval at the
+// table floor (10^-50) gives exactly 0, so the exact path's zero pattern is kept.  No exp10, no division:
+// about 10 + D FP64 operations per lookup against ~33 on the exp10 path.
+struct InvFact {
+  double v[16];
+  constexpr InvFact() : v{} {
+    double f = 1.0;
+    v[0] = 1.0;
+    for (int i = 1; i < 16; ++i) {
+      f *= (double)i;
+      v[i] = 1.0 / f;
+    }
+  }
+};
+
+// the coefficients travel as a kernel argument (scalar registers: each FMA takes its addend from an SGPR
+// pair; as compile-time constants the compiler re-materialises both halves into VGPRs before every use)
+struct PolyCoef {
+  double c[16];
+};
+
+template <int D>
+__device__ __forceinline__ double exp_taylor(double a, const PolyCoef& pc) {
+  double p = pc.c[D];
+#pragma unroll
+  for (int k = D - 1; k >= 0; --k) p = __builtin_fma(p, a, pc.c[k]);
+  return p;
+}
+
+#ifndef PROM_SIG_POLY_ROWS
+#define PROM_SIG_POLY_ROWS 0
+#endif
+constexpr int kSigPolyRows = PROM_SIG_POLY_ROWS;   // rows (phases) per workgroup of k_sigma_poly (4 or 8; 0: per problem)
+// main workgroups' table access: 0 one species' slice in LDS at a time; 1 every species' slice staged at once;
+// 2 no LDS, records read from the global table
+#ifndef PROM_SIG_MODE
+#define PROM_SIG_MODE 0
+#endif
+constexpr int kSigMode = PROM_SIG_MODE;
+
+// Workgroups [0, n_main): one per (256-wavelength block whose slices all fit in LDS, chunk of 16 rows).  Per
+// species the block's records {x_k, x_{k+1}} and {E_k, L_k} go to LDS; kind & 4 (the guess is numpy's
+// bracket for every target, k_seg_exact): one LDS round trip per lookup, else the +-1 bracket test and a
+// second one.  The rows accumulate Y (merged species) or their Q sum in registers, species after species.
+// Workgroups [n_main, ...): one per (other block, row), records read from the global table (one 32-byte
+// record, a second only for lanes whose bracket is the guess +- 1), or sigma_of without a guess.
+template <int NSIG, int D, bool MG, int R>
+__global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, const PolyCoef pc,
+                                                       const double* __restrict__ wav, int64_t n_wav,
+                                                       int32_t n_rows, const SigSeg* __restrict__ seg,
+                                                       const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
+                                                       int32_t n_rc, double* __restrict__ sig, float4* __restrict__ tq,
+                                                       int32_t merge_sp, double nscale_m, uint8_t* __restrict__ zfl,
+                                                       int32_t parts) {
+  static_assert(R == 4 || R == 8 || R == 16, "4, 8 or 16 rows per workgroup");
+  // per staged species: [0, kSigSeg) {x_k, x_{k+1}}, [kSigSeg, 2 kSigSeg) {E_k, L_k}
+  __shared__ double2 slds[2 * kSigSeg * (kSigMode == 1 ? NSIG : 1)];
+  double2* sxr = slds;
+  double2* sel = slds + kSigSeg;
+  const int tid = threadIdx.x;
+  const int64_t n_halves = 2 * ((n_wav + kTW - 1) / kTW);
+  const int32_t nse = MG ? 1 : NSIG;
+  // one workgroup per (256-wavelength block, chunk of R rows), XCD-aware: the row chunks of a block are 8
+  // workgroups apart (one XCD's L2 for its slices)
+  const int64_t bid = blockIdx.x;
+  const int64_t grp = bid / (8 * n_rc), rem = bid % (8 * n_rc);
+  const int64_t wb = grp * 8 + rem % 8;
+  const int32_t r0 = (int32_t)(rem / 8) * R;
+  if (wb >= n_blk) return;
+  bool lds_ok = true;
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
+  // PROM_SIG_PARTS (profiling only): 1 = LDS blocks, 2 = global-record blocks
+  if (!(parts & (lds_ok ? 1 : 2))) return;
+  const int64_t w = wb * kBlock + tid;
+  const bool live = w < n_wav;
+  const double lam = wav[live ? w : n_wav - 1];
+  double acc[R];        // merged: Y = sum_s chi_s sigma_s;  else: Q = sum_s max(sigma_s / c_s, 0)
+  uint32_t zb = 0;      // merged: bit r set when some chi_s sigma_s is not > 0
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0;
+  constexpr int kPre = kSigSeg / kBlock;   // mode 3: records per thread and species (slices <= kSigSeg nodes)
+  double4 pre[kPre];
+  auto fetch = [&](int s) {
+    const SigSeg sg = seg[wb * NSIG + s];
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int32_t i = tid + j * kBlock;
+      pre[j] = i < sg.m ? tabv.t[s].rec[sg.lo + i] : make_double4(0.0, 0.0, 0.0, 0.0);
+    }
+  };
+  if (kSigMode == 3 && lds_ok) fetch(0);
+  if (kSigMode == 1 && lds_ok) {
+    // every species' slice staged at once (one global round trip; NSIG x 16 KB of LDS)
+#pragma unroll
+    for (int s = 0; s < NSIG; ++s) {
+      const SigSeg sg = seg[wb * NSIG + s];
+      for (int32_t i = tid; i < sg.m; i += kBlock) {
+        const double4 q = tabv.t[s].rec[sg.lo + i];
+        slds[s * 2 * kSigSeg + i] = make_double2(q.x, q.w);
+        slds[s * 2 * kSigSeg + kSigSeg + i] = make_double2(q.y, q.z);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) {
+    const SigTabDev& tb = tabv.t[s];
+    const SigSeg sg = seg[wb * NSIG + s];
+    const double2* __restrict__ sx_ = kSigMode == 1 ? slds + s * 2 * kSigSeg : sxr;
+    const double2* __restrict__ se_ = kSigMode == 1 ? slds + s * 2 * kSigSeg + kSigSeg : sel;
+    if (kSigMode == 0 && lds_ok) {
+      if (s > 0) __syncthreads();   // the previous species' slice is no longer read
+      for (int32_t i = tid; i < sg.m; i += kBlock) {
+        const double4 q = tb.rec[sg.lo + i];
+        sxr[i] = make_double2(q.x, q.w);
+        sel[i] = make_double2(q.y, q.z);
+      }
+      __syncthreads();
+    } else if (kSigMode == 3 && lds_ok) {
+      // this species' records were fetched into registers while the previous species computed; the next
+      // species' go out now and land during this one's lookups
+      if (s > 0) __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kPre; ++j) {
+        const int32_t i = tid + j * kBlock;
+        if (i < sg.m) {
+          sxr[i] = make_double2(pre[j].x, pre[j].w);
+          sel[i] = make_double2(pre[j].y, pre[j].z);
+        }
+      }
+      __syncthreads();
+      if (s + 1 < NSIG) fetch(s + 1);
+    }
+    const bool exact = (sg.kind & 4) != 0;
+    const double off = tb.offset, chi = tb.chi, nsc = tb.nscale;
+    auto emit = [&](int r, double v) {
+      const int32_t orow = r0 + r;
+      if constexpr (MG) {
+        const double cv = chi * v;
+        if (!(cv > 0.0)) zb |= 1u << r;
+        acc[r] += cv;
+      } else {
+        if (live && orow < n_rows) sig[((int64_t)orow * nse + s) * n_wav + w] = v;
+        const double qs = v * nsc;
+        acc[r] += qs > 0.0 ? qs : 0.0;
+      }
+    };
+    // the rows' targets first (scalar loads of the Doppler factors, one wait), so that the lookups' LDS reads
+    // are not serialised behind them (lgkmcnt counts scalar loads and LDS reads together)
+    double tt[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) tt[r] = tb.shift[r0 + r < n_rows ? r0 + r : n_rows - 1] * lam;
+    if (kSigMode == 2 || !lds_ok) {
+      // blocks with a slice too large for LDS (the high-resolution line windows, or a wide spread of Doppler
+      // factors): the records straight from the global table (L1 / L2), one 32-byte record per lookup (a second
+      // only for lanes whose bracket is the guess +- 1); no guess: the bucket directory (sigma_of)
+      if ((sg.kind & 3) > 0) {
+        // groups of G rows: G records in flight per lane (the register budget of the LDS path)
+        constexpr int G = R < 4 ? R : 4;
+        const double4* __restrict__ rr = tb.rec + sg.lo;
+#pragma unroll
+        for (int r0g = 0; r0g < R; r0g += G) {
+          double4 q[G];
+#pragma unroll
+          for (int j = 0; j < G; ++j) q[j] = rr[seg_guess(tt[r0g + j], sg.xs, sg.inv, sg.m)];
+          if (!exact) {
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+              const double t = tt[r0g + j];
+              const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+              const int32_t k = t < q[j].x ? g - 1 : (t >= q[j].w ? g + 1 : g);
+              if (k != g) q[j] = rr[k];
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < G; ++j)
+            emit(r0g + j, __builtin_fma(q[j].y, exp_taylor<D>(q[j].z * (tt[r0g + j] - q[j].x), pc), -off));
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) emit(r, sigma_of(tt[r], tb));
+      }
+    } else {
+      double xk[R];
+      double2 el[R];
+      if (exact) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
+          xk[r] = sx_[g].x;
+          el[r] = se_[g];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
+          const double2 xx = sx_[g];
+          const int32_t k = tt[r] < xx.x ? g - 1 : (tt[r] >= xx.y ? g + 1 : g);
+          xk[r] = sx_[k].x;
+          el[r] = se_[k];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) emit(r, __builtin_fma(el[r].x, exp_taylor<D>(el[r].y * (tt[r] - xk[r]), pc), -off));
+    }
+  }
+  // rows' outputs, then their half-tile Q ranges through LDS (over the slices, no longer read)
+  float qv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int32_t orow = r0 + r;
+    double Qv;
+    if constexpr (MG) {
+      if (live && orow < n_rows) {
+        sig[(int64_t)orow * n_wav + w] = acc[r];
+        zfl[(int64_t)orow * n_wav + w] = (zb >> r) & 1u;
+      }
+      const double qs = acc[r] * nscale_m;
+      Qv = qs > 0.0 ? qs : 0.0;
+    } else {
+      Qv = acc[r];
+    }
+    qv[r] = Qv <= 1.0e100 ? (float)Qv : -1.0f;
+  }
+  static_assert(sizeof(double2) * 2 * kSigSeg >= sizeof(float) * R * kBlock, "Q staging fits over the slices");
+  float* sq = reinterpret_cast<float*>(slds);   // [R][kBlock]
+  __syncthreads();   // every lane's lookups done: the slices are free
+#pragma unroll
+  for (int r = 0; r < R; ++r) sq[r * kBlock + tid] = qv[r];
+  __syncthreads();
+  {
+    constexpr int TPH = kBlock / (R * 4), VPT = 64 / TPH;
+    static_assert(TPH >= 4 && TPH <= 16 && TPH * VPT == 64, "4 to 16 threads per (row, half tile)");
+    const int r = tid / (4 * TPH), h = (tid / TPH) & 3, pp = tid % TPH;
+    const float* q8 = sq + r * kBlock + h * 64 + pp * VPT;
+    float mn = q8[0], mx = q8[0];
+#pragma unroll
+    for (int i = 1; i < VPT; ++i) { mn = fminf(mn, q8[i]); mx = fmaxf(mx, q8[i]); }
+    mn = fminf(mn, dpp_movf<0xB1>(mn)); mx = fmaxf(mx, dpp_movf<0xB1>(mx));     // quad_perm [1,0,3,2]
+    mn = fminf(mn, dpp_movf<0x4E>(mn)); mx = fmaxf(mx, dpp_movf<0x4E>(mx));     // quad_perm [2,3,0,1]
+    if (TPH >= 8) { mn = fminf(mn, dpp_movf<0x141>(mn)); mx = fmaxf(mx, dpp_movf<0x141>(mx)); }   // row_half_mirror
+    if (TPH >= 16) { mn = fminf(mn, dpp_movf<0x140>(mn)); mx = fmaxf(mx, dpp_movf<0x140>(mx)); }  // row_mirror
+    const int64_t hw2 = wb * (kBlock / 64) + h;
+    if (pp == 0 && r0 + r < n_rows && hw2 < n_halves)
+      reinterpret_cast<float2*>(tq)[(int64_t)(r0 + r) * n_halves + hw2] = q_range(mn, mx);
+  }
+}
+
+// prom_transit_set: flags[b][s] = 1 when the guess of segment (b, s) differs from numpy's bracket for some
+// target shift_o lambda_w of the block (every row, and the last wavelength for lanes past n_wav, as the
+// sigma-row kernels take it); k_seg_mark then sets kind |= 4 on the others.
+template <int NSIG>
+__global__ void __launch_bounds__(kBlock) k_seg_exact(const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
+                                                      int32_t n_rows, const SigSeg* __restrict__ seg,
+                                                      int32_t* __restrict__ flags) {
+  const int64_t wb = blockIdx.x;
+  const int64_t w = wb * kBlock + threadIdx.x;
+  const double lam = wav[w < n_wav ? w : n_wav - 1];
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) {
+    const SigSeg sg = seg[wb * NSIG + s];
+    if ((sg.kind & 3) == 0) continue;
+    const SigTabDev& tb = tabv.t[s];
+    const double* __restrict__ X = tb.x + sg.lo;
+    bool ok = true;
+    for (int32_t o = 0; o < n_rows; ++o) {
+      const double t = tb.shift[o] * lam;
+      const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+      int32_t a = 0, b = sg.m - 1;   // X[a] <= t < X[b] (the host's slice bounds)
+      while (b - a > 1) {
+        const int32_t mid = (a + b) >> 1;
+        if (X[mid] <= t) a = mid; else b = mid;
+      }
+      ok = ok && a == g;
+    }
+    if (__ballot(!ok) != 0ull && (threadIdx.x & 63) == 0) atomicOr(&flags[wb * NSIG + s], 1);
+  }
+}
+
+__global__ void k_seg_mark(SigSeg* __restrict__ seg, const int32_t* __restrict__ flags, int64_t n) {
+  const int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  if (i < n && (seg[i].kind & 3) != 0 && flags[i] == 0) seg[i].kind |= 4;
+}
+
+void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
+                      int32_t n_rows, SigSeg* seg, int32_t* flags) {
+  const int64_t n_blk = (n_wav + kBlock - 1) / kBlock;
+  PROM_HIP(hipMemsetAsync(flags, 0, sizeof(int32_t) * n_blk * nsig, s));
+#define PROM_SE(NS) \
+  hipLaunchKernelGGL((k_seg_exact<NS>), dim3((unsigned)n_blk), dim3(kBlock), 0, s, tabv, wav, n_wav, n_rows, seg, flags)
+  switch (nsig) {
+    case 1: PROM_SE(1); break;
+    case 2: PROM_SE(2); break;
+    case 3: PROM_SE(3); break;
+    default: PROM_SE(4); break;
+  }
+#undef PROM_SE
+  PROM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_seg_mark, dim3(grid_for(n_blk * nsig)), dim3(kBlock), 0, s, seg, flags, n_blk * nsig);
+  PROM_HIP(hipGetLastError());
+}
+
+void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4& tabv, const double* wav, int64_t n_wav,
+                       int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop) {
+  const int32_t n_blk = (int32_t)grid_for(n_wav);
+  // rows per workgroup: PROM_SIG_POLY_ROWS when set at build time, else 8 for several species (their lookups
+  // fill the workgroup) and 4 for one (more workgroups in flight)
+  const int R = kSigPolyRows > 0 ? kSigPolyRows : (nsig >= 2 ? 8 : 4);
+  const int32_t n_rc = (n_rows + R - 1) / R;
+  // PROM_SIG_PARTS (profiling only: R is wrong without both): 1 = LDS workgroups, 2 = global-record ones
+  static const int32_t parts = std::getenv("PROM_SIG_PARTS") ? std::atoi(std::getenv("PROM_SIG_PARTS")) : 3;
+  const unsigned nb = (unsigned)((int64_t)((n_blk + 7) / 8) * 8 * n_rc);
+  static const PolyCoef pc = [] {
+    PolyCoef c{};
+    constexpr InvFact F{};
+    for (int k = 0; k < 16; ++k) c.c[k] = F.v[k];
+    return c;
+  }();
+#define PROM_SIGP(NS, DG)                                                                                          \
+  do {                                                                                                             \
+    if (merge_sp && R == 8)                                                                                        \
+      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, true, 8>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, tabv, \
+                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts); \
+    else if (merge_sp)                                                                                             \
+      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, true, 4>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, tabv, \
+                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts); \
+    else if (R == 8)                                                                                               \
+      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, false, 8>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0,   \
+                            tabv, pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, \
+                            parts);                                                                                \
+    else                                                                                                           \
+      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, false, 4>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0,   \
+                            tabv, pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, \
+                            parts);                                                                                \
+  } while (0)
+#define PROM_SIGP_D(NS)                      \
+  switch (deg) {                             \
+    case 4: PROM_SIGP(NS, 4); break;         \
+    case 6: PROM_SIGP(NS, 6); break;         \
+    case 8: PROM_SIGP(NS, 8); break;         \
+    case 10: PROM_SIGP(NS, 10); break;       \
+    case 12: PROM_SIGP(NS, 12); break;       \
+    default: PROM_SIGP(NS, 14); break;       \
+  }
+  switch (nsig) {
+    case 1: PROM_SIGP_D(1) break;
+    case 2: PROM_SIGP_D(2) break;
+    case 3: PROM_SIGP_D(3) break;
+    default: PROM_SIGP_D(4) break;
+  }
+#undef PROM_SIGP_D
+#undef PROM_SIGP
+  PROM_HIP(hipGetLastError());
+}
+
 // ---- half-tile Q bounds for the fused path (no sigma rows in HBM) -------------------------------------
 // k_order / k_windows pick each tile's tau window from a Q range that must enclose Q at every wavelength of
 // the half tile.  Without the sigma rows it is bounded from the table nodes the half tile's targets can
@@ -266,7 +630,7 @@ __global__ void __launch_bounds__(kBlock) k_qbounds(const SigTabs4 tabv, const d
     double flo, fhi;
     if (sg.m <= 0) { bad = true; continue; }
     const double ta = tb.shift[orow] * wav[w0 < n_wav ? w0 : n_wav - 1], tz = tb.shift[orow] * wav[w1];
-    if (sg.kind > 0) {
+    if ((sg.kind & 3) > 0) {
       // first / last target's bracket within one node of the guess: the range [g_a - 1, g_z + 2] holds both
       // brackets' nodes
       const int32_t ga = seg_guess(ta, sg.xs, sg.inv, sg.m), gz = seg_guess(tz, sg.xs, sg.inv, sg.m);
@@ -317,13 +681,13 @@ void launch_qbounds(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const dou
 
 void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                        int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
-                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start) {
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop) {
   const int32_t n_blk = (int32_t)grid_for(n_wav);
   const int32_t n_rc = (n_rows + kSigRowChunk - 1) / kSigRowChunk;
   const int32_t n_fc = (n_rows + kSigFbRows - 1) / kSigFbRows;
   const unsigned nb = (unsigned)((int64_t)((n_blk + 7) / 8) * 8 * n_rc + (int64_t)((n_fb + 7) / 8) * 8 * n_fc);
 #define PROM_SIGR(NS)                                                                                        \
-  hipExtLaunchKernelGGL((k_sigma_rows<NS>), dim3(nb), dim3(kBlock), 0, s, ev_start, nullptr, 0, tabv, wav, n_wav, \
+  hipExtLaunchKernelGGL((k_sigma_rows<NS>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, tabv, wav, n_wav, \
                         n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl)
   switch (nsig) {
     case 1: PROM_SIGR(1); break;

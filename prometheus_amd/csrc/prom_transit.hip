@@ -2006,6 +2006,40 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
 #endif
 }
 
+// The Doppler cross-section rows of one run: polynomial rows (k_sigma_poly) when the problem's tables allow
+// them (TransitDev::sig_deg), else the exp10 rows (k_sigma_rows)
+static void launch_rows(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, int32_t sig_rows, bool msp,
+                        hipEvent_t ev_start) {
+  hipEvent_t ev_stop = nullptr;
+  if (tr.kprof) {
+    tr.kprof_mask |= 1u << PROM_K_SIGMA;
+    ev_start = tr.kprof[2 * PROM_K_SIGMA];
+    ev_stop = tr.kprof[2 * PROM_K_SIGMA + 1];
+  }
+  if (tr.sig_deg > 0)
+    launch_sigma_poly(s, nsig, tr.sig_deg, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
+                      tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(),
+                      rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(), ev_start, ev_stop);
+  else
+    launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
+                      tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0,
+                      tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(), ev_start, ev_stop);
+}
+
+// prom_transit_kernel_ms: the start / stop events of kernel `id` (the given defaults when not profiling);
+// kp_rec records one of them on the stream around a group of plain launches
+static hipEvent_t kp_start(TransitDev& tr, int id, hipEvent_t d) {
+  if (!tr.kprof) return d;
+  tr.kprof_mask |= 1u << id;
+  return tr.kprof[2 * id];
+}
+static hipEvent_t kp_stop(TransitDev& tr, int id, hipEvent_t d) { return tr.kprof ? tr.kprof[2 * id + 1] : d; }
+static void kp_rec(TransitDev& tr, int id, bool stop, hipStream_t s) {
+  if (!tr.kprof) return;
+  tr.kprof_mask |= 1u << id;
+  PROM_HIP(hipEventRecord(tr.kprof[2 * id + (stop ? 1 : 0)], s));
+}
+
 void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vector<AtomTable>& tables,
                     const std::vector<MolTable>& mtables, hipEvent_t* ev, int* variant, bool stage_events) {
   const int64_t per = (int64_t)tr.n_orb * tr.n_pr * tr.n_x;
@@ -2065,10 +2099,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
     }
     auto sigma_rows = [&]() {
-      launch_sigma_rows(sig_fork ? rs.aux : s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
-                        tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(),
-                        rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(),
-                        sig_fork ? nullptr : ev0);
+      launch_rows(sig_fork ? rs.aux : s, tr, rs, nsig, sig_rows, msp, sig_fork ? nullptr : ev0);
       if (sig_fork) PROM_HIP(hipEventRecord(rs.ev_join, rs.aux));
       else ev0 = nullptr;
     };
@@ -2081,7 +2112,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #define PROM_COLS(SV, NSV)                                                                               \
   hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
                      dim3(col_blocks),                                                                    \
-                     dim3(kBlock), 0, s, ev0, nullptr, 0, cargs, n_terms,                                 \
+                     dim3(kBlock), 0, s, kp_start(tr, PROM_K_COLUMNS, ev0), kp_stop(tr, PROM_K_COLUMNS, nullptr), 0, \
+                     cargs, n_terms,                                                                      \
                      tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
                      tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
                      tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
@@ -2106,6 +2138,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     ev0 = nullptr;
   } else {
     if (ev0) PROM_HIP(hipEventRecord(ev0, s));
+    kp_rec(tr, PROM_K_COLUMNS, false, s);
     for (int32_t sc = 0; sc < tr.n_sc; ++sc) {
       const DensityDev& m = tr.dens[sc];
       const double* tab = nullptr;
@@ -2132,11 +2165,14 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                        tr.sigma_max_dev.as<double>(), mol_max, tr.cull_tau, rs.ncol.as<double>(),
                        tr.molcol.as<double>(), rs.flags.as<int32_t>());
     PROM_HIP(hipGetLastError());
+    kp_rec(tr, PROM_K_COLUMNS, true, s);
   }
   if (tr.star) {
     // 2'. stellar spectrum: one exact chord-order kernel over the flags / columns
     if (ev1) PROM_HIP(hipEventRecord(ev1, s));
+    kp_rec(tr, PROM_K_TAU, false, s);
     launch_tau_rm(s, tr, rs, na, ev);
+    kp_rec(tr, PROM_K_TAU, true, s);
     *variant = 40 + (na <= 8 ? na : 0);
     PROM_HIP(hipGetLastError());
     return;
@@ -2147,7 +2183,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   const int64_t hcap = (int64_t)tr.n_orb * 2 * n_wtiles;   // heavy entries per list: at most one per half tile
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
-  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, nullptr, pre_sigma ? nullptr : ev_ord, 0, \
+  hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, kp_start(tr, PROM_K_ORDER, nullptr),    \
+                     kp_stop(tr, PROM_K_ORDER, pre_sigma ? nullptr : ev_ord), 0,                          \
                      rs.flags.as<int32_t>(),                                                              \
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
                      tr.window ? 1 : 0, tabs4, rs.recs.as<double>(),                                     \
@@ -2168,17 +2205,14 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       default: PROM_CHW(4); break;
     }
 #undef PROM_CHW
-    if (sig_after_order) {
-      launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
-                        tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0,
-                        tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(), nullptr);
-    }
+    if (sig_after_order) launch_rows(s, tr, rs, nsig, sig_rows, msp, nullptr);
     if (pre_sigma) {
       // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
       if (sig_rows > 1 && tr.sig_seg_ok && !fused && rs.aux && rs.ev_join) PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
       const dim3 gw((unsigned)((n_wtiles + kBlock - 1) / kBlock), (unsigned)tr.n_orb);
 #define PROM_WIN(NSV)                                                                                    \
-  hipExtLaunchKernelGGL(k_windows<NSV>, gw, dim3(kBlock), 0, s, nullptr, ev_ord, 0, rs.tq.as<float4>(),      \
+  hipExtLaunchKernelGGL(k_windows<NSV>, gw, dim3(kBlock), 0, s, kp_start(tr, PROM_K_WINDOWS, nullptr),        \
+                        kp_stop(tr, PROM_K_WINDOWS, ev_ord), 0, rs.tq.as<float4>(),                          \
                         sig_rows, n_wtiles, tr.n_wav, rs.counts.as<int32_t>(), rs.wenv.as<int32_t>(),       \
                         rs.trec.as<int4>(), tr.plan ? rs.hlist.as<int4>() : nullptr, hcap,                  \
                         tr.plan ? rs.hcnt.as<int32_t>() : nullptr)
@@ -2191,10 +2225,12 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #undef PROM_WIN
     }
   } else {
+    kp_rec(tr, PROM_K_ORDER, false, s);
     hipLaunchKernelGGL(k_chords, dim3(tr.n_orb), dim3(kChordBlock), 0, s, rs.flags.as<int32_t>(),
                        tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_atoms, tr.n_pr, tr.n_orb,
                        (tr.merge && tr.exp_mode && tr.n_mol == 0) ? 1 : 0, rs.recs.as<double>(), rs.act_ip.as<int32_t>(),
                        rs.mrecs.as<double>(), rs.counts.as<int32_t>(), rs.tsum.as<double>(), rs.fsum.as<double>());
+    kp_rec(tr, PROM_K_ORDER, true, s);
     if (ev1) PROM_HIP(hipEventRecord(ev1, s));
   }
   PROM_HIP(hipGetLastError());
@@ -2234,12 +2270,13 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   }
   const bool tau_w = !(tr.n_mol > 0) && tr.exp_mode && wpath && tr.window;
   if (ev && !tau_w) PROM_HIP(hipEventRecord(ev[2], s));
+  if (!tau_w && tr.n_mol == 0) kp_rec(tr, PROM_K_TAU, false, s);   // (k_tau_mol: its own packet events)
   if (tr.n_mol > 0) {
     launch_tau_mol(s, tr, rs, na, g, ppg);
   } else if (tr.exp_mode && wpath && tr.window) {
 #define PROM_TAUW(NSV, PMV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_tau_w<NSV, UV>), dim3((unsigned)((tr.n_wav + kTW - 1) / kTW), (unsigned)((tr.n_orb + kTP - 1) / kTP)), \
-                     dim3(kBlock), 0, s, ev_tau0, ev ? ev[3] : nullptr, 0,                              \
+                     dim3(kBlock), 0, s, kp_start(tr, PROM_K_TAU, ev_tau0), kp_stop(tr, PROM_K_TAU, ev ? ev[3] : nullptr), 0, \
                      tabs4, wav, recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr,                           \
                      tr.n_orb, tr.n_wav, rs.wenv.as<int32_t>(), rs.wmom.as<double>(), rs.sig.as<double>(),  \
                      rs.trec.as<int4>(), n_wtiles, msp ? rs.zfl.as<uint8_t>() : nullptr, (UV) ? sig_rows : 1, \
@@ -2289,7 +2326,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       tr.ts_blocks = tsp ? (int32_t)blocks : 0;
 #define PROM_TAUP(NSV, PHV, FSV)                                                                        \
   hipExtLaunchKernelGGL((k_tau_p<NSV, PHV, FSV>), dim3((unsigned)blocks), dim3(kBlock), 0, s,           \
-                        ev_tau0, ev ? ev[3] : nullptr, 0, tabs4, rs.sig.as<double>(),                     \
+                        kp_start(tr, PROM_K_TAU, ev_tau0), kp_stop(tr, PROM_K_TAU, ev ? ev[3] : nullptr), 0, \
+                        tabs4, rs.sig.as<double>(),                                                      \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
                         rs.wmom.as<double>(), rs.trec.as<int4>(), n_wtiles, rs.hlist.as<int4>(),        \
                         hcap, rs.hcnt.as<int32_t>(), (int32_t)n_static,                                 \
@@ -2325,6 +2363,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #undef PROM_TAU
   PROM_HIP(hipGetLastError());
   if (ev && !tau_w) PROM_HIP(hipEventRecord(ev[3], s));
+  if (!tau_w && tr.n_mol == 0) kp_rec(tr, PROM_K_TAU, true, s);
 }
 
 }  // namespace prom

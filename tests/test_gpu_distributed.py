@@ -27,7 +27,7 @@ def _bench(tmp, world, config):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--steps", "3", "--warmup", "1", "--config", config, "--scaling", "strong",
-           "--no-cpu-baseline", "--dump-R", out]
+           "--no-cpu-baseline", "--no-projection", "--dump-R", out]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
@@ -57,3 +57,21 @@ def test_two_rank_bench_gathers_bitwise(config, tmp_path):
     assert np.array_equal(R, s1[2])
     # whole-job points / s counts every rank's shard once
     assert res2["config"]["global_wavelengths"] == res1["config"]["global_wavelengths"]
+
+
+def test_shard_mode_is_one_ranks_work(tmp_path):
+    """bench.py --shard r/N times exactly rank r's shard of an N-way strong split on one GPU: its R is the
+    matching slice of the two-rank run's gathered spectrum (C2: bitwise)."""
+    res1, (s1,) = _bench(str(tmp_path), 1, "C2")
+    out = os.path.join(str(tmp_path), "shard")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1", "--config", "C2",
+           "--shard", "1/2", "--no-cpu-baseline", "--no-projection", "--dump-R", out]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    res = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["scaling"] == "strong" and "shard 1/2" in res["config"]["workload"]
+    with open(os.path.join(out, "range_rank0.json")) as fh:
+        rg = json.load(fh)
+    part = np.load(os.path.join(out, "R_rank0.npy"))
+    assert rg["w0"] > 0 and rg["w1"] == s1[2].shape[1]
+    assert np.array_equal(part, s1[2][:, rg["w0"]:rg["w1"]])

@@ -38,11 +38,12 @@ def _sample(n_wav, k, seed):
 CASES = {
     "C3": ((16, 351222), 400, 13),
     "C4": ((8, 186604), 600, 14),
-    "C5": ((32, 1000000), 6, 15),
+    "C4x10": ((8, None), 300, 16),    # the 8-GPU strong-scaling workload (~1.9e6 wavelengths)
+    "C5": ((32, 1000000), 40, 15),
 }
 
 
-@pytest.mark.parametrize("name", ["C3", "C4", "C5"])
+@pytest.mark.parametrize("name", ["C3", "C4", "C4x10", "C5"])
 def test_full_size_config_sampled(name):
     from prometheus_amd import configs, gasProperties as gp, setupfile
     shape, k, seed = CASES[name]
@@ -54,6 +55,8 @@ def test_full_size_config_sampled(name):
     tr = setupfile.build_transit(cfg)
     R = tr.sumOverChords(devices=[0])
     st = tr.last_stats[-1]
+    if shape[1] is None:
+        shape = (shape[0], len(tr.wavelength))
     assert R.shape == shape
     idx = _sample(shape[1], k, seed)
     scen, dop, grids = O.from_setup(cfg, mol)
@@ -74,3 +77,12 @@ def test_full_size_c3_shards_bitwise():
     R1 = tr.sumOverChords(devices=[0])
     assert np.array_equal(R1, tr.sumOverChords(devices=[0, 0]))
     assert np.array_equal(R1, tr.sumOverChords(devices=[0, 0, 0]))
+
+
+def test_full_size_c4x10_eight_shards_bitwise():
+    """The 8-GPU strong-scaling workload C4x10 split into 8 wavelength shards (emulated on one GPU, one host
+    thread per shard as on 8 devices) is bitwise the 1-shard R."""
+    from prometheus_amd import configs, setupfile
+    tr = setupfile.build_transit(configs.get("C4x10"))
+    R1 = tr.sumOverChords(devices=[0])
+    assert np.array_equal(R1, tr.sumOverChords(devices=[0] * 8))

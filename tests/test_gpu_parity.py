@@ -483,21 +483,28 @@ def test_graph_replay_matches(dev, monkeypatch):
 @pytest.mark.parametrize("name,merge", [("C3r", "1"), ("C3r", "0"), ("C4r", "1"), ("exomoon", "1"), ("C3", "1"),
                                         ("C3", "0"), ("C4", "1")])
 def test_sigma_rows_bitwise(dev, name, merge, monkeypatch):
-    """Orbital Doppler shift: the per-phase cross-section rows from k_sigma_rows (table slices staged in
-    LDS per wavelength block, slopes divided per node, brackets walked from row to row;
-    PROM_SIGMA_ROWS=1) are bit-for-bit the per-target directory lookups (PROM_SIGMA_ROWS=0), merged
-    (Y = sum_s chi_s sigma_s) and per species: R is identical."""
+    """Orbital Doppler shift: the per-phase cross-section rows against the per-target directory lookups
+    (PROM_SIGMA_ROWS=0: sigma_of, numpy.interp + exp10 per target).  The exp10 rows (k_sigma_rows, table
+    slices staged in LDS per wavelength block; PROM_SIG_POLY=0) are bit-for-bit those lookups, merged
+    (Y = sum_s chi_s sigma_s) and per species: R is identical.  The polynomial rows (k_sigma_poly, the
+    default: E_k e^a with a degree-D Taylor polynomial over the tables' {x, 10^y, ln10 slope} records) move
+    sigma by ~1e-14 relative: R within 1e-13."""
     from prometheus_amd import configs
     cfg = configs.get(name) if name in ("C3", "C4") else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
     monkeypatch.setenv("PROM_SPECIES_MERGE", merge)
     monkeypatch.setenv("PROM_FUSED", "0")   # the sigma-row kernel itself (the fused path: test_fused_sigma)
-    monkeypatch.setenv("PROM_SIGMA_ROWS", "1")
-    R_a = tr.sumOverChords(devices=[0])
     monkeypatch.setenv("PROM_SIGMA_ROWS", "0")
     R_b = tr.sumOverChords(devices=[0])
-    print(name, "merge", merge, "max rel diff %.3e" % rel(R_a, R_b))
+    monkeypatch.setenv("PROM_SIGMA_ROWS", "1")
+    monkeypatch.setenv("PROM_SIG_POLY", "0")
+    R_a = tr.sumOverChords(devices=[0])
+    monkeypatch.setenv("PROM_SIG_POLY", "1")
+    R_p = tr.sumOverChords(devices=[0])
+    print(name, "merge", merge, "exp10 rows max rel diff %.3e" % rel(R_a, R_b), "poly rows %.3e" % rel(R_p, R_b))
     assert np.array_equal(R_a, R_b)
+    assert rel(R_p, R_b) < 1e-13
+    assert np.array_equal(np.isnan(R_p), np.isnan(R_b))
 
 
 # ---- SERPENS gridded density, tidally heated moon, setup-file harness (fixtures: oracle/gen_golden.py)

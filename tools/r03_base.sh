@@ -5,6 +5,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 O=$PWD/gpurun_out/${TAG:-r03a}
 mkdir -p $O
+if [ -n "$KSEL" ]; then
+  timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -rA --timeout 300 --timeout-method thread -k "$KSEL" > $O/pytest.log 2>&1 \
+    || { tail -40 $O/pytest.log; exit 1; }
+  tail -3 $O/pytest.log
+fi
 (cd /tmp && timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1); echo "list rc=$?"
 grep -o "SQ_[A-Z0-9_]*" $O/counters.txt | sort -u > $O/sq_counters.txt || true
 wc -l $O/sq_counters.txt
