@@ -49,6 +49,10 @@ prom::DensityDev to_dev(const prom_density_model& m) {
   prom::DensityDev d{};
   d.kind = m.kind;
   for (int i = 0; i < 8; ++i) d.p[i] = m.p[i];
+  // power law with a small integral exponent q (the setup files' q_esc, e.g. 6): (R / r)^q by repeated
+  // squaring on the device (pad = q + 1) instead of a general pow
+  if (m.kind == PROM_DENSITY_POWERLAW && m.p[2] >= 0.0 && m.p[2] <= 64.0 && m.p[2] == std::floor(m.p[2]))
+    d.pad = (int32_t)m.p[2] + 1;
   return d;
 }
 

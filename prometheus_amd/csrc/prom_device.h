@@ -348,7 +348,21 @@ __device__ __forceinline__ double density_at(const DensityDev& m, double xv, dou
     }
     case PROM_DENSITY_POWERLAW: {
       const double r = sqrt((dx * dx + dy * dy) + z * z);
-      return (m.p[0] * pow(m.p[1] / r, m.p[2])) * heaviside1(r - m.p[1]);
+      const double xr = m.p[1] / r;
+      double pw;
+      if (m.pad > 0) {
+        // x^q for an integral q by binary exponentiation (q uniform): at most 2 log2(q) rounded products,
+        // within a few ulp of numpy's pow (gasProperties.py:241 (R/r)**q)
+        pw = 1.0;
+        double b = xr;
+        for (int32_t e = m.pad - 1; e > 0; e >>= 1) {
+          if (e & 1) pw *= b;
+          if (e > 1) b *= b;
+        }
+      } else {
+        pw = pow(xr, m.p[2]);
+      }
+      return (m.p[0] * pw) * heaviside1(r - m.p[1]);
     }
     case PROM_DENSITY_TORUS: {
       const double a = sqrt(dx * dx + dy * dy);

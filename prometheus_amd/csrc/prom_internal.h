@@ -94,7 +94,7 @@ constexpr int kRmStarMax = 1024;
 // Device-side view of one density model (the prom_density_model scalars).
 struct DensityDev {
   int32_t kind;
-  int32_t pad;
+  int32_t pad;      // POWERLAW: q + 1 when q is an integer in [0, 64] (repeated squaring), else 0
   double p[8];
 };
 

@@ -541,6 +541,8 @@ __global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restric
 // counts[o * kCnt] = {active, transparent, blocked, nonfinite, records, sorted, windowed, 0}.
 constexpr int kLD = kWinMax / kWBlock;              // strided chords per thread and sweep
 constexpr int kRankMax = 2 * kWBlock;               // rank sort up to this many keys
+constexpr int kSlotMax = kWinMax / 2;               // slot sort up to this many keys (gathered into sIp's bytes)
+constexpr int kSlotBin = 128;                       // ... when no slot holds more than this many
 constexpr int kPayMax = 2048;                       // stage columns in LDS up to this many chords
 
 template <int NS>
@@ -714,7 +716,61 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     // ---- 3. sort the candidates [0, ncand); tail records [ncand, n) keep their compaction order
     {
     const int32_t n = ncand;
-    if (n <= kRankMax) {
+    // Slot sort (payload in LDS, candidates spread over the 1/8-octave slots of b): the key's slot is
+    // d >> 27 = (bits(1.0) - bits(b)) >> 49 with bits(b) >> 22 = d quantised inside one slot (2^22 divides
+    // 2^49), so ordering by (slot, key) IS the order of the keys: a counting sort over the slots (LDS
+    // histogram and cursors in hB / hA, keys gathered by slot into sIp's bytes), then each key's rank among
+    // its slot's keys.  The O(n^2 / threads) rank sort and the merge sort's dependent binary searches took
+    // 11-18 us of C3's 36 us k_order (~2,000 candidates per phase, profiles/r03*_trace_C3.txt).
+    bool slot_sorted = false;
+    if (n > 64 && n_all <= PAY && n <= kSlotMax) {
+      unsigned long long* sg_keys = reinterpret_cast<unsigned long long*>(sIp);   // [kSlotMax] (sIp unused: payload in LDS)
+      __shared__ int32_t s_flag;
+      if (tid == 0) s_flag = 0;
+      __syncthreads();
+      for (int32_t i = tid; i < n; i += kWBlock) {
+        const int64_t sk = (int64_t)(skey[i] >> 51);   // d >> 27 (the key is d << 24 | position)
+        if (sk >= kEnvN) s_flag = 1;
+        else atomicAdd(&hB[sk], 1);
+      }
+      __syncthreads();
+      if (!s_flag) {
+        // exclusive scan of the kEnvN slot counts (kEnvN / kWBlock per thread) -> cursors in hA
+        constexpr int PS = kEnvN / kWBlock;
+        int32_t c[PS], run = 0, cmax = 0;
+#pragma unroll
+        for (int k = 0; k < PS; ++k) { c[k] = hB[tid * PS + k]; run += c[k]; cmax = c[k] > cmax ? c[k] : cmax; }
+        int32_t tot;
+        const int32_t base = wg_excl_prefix<int32_t>(run, OpAdd(), 0, pg_, &tot);
+        int32_t acc = base;
+#pragma unroll
+        for (int k = 0; k < PS; ++k) { hA[tid * PS + k] = acc; hB[tid * PS + k] = acc; acc += c[k]; }
+        if (cmax > kSlotBin) s_flag = 1;   // a crowded slot: the rank step would be quadratic in it
+        __syncthreads();
+      }
+      if (!s_flag) {
+        // gather by slot (positions within a slot in arrival order), then rank inside the slot by key
+        for (int32_t i = tid; i < n; i += kWBlock) {
+          const unsigned long long k = skey[i];
+          sg_keys[atomicAdd(&hA[(int32_t)(k >> 51)], 1)] = k;
+        }
+        __syncthreads();
+        for (int32_t i = tid; i < n; i += kWBlock) {
+          const unsigned long long k = sg_keys[i];
+          const int32_t sk = (int32_t)(k >> 51);
+          const int32_t a = hB[sk], b = hA[sk];   // the slot's segment [a, b) (hA: the cursors' end)
+          int32_t r = 0;
+          for (int32_t j = a; j < b; ++j) r += sg_keys[j] < k;
+          skey[a + r] = k;
+        }
+        slot_sorted = true;
+      }
+      __syncthreads();
+      for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }   // (the envelope histograms)
+      __syncthreads();
+    }
+    if (slot_sorted) {
+    } else if (n <= kRankMax) {
       // rank = number of smaller keys (keys are unique: they carry the chord index); only the
       // wavefronts holding keys count, against LDS broadcasts
       const int32_t i0 = tid, i1 = tid + kWBlock;
@@ -943,6 +999,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         if ((headbits >> k) & 1u) { ++g; gk[k] = g; ak[k] = arun; }
       }
       // backward: moments
+      int32_t tailB = 0;
 #pragma unroll
       for (int k = kWPer - 1; k >= 0; --k) {
         if (k >= cnt) continue;
@@ -972,9 +1029,11 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           // envelopes -> histograms over the threshold-table index (1/8 octave): slot 0 below the
           // table, slot kEnvN + 1 above it
           // (tail records, unsorted behind every candidate: B = btail covers all of them)
-          const double Bg = i >= ncand ? btail * (1.0 + 0x1p-28) : (bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28));
+          // (tail records share one B slot: counted per thread and added once per wavefront below -- on
+          // C3 ~1,800 same-address LDS atomics per phase otherwise)
           const double Ag = ak[k] * (1.0 - 0x1p-38);
-          atomicAdd(&hB[env_slot(Bg)], 1);
+          if (i >= ncand) ++tailB;
+          else atomicAdd(&hB[env_slot(bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28))], 1);
           atomicAdd(&hA[env_slot(Ag)], 1);
 #pragma unroll
           for (int m = 0; m < K; ++m) {
@@ -982,6 +1041,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
             mm[(int64_t)gi * K + m] = v;
           }
         }
+      }
+      {
+        const int32_t tw = (int32_t)(wave_reduce_f((float)tailB, [](float a, float b) { return a + b; }) + 0.5f);
+        if (lane == 0 && tw > 0) atomicAdd(&hB[env_slot(btail * (1.0 + 0x1p-28))], tw);
       }
     }
     if (window) {

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 T=${TAG:-r03ck}
 O=$PWD/gpurun_out/$T
 mkdir -p $O
-has() { case " ${STEPS:-tests smoke bench stats traffic micro} " in *" $1 "*) return 0;; esac; return 1; }
+has() { case " ${STEPS:-tests smoke bench stats traffic micro trace} " in *" $1 "*) return 0;; esac; return 1; }
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -x -q -m gpu -rA --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
     || { tail -40 $O/pytest_gpu.log; exit 1; }
@@ -46,4 +46,8 @@ for c in ${CFGS:-C3}; do
     python3 tools/traffic_summary.py $O/traffic_$c > $O/traffic_$c/summary.json
   fi
 done
+if has trace; then
+  timeout -k 10 300 python -u tools/trace_kernels.py C3 > $O/trace_C3.txt 2>&1 || { tail -20 $O/trace_C3.txt; exit 1; }
+  head -20 $O/trace_C3.txt
+fi
 exit 0
