@@ -1198,6 +1198,11 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
         if (exact || tr.n_mol > 0 || !tr.exp_mode || tr.n_atoms > prom::kWinMaxSpecies || tr.star) unwindowed += recs;
       }
       for (int i = 0; i < 64; ++i) counted += (int64_t)ev64[i];
+      if (std::getenv("PROM_DEBUG"))
+        for (int32_t o = 0; o < tr.n_orb; ++o)
+          std::fprintf(stderr, "prom: phase %d active %d records %d candidates %d sort %d largest slot %d\n", o,
+                       cnt[o * K], cnt[o * K + 4], cnt[o * K + 7] & 8191, (cnt[o * K + 7] >> 13) & 3,
+                       cnt[o * K + 7] >> 16);
       stats->chord_lambda_evals = stats->active_chords * tr.n_wav;
       stats->exp_evals = counted + unwindowed * tr.n_wav;
       stats->tau_kernel_variant = variant;

@@ -274,12 +274,12 @@ constexpr int kSigPolyRows = PROM_SIG_POLY_ROWS;   // rows (phases) per workgrou
 #endif
 constexpr int kSigMode = PROM_SIG_MODE;
 
-// Workgroups [0, n_main): one per (256-wavelength block whose slices all fit in LDS, chunk of 16 rows).  Per
-// species the block's records {x_k, x_{k+1}} and {E_k, L_k} go to LDS; kind & 4 (the guess is numpy's
-// bracket for every target, k_seg_exact): one LDS round trip per lookup, else the +-1 bracket test and a
-// second one.  The rows accumulate Y (merged species) or their Q sum in registers, species after species.
-// Workgroups [n_main, ...): one per (other block, row), records read from the global table (one 32-byte
-// record, a second only for lanes whose bracket is the guess +- 1), or sigma_of without a guess.
+// One workgroup per (256-wavelength block, chunk of R rows).  Blocks whose slices all fit in LDS: per species
+// the block's records {x_k, x_{k+1}} and {E_k, L_k} go to LDS; kind & 4 (the guess is numpy's bracket for
+// every target, k_seg_exact): one LDS round trip per lookup, else the +-1 bracket test and a second one.
+// The rows accumulate Y (merged species) or their Q sum in registers, species after species.  Oversize
+// blocks (fb, dispatched first): records read from the global table (one 32-byte record, a second only for
+// lanes whose bracket is the guess +- 1), or sigma_of without a guess.
 template <int NSIG, int D, bool MG, int R>
 __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, const PolyCoef pc,
                                                        const double* __restrict__ wav, int64_t n_wav,
@@ -298,14 +298,29 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
   const int32_t nse = MG ? 1 : NSIG;
   // one workgroup per (256-wavelength block, chunk of R rows), XCD-aware: the row chunks of a block are 8
   // workgroups apart (one XCD's L2 for its slices)
-  const int64_t bid = blockIdx.x;
-  const int64_t grp = bid / (8 * n_rc), rem = bid % (8 * n_rc);
-  const int64_t wb = grp * 8 + rem % 8;
-  const int32_t r0 = (int32_t)(rem / 8) * R;
-  if (wb >= n_blk) return;
+  // The oversize blocks (fb, global-record lookups: a chain of L2 / HBM round trips per workgroup, the long
+  // pole) come first, so that they are not the last workgroups dispatched; their row chunks are n_fb8
+  // workgroups apart (one XCD).  The LDS blocks follow, in the XCD-aware order; oversize ones exit there.
+  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * n_rc;
+  int64_t bid = blockIdx.x, wb;
+  int32_t r0;
   bool lds_ok = true;
+  if (bid < n_front) {
+    const int64_t i = bid % n_fb8;
+    if (i >= n_fb) return;
+    wb = fb[i];
+    r0 = (int32_t)(bid / n_fb8) * R;
+    lds_ok = false;
+  } else {
+    bid -= n_front;
+    const int64_t grp = bid / (8 * n_rc), rem = bid % (8 * n_rc);
+    wb = grp * 8 + rem % 8;
+    r0 = (int32_t)(rem / 8) * R;
+    if (wb >= n_blk) return;
 #pragma unroll
-  for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
+    for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
+    if (!lds_ok) return;   // (a front workgroup's)
+  }
   // PROM_SIG_PARTS (profiling only): 1 = LDS blocks, 2 = global-record blocks
   if (!(parts & (lds_ok ? 1 : 2))) return;
   const int64_t w = wb * kBlock + tid;
@@ -547,7 +562,10 @@ void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4&
   const int32_t n_rc = (n_rows + R - 1) / R;
   // PROM_SIG_PARTS (profiling only: R is wrong without both): 1 = LDS workgroups, 2 = global-record ones
   static const int32_t parts = std::getenv("PROM_SIG_PARTS") ? std::atoi(std::getenv("PROM_SIG_PARTS")) : 3;
-  const unsigned nb = (unsigned)((int64_t)((n_blk + 7) / 8) * 8 * n_rc);
+  // front: the oversize blocks' workgroups; then the XCD-aware grid over all blocks (none when every
+  // block is oversize)
+  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * n_rc;
+  const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
   static const PolyCoef pc = [] {
     PolyCoef c{};
     constexpr InvFact F{};

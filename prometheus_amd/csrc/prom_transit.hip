@@ -541,8 +541,7 @@ __global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restric
 // counts[o * kCnt] = {active, transparent, blocked, nonfinite, records, sorted, windowed, 0}.
 constexpr int kLD = kWinMax / kWBlock;              // strided chords per thread and sweep
 constexpr int kRankMax = 2 * kWBlock;               // rank sort up to this many keys
-constexpr int kSlotMax = kWinMax / 2;               // slot sort up to this many keys (gathered into sIp's bytes)
-constexpr int kSlotBin = 128;                       // ... when no slot holds more than this many
+constexpr int kSlotBin = 128;                       // slot sort when no slot holds more than this many keys
 constexpr int kPayMax = 2048;                       // stage columns in LDS up to this many chords
 
 template <int NS>
@@ -567,7 +566,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   __shared__ unsigned long long skey[kWinMax];   // sort keys: 2^-30 buckets of b, compaction position
   __shared__ double sF[kWinMax];                 // F_out: by compaction position (payload in LDS) or by
                                                  // sorted position (columns fetched from HBM)
-  constexpr int PAY = NS >= 4 ? kPayMax / 2 : kPayMax;   // LDS budget (160 KiB)
+  constexpr int PAY = NS == 1 ? kWinMax : (NS >= 4 ? kPayMax / 2 : kPayMax);   // LDS budget (160 KiB)
   __shared__ double sN[NS][PAY];                 // columns by compaction position (n <= PAY)
   __shared__ int32_t sIp[kWinMax];               // chord index by compaction position
   __shared__ unsigned char sHead[kWinMax];
@@ -683,6 +682,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
   PROM_TS(o * 16 + 1);
   const bool sorted = nnf == 0 && nact <= kWinMax && (merge || window);
   int32_t G = nact;
+  int32_t dbg_word = 0;   // counts[7]: candidates | sort path << 13 | largest slot << 16
   if (!sorted) {
     // ---- 2. compaction into recs / act_ip (thread-major order, deterministic)
     int32_t base = 0;
@@ -716,22 +716,31 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     // ---- 3. sort the candidates [0, ncand); tail records [ncand, n) keep their compaction order
     {
     const int32_t n = ncand;
-    // Slot sort (payload in LDS, candidates spread over the 1/8-octave slots of b): the key's slot is
-    // d >> 27 = (bits(1.0) - bits(b)) >> 49 with bits(b) >> 22 = d quantised inside one slot (2^22 divides
-    // 2^49), so ordering by (slot, key) IS the order of the keys: a counting sort over the slots (LDS
-    // histogram and cursors in hB / hA, keys gathered by slot into sIp's bytes), then each key's rank among
-    // its slot's keys.  The O(n^2 / threads) rank sort and the merge sort's dependent binary searches took
-    // 11-18 us of C3's 36 us k_order (~2,000 candidates per phase, profiles/r03*_trace_C3.txt).
+    // Slot sort (candidates spread over the 1/8-octave slots of b): the key's slot is d >> 27 =
+    // (bits(1.0) - bits(b)) >> 49 with bits(b) >> 22 = d quantised inside one slot (2^22 divides 2^49), so
+    // ordering by (slot, key) IS the order of the keys: a counting sort over the slots (LDS histogram and
+    // cursors in hB / hA, the keys scattered by slot back into skey from registers), then each key's rank
+    // among its slot's keys, the lanes of a wavefront reading the same few slots (broadcasts).  The
+    // O(n^2 / threads) rank sort and the merge sort's dependent, bank-conflicted binary searches took
+    // 11-18 us of C3's 36 us k_order (~1,500 candidates per phase, profiles/r03*_trace_C3.txt).
+    constexpr int SQ = kWinMax / kWBlock;
     bool slot_sorted = false;
-    if (n > 64 && n_all <= PAY && n <= kSlotMax) {
-      unsigned long long* sg_keys = reinterpret_cast<unsigned long long*>(sIp);   // [kSlotMax] (sIp unused: payload in LDS)
+    int32_t dbg_path = 0, dbg_cmax = 0;
+    bool crowded = false;
+    if (n > 64) {
       __shared__ int32_t s_flag;
       if (tid == 0) s_flag = 0;
       __syncthreads();
-      for (int32_t i = tid; i < n; i += kWBlock) {
-        const int64_t sk = (int64_t)(skey[i] >> 51);   // d >> 27 (the key is d << 24 | position)
-        if (sk >= kEnvN) s_flag = 1;
-        else atomicAdd(&hB[sk], 1);
+      unsigned long long kk[SQ];
+#pragma unroll
+      for (int q = 0; q < SQ; ++q) {
+        const int32_t i = tid + q * kWBlock;
+        kk[q] = i < n ? skey[i] : 0ull;
+        if (i < n) {
+          const int64_t sk = (int64_t)(kk[q] >> 51);   // d >> 27 (the key is d << 24 | position)
+          if (sk >= kEnvN) s_flag = 1;
+          else atomicAdd(&hB[sk], 1);
+        }
       }
       __syncthreads();
       if (!s_flag) {
@@ -745,30 +754,47 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         int32_t acc = base;
 #pragma unroll
         for (int k = 0; k < PS; ++k) { hA[tid * PS + k] = acc; hB[tid * PS + k] = acc; acc += c[k]; }
-        if (cmax > kSlotBin) s_flag = 1;   // a crowded slot: the rank step would be quadratic in it
+        if (cmax > 0) atomicMax(&hB[kEnvN + 1], cmax);
         __syncthreads();
+        dbg_cmax = hB[kEnvN + 1];
+        crowded = dbg_cmax > kSlotBin;   // a crowded slot: the rank step would be quadratic in it
       }
-      if (!s_flag) {
-        // gather by slot (positions within a slot in arrival order), then rank inside the slot by key
-        for (int32_t i = tid; i < n; i += kWBlock) {
-          const unsigned long long k = skey[i];
-          sg_keys[atomicAdd(&hA[(int32_t)(k >> 51)], 1)] = k;
-        }
+      if (!s_flag && !crowded) {
+        // scatter by slot (arrival order within a slot), then rank inside the slot by key
+#pragma unroll
+        for (int q = 0; q < SQ; ++q)
+          if (tid + q * kWBlock < n) skey[atomicAdd(&hA[(int32_t)(kk[q] >> 51)], 1)] = kk[q];
         __syncthreads();
-        for (int32_t i = tid; i < n; i += kWBlock) {
-          const unsigned long long k = sg_keys[i];
+        int32_t dst[SQ];
+#pragma unroll
+        for (int q = 0; q < SQ; ++q) {
+          const int32_t i = tid + q * kWBlock;
+          dst[q] = -1;
+          if (i >= n) continue;
+          const unsigned long long k = skey[i];
           const int32_t sk = (int32_t)(k >> 51);
           const int32_t a = hB[sk], b = hA[sk];   // the slot's segment [a, b) (hA: the cursors' end)
-          int32_t r = 0;
-          for (int32_t j = a; j < b; ++j) r += sg_keys[j] < k;
-          skey[a + r] = k;
+          int32_t r = 0, j = a;
+          for (; j + 4 <= b; j += 4) {
+            const unsigned long long x0 = skey[j], x1 = skey[j + 1], x2 = skey[j + 2], x3 = skey[j + 3];
+            r += (x0 < k) + (x1 < k) + (x2 < k) + (x3 < k);
+          }
+          for (; j < b; ++j) r += skey[j] < k;
+          kk[q] = k;
+          dst[q] = a + r;
         }
+        __syncthreads();   // every rank counted before any key moves
+#pragma unroll
+        for (int q = 0; q < SQ; ++q)
+          if (dst[q] >= 0) skey[dst[q]] = kk[q];
         slot_sorted = true;
       }
       __syncthreads();
       for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }   // (the envelope histograms)
       __syncthreads();
     }
+    dbg_path = slot_sorted ? 1 : (n <= kRankMax ? 2 : 3);
+    dbg_word = n | (dbg_path << 13) | ((dbg_cmax < 2047 ? dbg_cmax : 2047) << 16);
     if (slot_sorted) {
     } else if (n <= kRankMax) {
       // rank = number of smaller keys (keys are unique: they carry the chord index); only the
@@ -1021,24 +1047,30 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           for (int32_t j = i + 1; j < n && !sHead[j]; ++j) F += sF[j];
         }
         double* r = mo + (int64_t)gi * ST;
-        r[0] = F;
+        if constexpr (ST == 2) {   // one 16-byte store (lanes' records are scattered: fewer store instructions)
+          *reinterpret_cast<double2*>(r) = make_double2(F, Nv[k][0]);
+        } else {
+          r[0] = F;
 #pragma unroll
-        for (int s = 0; s < NS; ++s) r[1 + s] = Nv[k][s];
+          for (int s = 0; s < NS; ++s) r[1 + s] = Nv[k][s];
+        }
         if (window) {
           // later members' a are within 2^-40 of the head's: A is widened by 2^-38 to cover them
           // envelopes -> histograms over the threshold-table index (1/8 octave): slot 0 below the
           // table, slot kEnvN + 1 above it
           // (tail records, unsorted behind every candidate: B = btail covers all of them)
-          // (tail records share one B slot: counted per thread and added once per wavefront below -- on
-          // C3 ~1,800 same-address LDS atomics per phase otherwise)
+          // (tail records share one B slot: counted per thread and added once per wavefront below)
           const double Ag = ak[k] * (1.0 - 0x1p-38);
           if (i >= ncand) ++tailB;
           else atomicAdd(&hB[env_slot(bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28))], 1);
           atomicAdd(&hA[env_slot(Ag)], 1);
+          if constexpr (K % 2 == 0) {   // 16-byte stores (wmom rows are K doubles, 16-byte aligned)
+            double2* mv = reinterpret_cast<double2*>(mm + (int64_t)gi * K);
 #pragma unroll
-          for (int m = 0; m < K; ++m) {
-            const double v = M.c[m] * msum[m];
-            mm[(int64_t)gi * K + m] = v;
+            for (int m = 0; m < K; m += 2) mv[m / 2] = make_double2(M.c[m] * msum[m], M.c[m + 1] * msum[m + 1]);
+          } else {
+#pragma unroll
+            for (int m = 0; m < K; ++m) mm[(int64_t)gi * K + m] = M.c[m] * msum[m];
           }
         }
       }
@@ -1088,7 +1120,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     counts[o * kCnt + 4] = G;
     counts[o * kCnt + 5] = sorted ? 1 : 0;
     counts[o * kCnt + 6] = (sorted && window) ? 1 : 0;
-    counts[o * kCnt + 7] = 0;
+    counts[o * kCnt + 7] = dbg_word;
   }
   PROM_TS(o * 16 + 8);
 }
