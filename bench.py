@@ -357,11 +357,12 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_pts * args.steps / elapsed
 
-    # variant // 10: 3 planned tau kernel on sigma rows, 5 planned with the Doppler sigma fused in
+    # variant // 10: 3 planned tau kernel on sigma rows, 5 / 6 planned with the Doppler sigma fused in (exp10 /
+    # polynomial lookups)
     tv = st.get("tau_kernel_variant", 0) // 10
-    fused = tv == 5
+    fused = tv in (5, 6)
     mol = bool(getattr(prob, "n_molecules", 0))
-    tau_kernel = "k_tau_mol" if mol else ("k_tau_p" if tv in (3, 5) else "k_tau_w")
+    tau_kernel = "k_tau_mol" if mol else ("k_tau_p" if tv in (3, 5, 6) else "k_tau_w")
     # k_tau_p in the pipelined loop: its span on the device clock (first workgroup start -> last workgroup end)
     tau_ms_events = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
     dev_ms = ms_runs[:, 3][np.isfinite(ms_runs[:, 3])] if len(ms_runs) else np.zeros(0)

@@ -1198,6 +1198,21 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
         if (exact || tr.n_mol > 0 || !tr.exp_mode || tr.n_atoms > prom::kWinMaxSpecies || tr.star) unwindowed += recs;
       }
       for (int i = 0; i < 64; ++i) counted += (int64_t)ev64[i];
+      if (std::getenv("PROM_DEBUG") && rs.trec.p && rs.hcnt.p && rs.tq.p) {
+        const int64_t n_wtiles = (tr.n_wav + 127) / 128;
+        std::vector<int32_t> trv(4 * tr.n_orb * n_wtiles), hc(4);
+        std::vector<float> tqv(4 * n_wtiles * tr.n_orb);
+        download(trv.data(), rs.trec, (int64_t)trv.size(), st);
+        download(hc.data(), rs.hcnt, 4, st);
+        download(tqv.data(), rs.tq, (int64_t)tqv.size(), st);
+        PROM_HIP(hipStreamSynchronize(st));
+        long long win = 0, fl = 0;
+        double tqs = 0.0;
+        for (int64_t i = 0; i < tr.n_orb * n_wtiles; ++i) { win += trv[4 * i + 1] - trv[4 * i]; fl += trv[4 * i + 2]; }
+        for (float v : tqv) tqs += v;
+        std::fprintf(stderr, "prom: windows sum %lld flags sum %lld heavy small %d big %d tq sum %.9g\n", win, fl, hc[0],
+                     hc[1], tqs);
+      }
       if (std::getenv("PROM_DEBUG"))
         for (int32_t o = 0; o < tr.n_orb; ++o)
           std::fprintf(stderr, "prom: phase %d active %d records %d candidates %d sort %d largest slot %d\n", o,

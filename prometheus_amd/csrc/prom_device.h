@@ -159,6 +159,55 @@ __device__ __forceinline__ int32_t seg_guess(double t, double b, double inv, int
   return g < 0 ? 0 : (g > m - 2 ? m - 2 : g);
 }
 
+struct InvFact {
+  double v[16];
+  constexpr InvFact() : v{} {
+    double f = 1.0;
+    v[0] = 1.0;
+    for (int i = 1; i < 16; ++i) {
+      f *= (double)i;
+      v[i] = 1.0 / f;
+    }
+  }
+};
+
+// the coefficients travel as a kernel argument (scalar registers: each FMA takes its addend from an SGPR
+// pair; as compile-time constants the compiler re-materialises both halves into VGPRs before every use)
+struct PolyCoef {
+  double c[16];
+};
+
+template <int D>
+__device__ __forceinline__ double exp_taylor(double a, const PolyCoef& pc) {
+  double p = pc.c[D];
+#pragma unroll
+  for (int k = D - 1; k >= 0; --k) p = __builtin_fma(p, a, pc.c[k]);
+  return p;
+}
+
+// exp_taylor at a run-time degree (one uniform branch; the degrees launch_sigma_poly instantiates)
+__device__ __forceinline__ double exp_taylor_d(double a, const PolyCoef& pc, int32_t deg) {
+  switch (deg) {
+    case 4: return exp_taylor<4>(a, pc);
+    case 6: return exp_taylor<6>(a, pc);
+    case 8: return exp_taylor<8>(a, pc);
+    case 10: return exp_taylor<10>(a, pc);
+    case 12: return exp_taylor<12>(a, pc);
+    default: return exp_taylor<14>(a, pc);
+  }
+}
+
+// the Taylor coefficients 1 / k! (host side, for the kernel arguments)
+inline const PolyCoef& poly_coef() {
+  static const PolyCoef pc = [] {
+    PolyCoef c{};
+    constexpr InvFact F{};
+    for (int k = 0; k < 16; ++k) c.c[k] = F.v[k];
+    return c;
+  }();
+  return pc;
+}
+
 // sigma_s(t) for the fused Doppler path (no sigma rows in HBM): the verified linear guess of the target's
 // 256-wavelength block (SigSeg, kind > 0) and two dependent reads of the global x / f arrays (numpy's slope
 // divided here), else the directory lookup.  Bit for bit the value k_sigma_rows would have stored.
@@ -177,15 +226,37 @@ __device__ __forceinline__ double sigma_seg(double t, const SigTabDev& tb, const
   return sigma_of(t, tb);
 }
 
+// sigma_s(t) on the polynomial path (TransitDev::sig_deg > 0): the block's verified guess, the bracket's
+// record {x_k, 10^f_k, ln10 slope_k, x_k+1} (a second record only when the guess is one node off), the
+// degree-deg Taylor e^a -- bit for bit the value k_sigma_poly stores (its LDS and global paths read the
+// same record); no guess: the directory lookup, as there.
+__device__ __forceinline__ double sigma_seg_poly(double t, const SigTabDev& tb, const SigSeg& sg, const PolyCoef& pc,
+                                                 int32_t deg) {
+  if ((sg.kind & 3) > 0) {
+    const double4* __restrict__ rr = tb.rec + sg.lo;
+    const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+    double4 q = rr[g];
+    if (!(sg.kind & 4)) {
+      const int32_t k = t < q.x ? g - 1 : (t >= q.w ? g + 1 : g);
+      if (k != g) q = rr[k];
+    }
+    return __builtin_fma(q.y, exp_taylor_d(q.z * (t - q.x), pc, deg), -tb.offset);
+  }
+  return sigma_of(t, tb);
+}
+
 // The tau kernel's cross sections at (phase o, wavelength lam) on the fused path: FS table species; NS == 1
 // with FS > 1 is the merged absorber Y = sum_s chi_s sigma_s (and z: some chi_s sigma_s not > 0), else the
 // species' sigma_s.
 template <int FS, int NS>
 __device__ __forceinline__ void fused_sigma(const SigTabs4& tabf, const SigSeg* __restrict__ sg, int32_t o, double lam,
-                                            double (&out)[NS], bool* z) {
+                                            double (&out)[NS], bool* z, const PolyCoef& pc, int32_t deg) {
   double v[FS];
 #pragma unroll
-  for (int s = 0; s < FS; ++s) v[s] = sigma_seg(tabf.t[s].shift[o] * lam, tabf.t[s], sg[s]);
+  for (int s = 0; s < FS; ++s) {
+    const double t = tabf.t[s].shift[o] * lam;
+    v[s] = deg > 0 ? sigma_seg_poly(t, tabf.t[s], sg[s], pc, deg) : sigma_seg(t, tabf.t[s], sg[s]);
+  }
   if constexpr (NS == 1 && FS > 1) {
     double Y = 0.0;
     bool zz = false;
@@ -209,12 +280,13 @@ __device__ __forceinline__ void fused_sigma(const SigTabs4& tabf, const SigSeg* 
 // by the vector L1's bytes, so numpy.interp's slope is divided here rather than fetched), so a thread
 // waits for two dependent round trips instead of 2 NS.  Same bracket rules and arithmetic as sigma_of, so
 // the results are identical bit for bit.
-template <int NS>
-__device__ __forceinline__ void sigma_multi(const SigTabs4& tabv, const double (&t)[NS], double (&v)[NS]) {
+// (TB(s): the table of element s -- tabv.t[s] for a wavelength's species, one table for several targets)
+template <int NS, class TB>
+__device__ __forceinline__ void sigma_multi_f(TB tbf, const double (&t)[NS], double (&v)[NS]) {
   int32_t d[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const SigTabDev& tb = tabv.t[s];
+    const SigTabDev& tb = tbf(s);
     const double fj = (t[s] - tb.dir_x0) * tb.dir_inv_h;
     const int32_t j = fj >= 0.0 ? (fj >= (double)(tb.n_dir - 1) ? tb.n_dir - 1 : (int32_t)fj) : 0;
     d[s] = tb.dir[j];
@@ -222,7 +294,7 @@ __device__ __forceinline__ void sigma_multi(const SigTabs4& tabv, const double (
   struct Win { double x0, x1, x2, x3, f0, f1, f2, f3; } u[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const SigTabDev& tb = tabv.t[s];
+    const SigTabDev& tb = tbf(s);
     const int32_t n = (int32_t)tb.n;
     int32_t l = d[s] - 1;
     l = l > n - 2 ? n - 2 : l;
@@ -233,7 +305,7 @@ __device__ __forceinline__ void sigma_multi(const SigTabs4& tabv, const double (
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const SigTabDev& tb = tabv.t[s];
+    const SigTabDev& tb = tbf(s);
     const double tt = t[s];
     const bool found = tb.n >= 2 && tt >= tb.xfirst && tt < tb.xlast && u[s].x0 <= tt && tt < u[s].x3;
     const bool c0 = tt < u[s].x1, c1 = tt < u[s].x2;
@@ -250,6 +322,11 @@ __device__ __forceinline__ void sigma_multi(const SigTabs4& tabv, const double (
     if (found && r == r) v[s] = exp10(r) - tb.offset;
     else v[s] = sigma_of(tt, tb);
   }
+}
+
+template <int NS>
+__device__ __forceinline__ void sigma_multi(const SigTabs4& tabv, const double (&t)[NS], double (&v)[NS]) {
+  sigma_multi_f<NS>([&](int s) -> const SigTabDev& { return tabv.t[s]; }, t, v);
 }
 
 // ---- wavefront scans on DPP row shifts + cross-row readlanes (no LDS traffic, no bpermute) ----

@@ -226,7 +226,6 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_rows(const SigTa
   }
 }
 
-
 // ---- polynomial sigma rows (prom_transit_set: sig_deg > 0) ---------------------------------------------
 // On numpy's bracket [x_k, x_{k+1}) of a target t,
 //   sigma_s(t) = 10^(f_k + slope_k (t - x_k)) - offset = E_k e^a - offset,   a = L_k (t - x_k),
@@ -237,31 +236,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_rows(const SigTa
 // node hit a = 0 and sigma is 10^f_k - offset as numpy's node rule gives it, and a flat interval at the
 // table floor (10^-50) gives exactly 0, so the exact path's zero pattern is kept.  No exp10, no division:
 // about 10 + D FP64 operations per lookup against ~33 on the exp10 path.
-struct InvFact {
-  double v[16];
-  constexpr InvFact() : v{} {
-    double f = 1.0;
-    v[0] = 1.0;
-    for (int i = 1; i < 16; ++i) {
-      f *= (double)i;
-      v[i] = 1.0 / f;
-    }
-  }
-};
-
-// the coefficients travel as a kernel argument (scalar registers: each FMA takes its addend from an SGPR
-// pair; as compile-time constants the compiler re-materialises both halves into VGPRs before every use)
-struct PolyCoef {
-  double c[16];
-};
-
-template <int D>
-__device__ __forceinline__ double exp_taylor(double a, const PolyCoef& pc) {
-  double p = pc.c[D];
-#pragma unroll
-  for (int k = D - 1; k >= 0; --k) p = __builtin_fma(p, a, pc.c[k]);
-  return p;
-}
+// (InvFact, PolyCoef, exp_taylor: prom_device.h, shared with the fused tau kernel)
 
 #ifndef PROM_SIG_POLY_ROWS
 #define PROM_SIG_POLY_ROWS 0
@@ -273,6 +248,10 @@ constexpr int kSigPolyRows = PROM_SIG_POLY_ROWS;   // rows (phases) per workgrou
 #define PROM_SIG_MODE 0
 #endif
 constexpr int kSigMode = PROM_SIG_MODE;
+#ifndef PROM_SIG_NOSTORE
+#define PROM_SIG_NOSTORE 0
+#endif
+constexpr bool kSigNoStore = PROM_SIG_NOSTORE != 0;   // profiling only: no sigma-row / zero-flag stores
 
 // One workgroup per (256-wavelength block, chunk of R rows).  Blocks whose slices all fit in LDS: per species
 // the block's records {x_k, x_{k+1}} and {E_k, L_k} go to LDS; kind & 4 (the guess is numpy's bracket for
@@ -281,13 +260,13 @@ constexpr int kSigMode = PROM_SIG_MODE;
 // blocks (fb, dispatched first): records read from the global table (one 32-byte record, a second only for
 // lanes whose bracket is the guess +- 1), or sigma_of without a guess.
 template <int NSIG, int D, bool MG, int R>
-__global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, const PolyCoef pc,
+__global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTabs4 tabv, const PolyCoef pc,
                                                        const double* __restrict__ wav, int64_t n_wav,
                                                        int32_t n_rows, const SigSeg* __restrict__ seg,
                                                        const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
                                                        int32_t n_rc, double* __restrict__ sig, float4* __restrict__ tq,
                                                        int32_t merge_sp, double nscale_m, uint8_t* __restrict__ zfl,
-                                                       int32_t parts) {
+                                                       int32_t parts, int32_t rf) {
   static_assert(R == 4 || R == 8 || R == 16, "4, 8 or 16 rows per workgroup");
   // per staged species: [0, kSigSeg) {x_k, x_{k+1}}, [kSigSeg, 2 kSigSeg) {E_k, L_k}
   __shared__ double2 slds[2 * kSigSeg * (kSigMode == 1 ? NSIG : 1)];
@@ -301,15 +280,18 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
   // The oversize blocks (fb, global-record lookups: a chain of L2 / HBM round trips per workgroup, the long
   // pole) come first, so that they are not the last workgroups dispatched; their row chunks are n_fb8
   // workgroups apart (one XCD).  The LDS blocks follow, in the XCD-aware order; oversize ones exit there.
-  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * n_rc;
+  // front workgroups take rf <= R rows (more of them in flight: their lookups are a chain of round trips)
+  const int32_t RF = rf;
+  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * ((n_rows + RF - 1) / RF);
   int64_t bid = blockIdx.x, wb;
-  int32_t r0;
+  int32_t r0, rcap = R;   // rows [r0, min(r0 + rcap, n_rows)) are this workgroup's
   bool lds_ok = true;
   if (bid < n_front) {
     const int64_t i = bid % n_fb8;
     if (i >= n_fb) return;
     wb = fb[i];
-    r0 = (int32_t)(bid / n_fb8) * R;
+    r0 = (int32_t)(bid / n_fb8) * RF;
+    rcap = RF;
     lds_ok = false;
   } else {
     bid -= n_front;
@@ -323,6 +305,10 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
   }
   // PROM_SIG_PARTS (profiling only): 1 = LDS blocks, 2 = global-record blocks
   if (!(parts & (lds_ok ? 1 : 2))) return;
+  const int32_t rlim = r0 + rcap < n_rows ? r0 + rcap : n_rows;
+#ifdef PROM_TRACE
+  const unsigned long long tr_t0 = wall_clock64();
+#endif
   const int64_t w = wb * kBlock + tid;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
@@ -392,7 +378,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
         if (!(cv > 0.0)) zb |= 1u << r;
         acc[r] += cv;
       } else {
-        if (live && orow < n_rows) sig[((int64_t)orow * nse + s) * n_wav + w] = v;
+        if (sig && live && orow < rlim) sig[((int64_t)orow * nse + s) * n_wav + w] = v;
         const double qs = v * nsc;
         acc[r] += qs > 0.0 ? qs : 0.0;
       }
@@ -412,6 +398,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
         const double4* __restrict__ rr = tb.rec + sg.lo;
 #pragma unroll
         for (int r0g = 0; r0g < R; r0g += G) {
+          if (r0g >= rcap) break;
           double4 q[G];
 #pragma unroll
           for (int j = 0; j < G; ++j) q[j] = rr[seg_guess(tt[r0g + j], sg.xs, sg.inv, sg.m)];
@@ -430,7 +417,8 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) emit(r, sigma_of(tt[r], tb));
+        for (int r = 0; r < R; ++r)
+          if (r < rcap) emit(r, sigma_of(tt[r], tb));
       }
     } else {
       double xk[R];
@@ -463,7 +451,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
     const int32_t orow = r0 + r;
     double Qv;
     if constexpr (MG) {
-      if (live && orow < n_rows) {
+      if (!kSigNoStore && sig && live && orow < rlim) {
         sig[(int64_t)orow * n_wav + w] = acc[r];
         zfl[(int64_t)orow * n_wav + w] = (zb >> r) & 1u;
       }
@@ -493,10 +481,37 @@ __global__ void __launch_bounds__(kBlock) k_sigma_poly(const SigTabs4 tabv, cons
     if (TPH >= 8) { mn = fminf(mn, dpp_movf<0x141>(mn)); mx = fmaxf(mx, dpp_movf<0x141>(mx)); }   // row_half_mirror
     if (TPH >= 16) { mn = fminf(mn, dpp_movf<0x140>(mn)); mx = fmaxf(mx, dpp_movf<0x140>(mx)); }  // row_mirror
     const int64_t hw2 = wb * (kBlock / 64) + h;
-    if (pp == 0 && r0 + r < n_rows && hw2 < n_halves)
+    if (pp == 0 && r0 + r < rlim && hw2 < n_halves)
       reinterpret_cast<float2*>(tq)[(int64_t)(r0 + r) * n_halves + hw2] = q_range(mn, mx);
   }
+#ifdef PROM_TRACE
+  // per workgroup: start, end (wall clock, 10 ns), block | lds << 32 | front << 33, first row | HW_ID << 32
+  if (threadIdx.x == 0 && blockIdx.x < (1u << 18)) {
+    unsigned long long* tp = g_trace + 4ull * blockIdx.x;
+    tp[0] = tr_t0;
+    tp[1] = wall_clock64();
+    tp[2] = (unsigned long long)wb | ((unsigned long long)lds_ok << 32) | ((unsigned long long)(blockIdx.x < n_front) << 33);
+    unsigned long long kinds = 0;   // 3 bits per species, then the largest slice
+    int32_t mmax = 0;
+    for (int s = 0; s < NSIG; ++s) {
+      kinds |= (unsigned long long)(seg[wb * NSIG + s].kind & 7) << (3 * s);
+      mmax = seg[wb * NSIG + s].m > mmax ? seg[wb * NSIG + s].m : mmax;
+    }
+    tp[3] = (unsigned long long)(uint32_t)r0 | (kinds << 32) | ((unsigned long long)(mmax > 65535 ? 65535 : mmax) << 44);
+  }
+#endif
 }
+
+#ifdef PROM_TRACE
+extern "C" int32_t prom_sig_trace_read(unsigned long long* out, int32_t n, int32_t clear) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+  if (clear) {
+    static unsigned long long zeros[1 << 20];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace), zeros, sizeof(zeros)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // prom_transit_set: flags[b][s] = 1 when the guess of segment (b, s) differs from numpy's bracket for some
 // target shift_o lambda_w of the block (every row, and the last wavelength for lanes past n_wav, as the
@@ -564,30 +579,33 @@ void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4&
   static const int32_t parts = std::getenv("PROM_SIG_PARTS") ? std::atoi(std::getenv("PROM_SIG_PARTS")) : 3;
   // front: the oversize blocks' workgroups; then the XCD-aware grid over all blocks (none when every
   // block is oversize)
-  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * n_rc;
+  // rows per front workgroup (measured, profiles/r03_sigma_rf_sweep.txt): R / 2 for several species (C3: 4
+  // of 8 rows, 37 against 49 us isolated); one species: all R rows when there are >= 16384 (block, row)
+  // pairs of oversize blocks (C4x10: 86 against 102 us at R / 2), else R / 2 (C4: 14.3 us, 21.2 at R; a
+  // C4x10 eighth shard: 25.5 against 31.6 us) -- PROM_SIG_RF overrides
+  static const int rf_env = std::getenv("PROM_SIG_RF") ? std::atoi(std::getenv("PROM_SIG_RF")) : 0;
+  int RF = R;
+  if (rf_env > 0) RF = rf_env < R ? rf_env : R;
+  else if (nsig >= 2 || (int64_t)n_fb * n_rows < 16384) RF = R / 2;
+  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
   const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
-  static const PolyCoef pc = [] {
-    PolyCoef c{};
-    constexpr InvFact F{};
-    for (int k = 0; k < 16; ++k) c.c[k] = F.v[k];
-    return c;
-  }();
+  const PolyCoef& pc = poly_coef();
 #define PROM_SIGP(NS, DG)                                                                                          \
   do {                                                                                                             \
     if (merge_sp && R == 8)                                                                                        \
       hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, true, 8>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, tabv, \
-                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts); \
+                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts, RF); \
     else if (merge_sp)                                                                                             \
       hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, true, 4>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, tabv, \
-                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts); \
+                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts, RF); \
     else if (R == 8)                                                                                               \
       hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, false, 8>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0,   \
                             tabv, pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, \
-                            parts);                                                                                \
+                            parts, RF);                                                                                \
     else                                                                                                           \
       hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, false, 4>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0,   \
                             tabv, pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, \
-                            parts);                                                                                \
+                            parts, RF);                                                                                \
   } while (0)
 #define PROM_SIGP_D(NS)                      \
   switch (deg) {                             \

@@ -1770,7 +1770,7 @@ __device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const 
                                             int32_t n_pr, int64_t n_wav, int lane, int64_t* w, bool* live,
                                             double (&sg)[1][NS], const double** src, double (&nx)[1 + NS],
                                             const SigTabs4& tabf, const SigSeg* __restrict__ fseg,
-                                            const double* __restrict__ wav) {
+                                            const double* __restrict__ wav, const PolyCoef& pc, int32_t sdeg) {
   constexpr int ST = 1 + NS;
   const int32_t o = en.w >> 8;
   *w = (int64_t)en.x * 64 + lane;
@@ -1778,7 +1778,7 @@ __device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const 
   if constexpr (FS > 0) {
     const int64_t wc = *live ? *w : n_wav - 1;
     bool z;
-    fused_sigma<FS, NS>(tabf, fseg + ((int64_t)en.x * 64 / kBlock) * FS, o, wav[wc], sg[0], &z);
+    fused_sigma<FS, NS>(tabf, fseg + ((int64_t)en.x * 64 / kBlock) * FS, o, wav[wc], sg[0], &z, pc, sdeg);
   } else {
     const double* so = sig + (PH ? (int64_t)o * NS * n_wav : 0);
 #pragma unroll
@@ -1816,7 +1816,8 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
                                                                    unsigned long long* __restrict__ tstamp,
                                                                    double* __restrict__ R, const SigTabs4 tabf,
                                                                    const SigSeg* __restrict__ fseg,
-                                                                   const double* __restrict__ wav) {
+                                                                   const double* __restrict__ wav,
+                                                                   const PolyCoef pc, int32_t sdeg) {
   // FS > 0 (fused Doppler path): the cross sections of the FS table species are looked up here
   // (fused_sigma) instead of read from sigma rows; merged absorbers also get their zero flags here
   constexpr int K = Monos<NS>::K;
@@ -1861,7 +1862,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
       const double lam = wav[live[j] ? w : n_wav - 1];
 #pragma unroll
       for (int r = 0; r < SR; ++r) {
-        if (r < np) fused_sigma<FS, NS>(tabf, fs_tile, o0 + r, lam, sg[r][j], &zb[r][j]);
+        if (r < np) fused_sigma<FS, NS>(tabf, fs_tile, o0 + r, lam, sg[r][j], &zb[r][j], pc, sdeg);
         else {
 #pragma unroll
           for (int s = 0; s < NS; ++s) sg[r][j][s] = 0.0;
@@ -1901,7 +1902,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
     double sgh[1][NS], nx[ST];
     const double* src;
     heavy_setup<NS, PH, FS>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), wid, sig, recs, mrecs, n_pr,
-                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav);
+                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav, pc, sdeg);
     double mm[K];
     if (wid == 0 && (f4 & 2)) {
       const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;   // t <= G <= n_pr: the row exists
@@ -1946,7 +1947,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
     double sgh[1][NS], nx[ST];
     const double* src;
     heavy_setup<NS, PH, FS>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), 0, sig, recs, mrecs, n_pr,
-                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav);
+                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav, pc, sdeg);
     const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
     double mm[K];
 #pragma unroll
@@ -2104,7 +2105,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
 // The Doppler cross-section rows of one run: polynomial rows (k_sigma_poly) when the problem's tables allow
 // them (TransitDev::sig_deg), else the exp10 rows (k_sigma_rows)
 static void launch_rows(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, int32_t sig_rows, bool msp,
-                        hipEvent_t ev_start) {
+                        hipEvent_t ev_start, bool rows_out = true) {
   hipEvent_t ev_stop = nullptr;
   if (tr.kprof) {
     tr.kprof_mask |= 1u << PROM_K_SIGMA;
@@ -2113,8 +2114,9 @@ static void launch_rows(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig
   }
   if (tr.sig_deg > 0)
     launch_sigma_poly(s, nsig, tr.sig_deg, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
-                      tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(),
-                      rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale, rs.zfl.as<uint8_t>(), ev_start, ev_stop);
+                      tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb,
+                      rows_out ? rs.sig.as<double>() : nullptr, rs.tq.as<float4>(), msp ? 1 : 0,
+                      tr.sigtab_m.t[0].nscale, rows_out ? rs.zfl.as<uint8_t>() : nullptr, ev_start, ev_stop);
   else
     launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
                       tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0,
@@ -2180,7 +2182,9 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
     // orbital Doppler shift with sigma segments: the rows come from their own kernel (k_sigma_rows)
     const bool rows_seg = pre_sigma && sig_rows > 1 && tr.sig_seg_ok;
-    const bool sig_fork = rows_seg && !fused && rs.aux && rs.ev_fork && rs.ev_join;
+    // fused with the polynomial rows: k_sigma_poly still gives the half-tile Q ranges (no rows stored)
+    const bool fused_poly = fused && tr.sig_deg > 0;
+    const bool sig_fork = rows_seg && (!fused || fused_poly) && rs.aux && rs.ev_fork && rs.ev_join;
     const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
     const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
     // the sigma rows do not depend on the columns or the ordering: with a second stream for the slot they
@@ -2194,11 +2198,12 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
     }
     auto sigma_rows = [&]() {
-      launch_rows(sig_fork ? rs.aux : s, tr, rs, nsig, sig_rows, msp, sig_fork ? nullptr : ev0);
+      static const bool dbg_rows = std::getenv("PROM_FUSED_ROWS") && std::atoi(std::getenv("PROM_FUSED_ROWS"));
+      launch_rows(sig_fork ? rs.aux : s, tr, rs, nsig, sig_rows, msp, sig_fork ? nullptr : ev0, !fused || dbg_rows);
       if (sig_fork) PROM_HIP(hipEventRecord(rs.ev_join, rs.aux));
       else ev0 = nullptr;
     };
-    if (fused) {
+    if (fused && !fused_poly) {
       launch_qbounds(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
                      rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale);
     } else if (rows_seg && sig_first && !sig_after_order) {
@@ -2229,7 +2234,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #undef PROM_COLS_L
 #undef PROM_COLS
     PROM_HIP(hipGetLastError());
-    if (rows_seg && !fused && !sig_first) sigma_rows();
+    if (rows_seg && (!fused || fused_poly) && !sig_first) sigma_rows();
     ev0 = nullptr;
   } else {
     if (ev0) PROM_HIP(hipEventRecord(ev0, s));
@@ -2303,7 +2308,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     if (sig_after_order) launch_rows(s, tr, rs, nsig, sig_rows, msp, nullptr);
     if (pre_sigma) {
       // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
-      if (sig_rows > 1 && tr.sig_seg_ok && !fused && rs.aux && rs.ev_join) PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
+      if (sig_rows > 1 && tr.sig_seg_ok && (!fused || tr.sig_deg > 0) && rs.aux && rs.ev_join)
+        PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
       const dim3 gw((unsigned)((n_wtiles + kBlock - 1) / kBlock), (unsigned)tr.n_orb);
 #define PROM_WIN(NSV)                                                                                    \
   hipExtLaunchKernelGGL(k_windows<NSV>, gw, dim3(kBlock), 0, s, kp_start(tr, PROM_K_WINDOWS, nullptr),        \
@@ -2428,7 +2434,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                         hcap, rs.hcnt.as<int32_t>(), (int32_t)n_static,                                 \
                         (msp && !fused) ? rs.zfl.as<uint8_t>() : nullptr,                                \
                         tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tsp, R,           \
-                        tr.sigtab_v, tr.sig_seg.as<prom::SigSeg>(), tr.wav.as<double>())
+                        tr.sigtab_v, tr.sig_seg.as<prom::SigSeg>(), tr.wav.as<double>(), poly_coef(),   \
+                        fused ? tr.sig_deg : 0)
       if (fused) {
         if (na == 1) {
           switch (fsv) { case 1: PROM_TAUP(1, true, 1); break; case 2: PROM_TAUP(1, true, 2); break;
@@ -2437,7 +2444,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
           switch (na) { case 2: PROM_TAUP(2, true, 2); break; case 3: PROM_TAUP(3, true, 3); break;
                         default: PROM_TAUP(4, true, 4); break; }
         }
-        *variant = 50 + (na <= 4 ? na : 0);
+        *variant = (tr.sig_deg > 0 ? 60 : 50) + (na <= 4 ? na : 0);   // 6x: polynomial lookups, k_sigma_poly's Q ranges
       } else {
         switch (na) {
           case 1: if (ph) { PROM_TAUP(1, true, 0); } else { PROM_TAUP(1, false, 0); } break;
