@@ -18,6 +18,8 @@ the data path (torch.distributed carries only the timing barrier and the max-ove
       C5), split into N contiguous shards.
   --shard r/N (one process): only shard r of N of the config's grid, timed alone on one GPU -- one rank's
       work under an N-way strong split.
+  --shard-axis phase: strong splits over orbital phases instead (every wavelength, phases [o0, o1)): the
+      phases are independent too, and a phase shard does not repeat the per-phase chord work.
 
 The N=1 line also carries, per kernel of the step, its device duration (prom_transit_kernel_ms: one run in
 flight, dispatch-packet events) with its algorithmic bytes and roofline fraction, the path-level fraction
@@ -55,6 +57,9 @@ def parse():
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--shard", default=None, metavar="r/N",
                     help="time only shard r of an N-way split of the config's grid (strong scaling, one process)")
+    ap.add_argument("--shard-axis", choices=("wavelength", "phase"), default="wavelength",
+                    help="strong splits (--shard, --scaling strong): contiguous wavelength ranges (default) or "
+                         "orbital-phase ranges (every wavelength, phases [o0, o1))")
     ap.add_argument("--no-projection", action="store_true",
                     help="skip the strong-scaling projection (C4x10 and C5, full grid vs shard 0 of 8)")
     ap.add_argument("--kernel-runs", type=int, default=20,
@@ -247,9 +252,10 @@ def time_runs(dev, prob, steps: int, warmup: int) -> float:
 
 
 def strong_projection(dev_id: int, names=("C4x10", "C5"), parts: int = 8):
-    """Strong scaling measured on one GPU: each configuration's full grid, then shard 0 of
-    `parts` (the rank with the most wavelengths: shards are equal to 256 wavelengths), both in the pipelined
-    loop.  T(full) / T(shard) is the speedup `parts` GPUs give at best (no collective, host gather only)."""
+    """Strong scaling measured on one GPU: each configuration's full grid, then the largest
+    of `parts` wavelength shards (edges on 256 wavelengths) and the largest of `parts` orbital-phase shards,
+    all in the pipelined loop.  T(full) / T(shard) is the speedup `parts` GPUs give at best on that axis (no
+    collective, host gather only); `axis` names the faster one (bench.py --scaling strong --shard-axis)."""
     from prometheus_amd import _native, configs, setupfile, sharding, gasProperties
     out = {}
     for name in names:
@@ -267,10 +273,23 @@ def strong_projection(dev_id: int, names=("C4x10", "C5"), parts: int = 8):
         k_full = dev.transit_kernel_ms(5)
         t_shard = time_runs(dev, tr._problem(dev, host, a, b, 0.0), steps, warm)
         k_shard = dev.transit_kernel_ms(5)
-        out[name] = {"wavelengths": n, "phases": len(host["orb"]), "shard": [a, b], "shards": parts,
-                     "ms_full": t_full, "ms_shard": t_shard, "projected_speedup": t_full / t_shard,
-                     "projected_efficiency": t_full / t_shard / parts,
-                     "kernel_ms_full": k_full, "kernel_ms_shard": k_shard}
+        # the other axis: the largest phase shard (every wavelength): phases are independent as well, and
+        # a phase shard does not repeat the per-phase chord work (columns, ordering) that every
+        # wavelength shard repeats in full
+        n_orb = len(host["orb"])
+        pa, pb = max(sharding.split(n_orb, parts, align=1), key=lambda ab: ab[1] - ab[0])
+        t_pshard = time_runs(dev, tr._problem(dev, sharding.phase_subset(host, pa, pb), 0, n, 0.0,
+                                              sharding.phase_options(host)), steps, warm)
+        k_pshard = dev.transit_kernel_ms(5)
+        best = "phase" if t_pshard < t_shard else "wavelength"
+        t_best = min(t_shard, t_pshard)
+        out[name] = {"wavelengths": n, "phases": n_orb, "shards": parts, "ms_full": t_full,
+                     "axis": best, "projected_speedup": t_full / t_best,
+                     "projected_efficiency": t_full / t_best / parts, "kernel_ms_full": k_full,
+                     "wavelength_shard": {"shard": [a, b], "ms_shard": t_shard, "projected_speedup": t_full / t_shard,
+                                          "kernel_ms_shard": k_shard},
+                     "phase_shard": {"phases": [pa, pb], "ms_shard": t_pshard,
+                                     "projected_speedup": t_full / t_pshard, "kernel_ms_shard": k_pshard}}
         del tr
     return out
 
@@ -307,15 +326,26 @@ def main():
     tr = setupfile.build_transit(cfg)   # lambda grid + device Voigt tables on this rank's GPU
     dev = _native.get_device(dev_id)
     n_wav_global = len(tr.wavelength)
+    host = tr._host_inputs()
+    n_orb_global = len(host["orb"])
     if args.shard:
         sr, sn = (int(v) for v in args.shard.split("/"))
         if not (0 <= sr < sn):
             raise SystemExit("--shard r/N needs 0 <= r < N")
-        w0, w1 = sharding.shard_for_rank(n_wav_global, sn, sr)
     else:
-        w0, w1 = sharding.shard_for_rank(n_wav_global, world, rank)   # tile-aligned contiguous shards
-    host = tr._host_inputs()
-    prob = tr._problem(dev, host, w0, w1, 0.0)
+        sr, sn = rank, world
+    o0, o1 = 0, n_orb_global
+    opts = 0
+    if args.shard_axis == "phase" and (args.shard or scaling == "strong"):
+        w0, w1 = 0, n_wav_global
+        o0, o1 = sharding.shard_for_rank(n_orb_global, sn, sr, align=1)
+        if o1 <= o0:
+            raise SystemExit("phase shard %d/%d is empty (%d phases)" % (sr, sn, n_orb_global))
+        opts = sharding.phase_options(host)
+        host = sharding.phase_subset(host, o0, o1)
+    else:
+        w0, w1 = sharding.shard_for_rank(n_wav_global, sn, sr)   # tile-aligned contiguous shards
+    prob = tr._problem(dev, host, w0, w1, 0.0, opts)
     dev.transit_set(prob)
     dev.transit_run()   # first launch of every kernel (code-object load) outside the stats run
     dev.synchronize()
@@ -350,7 +380,8 @@ def main():
         os.makedirs(args.dump_R, exist_ok=True)
         np.save(os.path.join(args.dump_R, "R_rank%d.npy" % rank), dev.transit_result())
         with open(os.path.join(args.dump_R, "range_rank%d.json" % rank), "w") as fh:
-            json.dump({"w0": int(w0), "w1": int(w1), "n_wav": int(n_wav_global), "world": world}, fh)
+            json.dump({"w0": int(w0), "w1": int(w1), "n_wav": int(n_wav_global), "o0": int(o0), "o1": int(o1),
+                       "n_orb": int(n_orb_global), "world": world}, fh)
     if dist:
         dist.barrier()
     elapsed, total_pts = sharding.reduce_timing(dist, t1 - t0, n_pts_rank)
@@ -463,7 +494,8 @@ def main():
     workload = "%s (%s), %d wavelengths x %d phases x %d chords x %d samples" % (
         cfg_name, describe(cfg), n_wav_global, n_orb, n_pr, n_x)
     if args.shard:
-        workload += ", shard %s: wavelengths [%d, %d)" % (args.shard, w0, w1)
+        workload += (", shard %s: phases [%d, %d)" % (args.shard, o0, o1) if args.shard_axis == "phase"
+                     else ", shard %s: wavelengths [%d, %d)" % (args.shard, w0, w1))
     result = {
         "metric": "spectrum points/sec (phase x wavelength)",
         "value": value,
@@ -480,7 +512,9 @@ def main():
         "config": {"workload": workload,
                    "global_wavelengths": n_wav_global, "orbital_phases": n_orb,
                    "chords_per_phase": n_pr, "los_samples": n_x,
-                   "parallelism": "wavelength shards x%d (no collective)" % world},
+                   "parallelism": "%s shards x%d (no collective)" % (
+                       "phase" if (args.shard_axis == "phase" and (args.shard or scaling == "strong")) else "wavelength",
+                       world)},
         "roofline": {"bound": dk.get("bound", "hbm"), "kernel": dom, "achieved": dk.get("achieved"),
                      "peak": dk.get("peak", HBM_PEAK_GBS), "unit": dk.get("unit", "GB/s"), "frac": dk.get("frac"),
                      "traffic": traffic, "algorithmic_bytes": dk.get("algorithmic_bytes"),

@@ -195,6 +195,9 @@ typedef struct prom_transit_problem {
 #define PROM_OPT_NO_MERGE 2    /* integrate every active chord (no merging of equal-column chords) */
 #define PROM_OPT_NO_WINDOW 4   /* evaluate exp(-tau) for every record at every wavelength (no saturated-
                                   head skip, no tail moments; see DESIGN.md "windowed integration") */
+#define PROM_OPT_DOPPLER_ROWS 8 /* one Doppler sigma row per orbital phase even when the phases' factors are
+                                  equal (a phase shard of a Doppler-shifted problem: the full problem's path,
+                                  so its R rows are the full run's bit for bit) */
 
 typedef struct prom_transit_stats {
   double ms_total;             /* device time of the last prom_transit_run (hipEvents)        */

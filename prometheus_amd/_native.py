@@ -67,6 +67,7 @@ ABI_VERSION = 5
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
 OPT_NO_WINDOW = 4
+OPT_DOPPLER_ROWS = 8
 
 
 class TransitStats(C.Structure):

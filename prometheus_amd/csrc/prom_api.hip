@@ -788,7 +788,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       stg.add(tr.sigtab, st.data(), (int64_t)st.size(), s);
       tr.qbound_v = 0.0;
       for (size_t i = 0; i < st.size(); ++i) tr.qbound_v += tr.atom_sigma_max[i] * st[i].nscale;
-      tr.uniform_shift = true;
+      // PROM_OPT_DOPPLER_ROWS: one sigma row per phase even when the factors are equal (a phase shard of a
+      // problem with orbital Doppler shift takes the full problem's sigma path: bitwise equal rows)
+      tr.uniform_shift = !(pb->options & PROM_OPT_DOPPLER_ROWS);
       for (const auto& t : tr.terms) {
         if (t.is_molecule) continue;
         for (int64_t o = 1; o < n_orb; ++o)

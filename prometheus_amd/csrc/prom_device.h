@@ -226,10 +226,49 @@ __device__ __forceinline__ double sigma_seg(double t, const SigTabDev& tb, const
   return sigma_of(t, tb);
 }
 
+// numpy's bracket of t (the largest j <= n-2 with x_j <= t) for x_0 <= t < x_{n-1}, n >= 2: sigma_of's
+// search (bucket directory, 4-node window, gallop + bisection), x only.
+__device__ __forceinline__ int64_t bracket_of(double t, const SigTabDev& tb) {
+  const double* __restrict__ xp = tb.x;
+  const int64_t n = tb.n;
+  const double fj = (t - tb.dir_x0) * tb.dir_inv_h;
+  const int32_t j = fj < 0.0 ? 0 : (fj >= (double)(tb.n_dir - 1) ? tb.n_dir - 1 : (int32_t)fj);
+  int64_t lo = tb.dir[j] - 1;
+  lo = lo < 0 ? 0 : (lo > n - 2 ? n - 2 : lo);
+  const int64_t l1 = lo + 1, l2 = lo + 2 < n ? lo + 2 : n - 1, l3 = lo + 3 < n ? lo + 3 : n - 1;
+  const double x0 = xp[lo], x1 = xp[l1], x2 = xp[l2], x3 = xp[l3];
+  if (x0 <= t) {
+    if (t < x1) return lo;
+    if (t < x2) return l1;
+    if (t < x3) return l2;
+  }
+  int64_t a = lo, b = l3;   // invariant after the gallop: xp[a] <= t < xp[b]
+  for (int64_t st = 1; a > 0 && xp[a] > t; st <<= 1) { b = a; a = a - st > 0 ? a - st : 0; }
+  for (int64_t st = 1; b < n - 1 && xp[b] <= t; st <<= 1) { a = b; b = b + st < n - 1 ? b + st : n - 1; }
+  while (b - a > 1) {
+    const int64_t mid = (a + b) >> 1;
+    if (xp[mid] <= t) a = mid; else b = mid;
+  }
+  return a;
+}
+
+// sigma_s(t) on the polynomial path without a verified guess: the bracket from the directory search, then
+// the record's E_k e^(L_k (t - x_k)) - offset -- the value the guessed paths give, so a row does not
+// depend on which segment kind a block got (phase shards change the segments: bitwise equal R rows);
+// numpy's end rules outside the table (node 0 / n-1: E - offset), NaN in, NaN out.
+__device__ __forceinline__ double sigma_poly_of(double t, const SigTabDev& tb, const PolyCoef& pc, int32_t deg) {
+  if (t != t) return t;
+  const int64_t n = tb.n;
+  if (n == 1 || !(t >= tb.x[0])) return __builtin_fma(tb.rec[0].y, 1.0, -tb.offset);
+  if (t >= tb.x[n - 1]) return __builtin_fma(tb.rec[n - 1].y, 1.0, -tb.offset);
+  const double4 q = tb.rec[bracket_of(t, tb)];
+  return __builtin_fma(q.y, exp_taylor_d(q.z * (t - q.x), pc, deg), -tb.offset);
+}
+
 // sigma_s(t) on the polynomial path (TransitDev::sig_deg > 0): the block's verified guess, the bracket's
 // record {x_k, 10^f_k, ln10 slope_k, x_k+1} (a second record only when the guess is one node off), the
 // degree-deg Taylor e^a -- bit for bit the value k_sigma_poly stores (its LDS and global paths read the
-// same record); no guess: the directory lookup, as there.
+// same record); no guess: sigma_poly_of, as there.
 __device__ __forceinline__ double sigma_seg_poly(double t, const SigTabDev& tb, const SigSeg& sg, const PolyCoef& pc,
                                                  int32_t deg) {
   if ((sg.kind & 3) > 0) {
@@ -242,7 +281,7 @@ __device__ __forceinline__ double sigma_seg_poly(double t, const SigTabDev& tb, 
     }
     return __builtin_fma(q.y, exp_taylor_d(q.z * (t - q.x), pc, deg), -tb.offset);
   }
-  return sigma_of(t, tb);
+  return sigma_poly_of(t, tb, pc, deg);
 }
 
 // The tau kernel's cross sections at (phase o, wavelength lam) on the fused path: FS table species; NS == 1
@@ -619,6 +658,15 @@ struct OpAdd { template <typename T> __device__ T operator()(T a, T b) const { r
 struct OpMax { __device__ double operator()(double a, double b) const { return a > b ? a : b; } };
 struct OpMin { __device__ double operator()(double a, double b) const { return a < b ? a : b; } };
 
+// Workgroup barrier for LDS data only: waits for this wave's LDS operations (lgkmcnt), not for its global
+// loads and stores (HIP's __syncthreads fences every address space: vmcnt(0) before the barrier, so a
+// wave's outstanding global stores would stall the whole workgroup at every step)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Exclusive scans over the kWBlock threads of a workgroup (8 waves); wsum: NW slots of LDS.
 // *total (optional) receives the fold over all threads.
 template <typename T, typename Op>
@@ -632,9 +680,9 @@ __device__ __forceinline__ T wg_excl_prefix(T v, Op op, T id, T* wsum, T* total 
   }
   T exc = __shfl_up(inc, 1, 64);
   if (lane == 0) exc = id;
-  __syncthreads();
+  lds_barrier();
   if (lane == 63) wsum[wid] = inc;
-  __syncthreads();
+  lds_barrier();
   T carry = id, all = id;
   for (int w = 0; w < NW; ++w) {
     if (w < wid) carry = op(carry, wsum[w]);

@@ -258,7 +258,7 @@ constexpr bool kSigNoStore = PROM_SIG_NOSTORE != 0;   // profiling only: no sigm
 // every target, k_seg_exact): one LDS round trip per lookup, else the +-1 bracket test and a second one.
 // The rows accumulate Y (merged species) or their Q sum in registers, species after species.  Oversize
 // blocks (fb, dispatched first): records read from the global table (one 32-byte record, a second only for
-// lanes whose bracket is the guess +- 1), or sigma_of without a guess.
+// lanes whose bracket is the guess +- 1), or sigma_poly_of without a guess.
 template <int NSIG, int D, bool MG, int R>
 __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTabs4 tabv, const PolyCoef pc,
                                                        const double* __restrict__ wav, int64_t n_wav,
@@ -306,6 +306,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
   // PROM_SIG_PARTS (profiling only): 1 = LDS blocks, 2 = global-record blocks
   if (!(parts & (lds_ok ? 1 : 2))) return;
   const int32_t rlim = r0 + rcap < n_rows ? r0 + rcap : n_rows;
+  rcap = rlim - r0;   // rows present (front workgroups: no lookups for padding rows)
 #ifdef PROM_TRACE
   const unsigned long long tr_t0 = wall_clock64();
 #endif
@@ -391,7 +392,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
     if (kSigMode == 2 || !lds_ok) {
       // blocks with a slice too large for LDS (the high-resolution line windows, or a wide spread of Doppler
       // factors): the records straight from the global table (L1 / L2), one 32-byte record per lookup (a second
-      // only for lanes whose bracket is the guess +- 1); no guess: the bucket directory (sigma_of)
+      // only for lanes whose bracket is the guess +- 1); no guess: the bucket directory (sigma_poly_of)
       if ((sg.kind & 3) > 0) {
         // groups of G rows: G records in flight per lane (the register budget of the LDS path)
         constexpr int G = R < 4 ? R : 4;
@@ -418,7 +419,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
       } else {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-          if (r < rcap) emit(r, sigma_of(tt[r], tb));
+          if (r < rcap) emit(r, sigma_poly_of(tt[r], tb, pc, D));
       }
     } else {
       double xk[R];

@@ -541,6 +541,9 @@ __global__ void __launch_bounds__(kChordBlock) k_chords(const int32_t* __restric
 // counts[o * kCnt] = {active, transparent, blocked, nonfinite, records, sorted, windowed, 0}.
 constexpr int kLD = kWinMax / kWBlock;              // strided chords per thread and sweep
 constexpr int kRankMax = 2 * kWBlock;               // rank sort up to this many keys
+#ifndef PROM_ORD_EXP
+#define PROM_ORD_EXP 0   // profiling only: skip parts of k_order's record step (wrong results)
+#endif
 constexpr int kSlotBin = 128;                       // slot sort when no slot holds more than this many keys
 constexpr int kPayMax = 2048;                       // stage columns in LDS up to this many chords
 
@@ -642,13 +645,13 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     const double fpw = lane_read(wave_prefix<double>(fp, OpAdd()), 63);
     const double tpw = lane_read(wave_prefix<double>(tp, OpAdd()), 63);
     const int32_t c1w = (pa63 >> 20) & 1023, c2w = pb & 1023, c3w = (pb >> 10) & 1023;
-    __syncthreads();
+    lds_barrier();
     if (lane == 63) { pi_[wid][0] = inc; pi_[wid][4] = inct; }
     if (lane == 0) {
       pi_[wid][1] = c1w; pi_[wid][2] = c2w; pi_[wid][3] = c3w;
       pd_[wid][0] = fpw; pd_[wid][1] = tpw;
     }
-    __syncthreads();
+    lds_barrier();
     int32_t sc_ = 0;   // candidates of this sweep
     for (int w = 0; w < NW; ++w) sc_ += pi_[w][0];
     int32_t pos = nact + inc - c[0];
@@ -678,7 +681,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       if (tl) ++post; else ++pos;
     }
   }
-  __syncthreads();   // keys visible to the sort
+  lds_barrier();   // keys visible to the sort
   PROM_TS(o * 16 + 1);
   const bool sorted = nnf == 0 && nact <= kWinMax && (merge || window);
   int32_t G = nact;
@@ -730,7 +733,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     if (n > 64) {
       __shared__ int32_t s_flag;
       if (tid == 0) s_flag = 0;
-      __syncthreads();
+      lds_barrier();
       unsigned long long kk[SQ];
 #pragma unroll
       for (int q = 0; q < SQ; ++q) {
@@ -742,7 +745,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           else atomicAdd(&hB[sk], 1);
         }
       }
-      __syncthreads();
+      lds_barrier();
       if (!s_flag) {
         // exclusive scan of the kEnvN slot counts (kEnvN / kWBlock per thread) -> cursors in hA
         constexpr int PS = kEnvN / kWBlock;
@@ -755,7 +758,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
 #pragma unroll
         for (int k = 0; k < PS; ++k) { hA[tid * PS + k] = acc; hB[tid * PS + k] = acc; acc += c[k]; }
         if (cmax > 0) atomicMax(&hB[kEnvN + 1], cmax);
-        __syncthreads();
+        lds_barrier();
         dbg_cmax = hB[kEnvN + 1];
         crowded = dbg_cmax > kSlotBin;   // a crowded slot: the rank step would be quadratic in it
       }
@@ -764,7 +767,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
 #pragma unroll
         for (int q = 0; q < SQ; ++q)
           if (tid + q * kWBlock < n) skey[atomicAdd(&hA[(int32_t)(kk[q] >> 51)], 1)] = kk[q];
-        __syncthreads();
+        lds_barrier();
         int32_t dst[SQ];
 #pragma unroll
         for (int q = 0; q < SQ; ++q) {
@@ -783,15 +786,15 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           kk[q] = k;
           dst[q] = a + r;
         }
-        __syncthreads();   // every rank counted before any key moves
+        lds_barrier();   // every rank counted before any key moves
 #pragma unroll
         for (int q = 0; q < SQ; ++q)
           if (dst[q] >= 0) skey[dst[q]] = kk[q];
         slot_sorted = true;
       }
-      __syncthreads();
+      lds_barrier();
       for (int32_t i = tid; i < kEnvN + 2; i += kWBlock) { hB[i] = 0; hA[i] = 0; }   // (the envelope histograms)
-      __syncthreads();
+      lds_barrier();
     }
     dbg_path = slot_sorted ? 1 : (n <= kRankMax ? 2 : 3);
     dbg_word = n | (dbg_path << 13) | ((dbg_cmax < 2047 ? dbg_cmax : 2047) << 16);
@@ -806,7 +809,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       int32_t r0 = 0, r1 = 0;
       // keys past n read as ~0 (never smaller); 16 broadcast loads in flight per step
       for (int32_t i = n + tid; i < ((n + 15) & ~15); i += kWBlock) skey[i] = ~0ull;
-      __syncthreads();
+      lds_barrier();
       const int32_t n16 = (n + 15) & ~15;
       if (n > kWBlock) {
         for (int32_t j = 0; j < n16; j += 16) {
@@ -825,10 +828,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           for (int q = 0; q < 16; ++q) r0 += a[q] < k0;
         }
       }
-      __syncthreads();
+      lds_barrier();
       if (has0) skey[r0] = k0;
       if (has1) skey[r1] = k1;
-      __syncthreads();
+      lds_barrier();
     } else {
       // merge sort in place (keys are unique): thread t owns positions [8t, 8t + 8); its eight keys are
       // sorted in registers, then runs of L = 8, 16, .. P/2 merge pairwise: a key's position in the
@@ -840,7 +843,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       while (P < n) P <<= 1;
       // padding keys: unique (the merge ranks assume it) and above every real key (<= 0xffc0... | pos)
       for (int32_t i = n + tid; i < P; i += kWBlock) skey[i] = 0xffffffffffff0000ull | (unsigned)i;
-      __syncthreads();
+      lds_barrier();
       const int32_t p0 = KP * tid;
       const bool own = p0 < P;
       unsigned long long k[KP];
@@ -858,12 +861,12 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
       cx(2, 4); cx(3, 5);
       cx(1, 2); cx(3, 4); cx(5, 6);
-      __syncthreads();   // every chunk loaded before any sorted chunk is stored
+      lds_barrier();   // every chunk loaded before any sorted chunk is stored
       if (own) {
 #pragma unroll
         for (int q = 0; q < KP; ++q) skey[p0 + q] = k[q];
       }
-      __syncthreads();
+      lds_barrier();
       for (int32_t L = KP; L < P; L <<= 1) {
         const int32_t base = p0 & ~(2 * L - 1);
         const bool left = (p0 & L) == 0;
@@ -882,12 +885,12 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           for (int q = 0; q < KP; ++q)
             if (lo[q] == L - 1 && skey[ps + L - 1] < k[q]) lo[q] = L;
         }
-        __syncthreads();   // every search done before any key moves
+        lds_barrier();   // every search done before any key moves
         if (own) {
 #pragma unroll
           for (int q = 0; q < KP; ++q) skey[base + idx + q + lo[q]] = k[q];
         }
-        __syncthreads();
+        lds_barrier();
         if (own) {
 #pragma unroll
           for (int q = 0; q < KP; ++q) k[q] = skey[p0 + q];
@@ -897,9 +900,9 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     }
     // tail keys: only their compaction position (low 24 bits) is read from here on; the sort's padding
     // may have overwritten some, so they are rewritten
-    __syncthreads();
+    lds_barrier();
     for (int32_t i = ncand + tid; i < n_all; i += kWBlock) skey[i] = (unsigned long long)i;
-    __syncthreads();
+    lds_barrier();
     PROM_TS(o * 16 + 2);
     // ---- 4. this thread's sorted positions [i0, i0 + cnt)
     const int32_t per = (n + kWBlock - 1) / kWBlock;   // <= kWPer
@@ -989,7 +992,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
     }
     if (lane == 63) { pg_[wid] = hinc; pm_[wid][K] = ainc; }
     if (lane == 0) pm_[wid][K + 1] = bw;
-    __syncthreads();
+    lds_barrier();
     PROM_TS(o * 16 + 6);
     int32_t gb = hinc - nheads, gtot = 0;
     double ball = 0.0;
@@ -1024,12 +1027,13 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         arun = av[k] < arun ? av[k] : arun;
         if ((headbits >> k) & 1u) { ++g; gk[k] = g; ak[k] = arun; }
       }
+      PROM_TS(o * 16 + 9);
       // backward: moments
       int32_t tailB = 0;
 #pragma unroll
       for (int k = kWPer - 1; k >= 0; --k) {
         if (k >= cnt) continue;
-        if (window) {
+        if (window && !(PROM_ORD_EXP & 8)) {
           double pw[NS][TailDeg<NS>::D + 1], vv[NS];
 #pragma unroll
           for (int s = 0; s < NS; ++s) vv[s] = Nv[k][s] * cs[s];
@@ -1041,13 +1045,15 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
         const int32_t gi = gk[k];
         const int32_t i = i0 + k;
         double F = Fv[k];
-        if (lds_pay) {
+        if (PROM_ORD_EXP & 1) {
+        } else if (lds_pay) {
           for (int32_t j = i + 1; j < n && !sHead[j]; ++j) F += sF[(int32_t)(skey[j] & 0xffffffull)] / fs;
         } else {
           for (int32_t j = i + 1; j < n && !sHead[j]; ++j) F += sF[j];
         }
         double* r = mo + (int64_t)gi * ST;
-        if constexpr (ST == 2) {   // one 16-byte store (lanes' records are scattered: fewer store instructions)
+        if (PROM_ORD_EXP & 2) {
+        } else if constexpr (ST == 2) {   // one 16-byte store (lanes' records are scattered: fewer store instructions)
           *reinterpret_cast<double2*>(r) = make_double2(F, Nv[k][0]);
         } else {
           r[0] = F;
@@ -1062,9 +1068,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           // (tail records share one B slot: counted per thread and added once per wavefront below)
           const double Ag = ak[k] * (1.0 - 0x1p-38);
           if (i >= ncand) ++tailB;
-          else atomicAdd(&hB[env_slot(bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28))], 1);
-          atomicAdd(&hA[env_slot(Ag)], 1);
-          if constexpr (K % 2 == 0) {   // 16-byte stores (wmom rows are K doubles, 16-byte aligned)
+          else if (!(PROM_ORD_EXP & 4)) atomicAdd(&hB[env_slot(bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28))], 1);
+          if (!(PROM_ORD_EXP & 4)) atomicAdd(&hA[env_slot(Ag)], 1);
+          if (PROM_ORD_EXP & 2) {
+          } else if constexpr (K % 2 == 0) {   // 16-byte stores (wmom rows are K doubles, 16-byte aligned)
             double2* mv = reinterpret_cast<double2*>(mm + (int64_t)gi * K);
 #pragma unroll
             for (int m = 0; m < K; m += 2) mv[m / 2] = make_double2(M.c[m] * msum[m], M.c[m + 1] * msum[m + 1]);
@@ -1074,6 +1081,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           }
         }
       }
+      PROM_TS(o * 16 + 10);
       {
         const int32_t tw = (int32_t)(wave_reduce_f((float)tailB, [](float a, float b) { return a + b; }) + 0.5f);
         if (lane == 0 && tw > 0) atomicAdd(&hB[env_slot(btail * (1.0 + 0x1p-28))], tw);
@@ -1083,7 +1091,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       if (tid < K) {
         mm[(int64_t)G * K + tid] = 0.0;
       }
-      __syncthreads();
+      lds_barrier();
       PROM_TS(o * 16 + 4);
       // tab_t[v] = #{g : B_g >= X_v} = sum of hB over slots >= v + 1 (and likewise tab_h from hA):
       // one workgroup suffix scan over kEnvN + 2 slots, kEnvN / kWBlock per thread
@@ -1099,7 +1107,7 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       int32_t bex = dpp_mov<0x130>(bin), aex = dpp_mov<0x130>(ain);   // wave_shl:1
       if (lane == 63) { bex = 0; aex = 0; }
       if (lane == 0) { pi_[wid][0] = bin; pi_[wid][1] = ain; }
-      __syncthreads();
+      lds_barrier();
       int32_t bc = bex + hB[kEnvN + 1], ac = aex + hA[kEnvN + 1];
       for (int w = NW - 1; w > wid; --w) { bc += pi_[w][0]; ac += pi_[w][1]; }
       int32_t* et = wenv + (int64_t)o * 2 * kEnvN;
@@ -2154,7 +2162,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // bounds (k_qbounds).  Correct (test_fused_sigma) but slower on C3: 122 us for the fused tau kernel and
   // 1 ms for the bounds' node scans against 48 + 28 us for k_sigma_rows + k_tau_p (DESIGN.md "Tried").
   const char* fenv = std::getenv("PROM_FUSED");
-  const bool fused = pre_sigma && sig_rows > 1 && tr.sig_seg_ok && tr.plan && tr.n_atoms <= 4 &&
+  const bool fused = pre_sigma && !tr.uniform_shift && tr.sig_seg_ok && tr.plan && tr.n_atoms <= 4 &&
                      fenv && std::atoi(fenv) != 0;
   const int32_t nsig = tr.n_atoms;                 // species the column kernel resamples
   const int32_t na = msp ? 1 : tr.n_atoms;         // species the ordering and tau kernels see
@@ -2181,7 +2189,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     const unsigned chord_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
     // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
     // orbital Doppler shift with sigma segments: the rows come from their own kernel (k_sigma_rows)
-    const bool rows_seg = pre_sigma && sig_rows > 1 && tr.sig_seg_ok;
+    const bool rows_seg = pre_sigma && !tr.uniform_shift && tr.sig_seg_ok;   // (one row per phase, even one phase)
     // fused with the polynomial rows: k_sigma_poly still gives the half-tile Q ranges (no rows stored)
     const bool fused_poly = fused && tr.sig_deg > 0;
     const bool sig_fork = rows_seg && (!fused || fused_poly) && rs.aux && rs.ev_fork && rs.ev_join;
@@ -2308,7 +2316,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     if (sig_after_order) launch_rows(s, tr, rs, nsig, sig_rows, msp, nullptr);
     if (pre_sigma) {
       // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
-      if (sig_rows > 1 && tr.sig_seg_ok && (!fused || tr.sig_deg > 0) && rs.aux && rs.ev_join)
+      if (!tr.uniform_shift && tr.sig_seg_ok && (!fused || tr.sig_deg > 0) && rs.aux && rs.ev_join)
         PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
       const dim3 gw((unsigned)((n_wtiles + kBlock - 1) / kBlock), (unsigned)tr.n_orb);
 #define PROM_WIN(NSV)                                                                                    \

@@ -75,3 +75,25 @@ def test_shard_mode_is_one_ranks_work(tmp_path):
     part = np.load(os.path.join(out, "R_rank0.npy"))
     assert rg["w0"] > 0 and rg["w1"] == s1[2].shape[1]
     assert np.array_equal(part, s1[2][:, rg["w0"]:rg["w1"]])
+
+
+@pytest.mark.parametrize("config", ["C2", "C4"])
+def test_phase_shard_is_full_runs_rows(config, tmp_path):
+    """bench.py --shard r/N --shard-axis phase: rank r's orbital phases over every wavelength; its R is
+    the single-rank run's rows [o0, o1) bit for bit (phases are independent: per-phase columns, ordering,
+    sigma row and tau)."""
+    res1, (s1,) = _bench(str(tmp_path), 1, config)
+    out = os.path.join(str(tmp_path), "pshard")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1", "--config", config,
+           "--shard", "1/2", "--shard-axis", "phase", "--no-cpu-baseline", "--no-projection", "--dump-R", out]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    res = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["scaling"] == "strong" and "phases [" in res["config"]["workload"]
+    assert res["config"]["parallelism"].startswith("phase shards")
+    with open(os.path.join(out, "range_rank0.json")) as fh:
+        rg = json.load(fh)
+    part = np.load(os.path.join(out, "R_rank0.npy"))
+    n_orb = s1[2].shape[0]
+    assert rg["w0"] == 0 and rg["w1"] == s1[2].shape[1] and 0 < rg["o0"] < rg["o1"] == n_orb
+    assert np.array_equal(part, s1[2][rg["o0"]:rg["o1"]], equal_nan=True)

@@ -30,6 +30,30 @@ def test_shard_for_rank_empty_tail():
     assert sharding.shard_for_rank(300, 4, 0) == (0, 256)
 
 
+@pytest.mark.parametrize("parts", [1, 2, 3, 8])
+def test_phase_subset_slices_every_per_phase_array(parts):
+    """Phase shards (bench.py --shard-axis phase): split over phases with unit alignment covers them once;
+    phase_subset slices exactly the per-phase inputs and shares the chord ones."""
+    n = 8
+    orb = np.linspace(-0.1, 0.1, n)
+    host = {"orb": orb, "y": np.arange(5.0), "z": np.arange(5.0), "fout": np.ones(5), "planet_y": orb * 2,
+            "moon_y": np.vstack([orb * 3, orb * 4]), "moon_R": np.ones(2),
+            "scenarios": [{"shift": 1 + orb * 1e-5, "body_x": orb * 5, "body_y": 0.0, "n_tabulated": np.ones((5, 3))},
+                          {"shift": 1 + orb * 2e-5}]}
+    s = sharding.split(n, parts, align=1)
+    assert s[0][0] == 0 and s[-1][1] == n and len(s) == min(parts, n)
+    for o0, o1 in s:
+        h = sharding.phase_subset(host, o0, o1)
+        assert np.array_equal(h["orb"], orb[o0:o1]) and np.array_equal(h["planet_y"], orb[o0:o1] * 2)
+        assert h["moon_y"].shape == (2, o1 - o0) and np.array_equal(h["moon_y"][1], orb[o0:o1] * 4)
+        assert np.array_equal(h["scenarios"][0]["shift"], 1 + orb[o0:o1] * 1e-5)
+        assert np.array_equal(h["scenarios"][0]["body_x"], orb[o0:o1] * 5) and h["scenarios"][0]["body_y"] == 0.0
+        assert h["scenarios"][0]["n_tabulated"] is host["scenarios"][0]["n_tabulated"]
+        assert np.array_equal(h["scenarios"][1]["shift"], 1 + orb[o0:o1] * 2e-5)
+        assert h["y"] is host["y"] and h["fout"] is host["fout"]
+    assert len(host["orb"]) == n   # the input is not modified
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -44,12 +44,13 @@ for it in range(3):
 a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
 n_orb = len(host["orb"])
 print("k_order step times (us, workgroup of each phase, in time order; stamps 0 start, 7 loads issued+landed, "
-      "1 classify+scan, 2 sort, 5 fetch+per-key work, 6 scans, 3 combine, 4 records, 8 tables+end)")
+      "1 classify+scan, 2 sort, 5 fetch+per-key work, 6 scans, 3 combine, 9 forward, 10 records, 4 tail+barrier, "
+      "8 tables+end)")
 for o in range(n_orb):
-    t = a[o * 16: o * 16 + 9]
+    t = a[o * 16: o * 16 + 11]
     if t[0] == 0:
         continue
-    idx = sorted((i for i in range(9) if t[i] != 0), key=lambda i: t[i])   # stamps in time order
+    idx = sorted((i for i in range(11) if t[i] != 0), key=lambda i: t[i])   # stamps in time order
     d = ["%d->%d %5.2f" % (i, j, (t[j] - t[i]) * 0.01) for i, j in zip(idx, idx[1:])]
     print("  phase %2d: total %6.2f  steps %s" % (o, (t[8] - t[0]) * 0.01, " | ".join(d)))
 kt = a[65536:600000 - (600000 - 65536) % 8].reshape(-1, 8)
