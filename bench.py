@@ -108,7 +108,7 @@ def tau_bytes_per_launch(n_wav: int, n_orb: int, n_sigma: int, sigma_rows: int =
     return 8 * n_orb * n_wav + 8 * n_wav * n_sigma * sigma_rows
 
 
-def latest_profile_traffic(kernel: str, config: str):
+def latest_profile_traffic(kernel: str, config: str, suffix: str = ""):
     """Measured HBM bytes per launch of ``kernel`` on ``config`` from the newest committed rocprofv3 PMC
     summary (profiles/r*_<config>_traffic.json, written by tools/bench_traffic.sh through
     tools/traffic_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
@@ -120,7 +120,7 @@ def latest_profile_traffic(kernel: str, config: str):
         except Exception:
             continue
         for name, v in d.items():
-            if name.startswith(kernel):
+            if name.startswith(kernel) and name.endswith(suffix):
                 return v.get("hbm_bytes_per_launch")
     return None
 
@@ -389,11 +389,13 @@ def main():
     value = total_pts * args.steps / elapsed
 
     # variant // 10: 3 planned tau kernel on sigma rows, 5 / 6 planned with the Doppler sigma fused in (exp10 /
-    # polynomial lookups)
+    # polynomial lookups), 7 fused Doppler rows (k_sigma_poly integrates the light windows; k_tau_p takes the
+    # heavy half tiles only)
     tv = st.get("tau_kernel_variant", 0) // 10
     fused = tv in (5, 6)
+    sig_tau = tv == 7
     mol = bool(getattr(prob, "n_molecules", 0))
-    tau_kernel = "k_tau_mol" if mol else ("k_tau_p" if tv in (3, 5, 6) else "k_tau_w")
+    tau_kernel = "k_tau_mol" if mol else ("k_tau_p" if tv in (3, 5, 6, 7) else "k_tau_w")
     # k_tau_p in the pipelined loop: its span on the device clock (first workgroup start -> last workgroup end)
     tau_ms_events = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
     dev_ms = ms_runs[:, 3][np.isfinite(ms_runs[:, 3])] if len(ms_runs) else np.zeros(0)
@@ -424,9 +426,14 @@ def main():
     tau_bytes = tau_bytes_per_launch(n_w, n_orb, 0 if fused else n_atoms, sigma_rows) + (8 * n_w if fused else 0)
     flops_unit = flops_per_eval(n_atoms) + (6 * n_x if mol else 0)
     tau_ms_iso = kms.get("tau")
-    kernels[tau_kernel] = dict(hbm(tau_bytes, tau_ms_iso) or {}, ms=tau_ms_iso, ms_pipelined_loop=tau_ms_loop,
-                               exp_evals=evals, exp_per_s=(evals / (tau_ms_iso * 1e-3)) if tau_ms_iso else None,
-                               valu_tflops=(evals * flops_unit / (tau_ms_iso * 1e-3) / 1e12) if tau_ms_iso else None)
+    if sig_tau:
+        # heavy half tiles only (line cores: windows of > 8 records, spread over the chip); their share of R and
+        # of the exponentials is not counted on the host, so no byte roofline
+        kernels[tau_kernel] = {"bound": "latency", "ms": tau_ms_iso, "role": "heavy half tiles of the fused rows"}
+    else:
+        kernels[tau_kernel] = dict(hbm(tau_bytes, tau_ms_iso) or {}, ms=tau_ms_iso, ms_pipelined_loop=tau_ms_loop,
+                                   exp_evals=evals, exp_per_s=(evals / (tau_ms_iso * 1e-3)) if tau_ms_iso else None,
+                                   valu_tflops=(evals * flops_unit / (tau_ms_iso * 1e-3) / 1e12) if tau_ms_iso else None)
     if mol:
         # SURVEY.md 8d rule (ii): per chord-wavelength n_x table lookups (P-lerp + 10^v + FMA) against the
         # measured table-exp rate (profiles/r02u_fp64_exp_peak.json: 2.8e12/s)
@@ -440,10 +447,18 @@ def main():
         # and their zero flags written, the wavelengths and the refined tables' nodes (x, log10 sigma) read
         out_rows = 1 if merged else prob.n_atoms
         nodes = table_nodes_in_range(tr, host, w0, w1)
-        sig_bytes = 8 * sigma_rows * out_rows * n_w + (sigma_rows * n_w if merged else 0) + 8 * n_w + 16 * nodes
         lookups = sigma_rows * n_w * prob.n_atoms
-        kernels["k_sigma"] = dict(hbm(sig_bytes, kms["sigma"]), ms=kms["sigma"], lookups=lookups, table_nodes=nodes,
-                                  lookups_per_s=lookups / (kms["sigma"] * 1e-3))
+        if sig_tau:
+            # fused rows: R written (every point but the heavy half tiles' -- counted whole), the wavelengths and
+            # the table nodes read; no Y rows or zero flags
+            sig_bytes = 8 * n_orb * n_w + 8 * n_w + 16 * nodes
+            kernels["k_sigma_tau"] = dict(hbm(sig_bytes, kms["sigma"]), ms=kms["sigma"], lookups=lookups,
+                                          table_nodes=nodes, lookups_per_s=lookups / (kms["sigma"] * 1e-3),
+                                          exp_evals_both_kernels=evals)
+        else:
+            sig_bytes = 8 * sigma_rows * out_rows * n_w + (sigma_rows * n_w if merged else 0) + 8 * n_w + 16 * nodes
+            kernels["k_sigma"] = dict(hbm(sig_bytes, kms["sigma"]), ms=kms["sigma"], lookups=lookups, table_nodes=nodes,
+                                      lookups_per_s=lookups / (kms["sigma"] * 1e-3))
     if kms.get("columns"):
         dens = n_orb * n_pr * n_x * len(host["scenarios"])
         col_bytes = 8 * n_orb * n_pr * prob.n_atoms + 4 * n_orb * n_pr + 8 * (3 * n_pr + n_x)
@@ -462,7 +477,11 @@ def main():
     cand = [k for k in kernels if kernels[k].get("bound") != "latency"] or list(kernels)
     dom = max(cand, key=lambda k: kernels[k].get("ms") or 0.0)
     dk = kernels[dom]
-    traffic = latest_profile_traffic("prom::" + dom, cfg_name)
+    # rocprofv3 kernel names: the fused rows are k_sigma_poly<..., true>, the row kernels k_sigma_poly<..., false>
+    # (or k_sigma_rows)
+    sym, suffix = {"k_sigma_tau": ("prom::k_sigma_poly", ", true>"), "k_sigma": ("prom::k_sigma", "")}.get(
+        dom, ("prom::" + dom, ""))
+    traffic = latest_profile_traffic(sym, cfg_name, suffix)
     # latency of one run alone on an idle device (host clock: submit, kernels, synchronize; no stats
     # instrumentation), median of 20 -- what one retrieval sample waits for with inputs resident; not `value`
     dev.transit_set(prob)

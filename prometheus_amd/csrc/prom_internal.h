@@ -178,6 +178,28 @@ struct SigTabs4 {
   SigTabDev t[4];
 };
 
+// The integration half of the fused Doppler-row kernel (k_sigma_poly with TAU, prom_sigma.hip): k_order's
+// per-phase plan and the run's outputs.  One effective absorber (merged species, or one species).
+struct TauArgs {
+  const int32_t* counts;     // [n_orb][kCnt]
+  const int32_t* wenv;       // [n_orb][2][kEnvN] threshold -> record tables
+  const double* wmom;        // [n_orb][n_pr + 1][K] suffix tail moments
+  const double* recs;        // chord-order records {F, N} [n_orb][n_pr][2]
+  const double* mrecs;       // sorted / merged records, same layout
+  const int32_t* act_ip;     // [n_orb][n_pr] chord positions (exact path)
+  const double* fout;        // [n_pr] F_out (exact path)
+  const double* tfrac;       // [n_orb] transparent fraction
+  const double* fsum;        // [n_orb] F_out sum (exact path)
+  double* R;                 // [n_orb][n_wav]
+  double* sigh;              // [n_orb][n_wav]: Y of the heavy half tiles (read by k_tau_p's heavy entries)
+  int4* hlist;               // heavy entries: small list [hcap], then big list [hcap]
+  int32_t* hcnt;             // their counts (zeroed by k_columns8)
+  unsigned long long* evals; // [64] exp-evaluation counters (stats runs) or null
+  int64_t hcap;
+  int32_t n_pr, n_tiles;     // chords per phase, 128-wavelength tiles
+  double nscale;             // the effective absorber's 1 / c (tail polynomial argument q = Y nscale)
+};
+
 struct AtomTable {
   bool live = false;     // slot in use (prom_table_free releases it for reuse)
   DevBuf x, y;
@@ -385,7 +407,8 @@ void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const 
 // the same rows with e^a polynomials over the tables' {x, 10^y, ln10 slope, x_next} records (prom_sigma.hip)
 void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                        int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
-                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop);
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop,
+                       const TauArgs* tau = nullptr);
 // prom_transit_set: mark the sigma segments whose guess is numpy's bracket for every target (kind |= 4)
 void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                       int32_t n_rows, SigSeg* seg, int32_t* flags);

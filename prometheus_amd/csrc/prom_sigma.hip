@@ -259,15 +259,20 @@ constexpr bool kSigNoStore = PROM_SIG_NOSTORE != 0;   // profiling only: no sigm
 // The rows accumulate Y (merged species) or their Q sum in registers, species after species.  Oversize
 // blocks (fb, dispatched first): records read from the global table (one 32-byte record, a second only for
 // lanes whose bracket is the guess +- 1), or sigma_poly_of without a guess.
-template <int NSIG, int D, bool MG, int R>
+// TAU (fused Doppler path, one effective absorber: merged species or one species): no rows are stored; after
+// the Q ranges the workgroup integrates its (row, half tile) windows itself (k_windows' window choice and
+// k_tau_p's static-unit arithmetic, so R is bit for bit that of the row path) and hands the heavy half tiles
+// (window > kHeavy records) to k_tau_p as entries, storing Y for those half tiles only.
+template <int NSIG, int D, bool MG, int R, bool TAU>
 __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTabs4 tabv, const PolyCoef pc,
                                                        const double* __restrict__ wav, int64_t n_wav,
                                                        int32_t n_rows, const SigSeg* __restrict__ seg,
                                                        const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
                                                        int32_t n_rc, double* __restrict__ sig, float4* __restrict__ tq,
                                                        int32_t merge_sp, double nscale_m, uint8_t* __restrict__ zfl,
-                                                       int32_t parts, int32_t rf) {
+                                                       int32_t parts, int32_t rf, const TauArgs ta) {
   static_assert(R == 4 || R == 8 || R == 16, "4, 8 or 16 rows per workgroup");
+  static_assert(!TAU || MG || NSIG == 1, "the fused integration takes one effective absorber");
   // per staged species: [0, kSigSeg) {x_k, x_{k+1}}, [kSigSeg, 2 kSigSeg) {E_k, L_k}
   __shared__ double2 slds[2 * kSigSeg * (kSigMode == 1 ? NSIG : 1)];
   double2* sxr = slds;
@@ -315,6 +320,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
   const double lam = wav[live ? w : n_wav - 1];
   double acc[R];        // merged: Y = sum_s chi_s sigma_s;  else: Q = sum_s max(sigma_s / c_s, 0)
   uint32_t zb = 0;      // merged: bit r set when some chi_s sigma_s is not > 0
+  double sv[(TAU && !MG) ? R : 1];   // TAU, one species: the row's sigma (acc holds its Q)
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0;
   constexpr int kPre = kSigSeg / kBlock;   // mode 3: records per thread and species (slices <= kSigSeg nodes)
@@ -379,7 +385,8 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
         if (!(cv > 0.0)) zb |= 1u << r;
         acc[r] += cv;
       } else {
-        if (sig && live && orow < rlim) sig[((int64_t)orow * nse + s) * n_wav + w] = v;
+        if constexpr (TAU) sv[r] = v;
+        else if (sig && live && orow < rlim) sig[((int64_t)orow * nse + s) * n_wav + w] = v;
         const double qs = v * nsc;
         acc[r] += qs > 0.0 ? qs : 0.0;
       }
@@ -452,7 +459,7 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
     const int32_t orow = r0 + r;
     double Qv;
     if constexpr (MG) {
-      if (!kSigNoStore && sig && live && orow < rlim) {
+      if (!TAU && !kSigNoStore && sig && live && orow < rlim) {
         sig[(int64_t)orow * n_wav + w] = acc[r];
         zfl[(int64_t)orow * n_wav + w] = (zb >> r) & 1u;
       }
@@ -465,6 +472,13 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
   }
   static_assert(sizeof(double2) * 2 * kSigSeg >= sizeof(float) * R * kBlock, "Q staging fits over the slices");
   float* sq = reinterpret_cast<float*>(slds);   // [R][kBlock]
+  __shared__ float2 sqr[TAU ? R * 4 : 1];       // TAU: the (row, half tile) Q ranges
+  double etv[TAU ? 4 : 1];
+  if constexpr (TAU) {
+    // the exp table 2^(i/1024) (the even entries of the 2^(i/2048) table), in flight during the reduction
+#pragma unroll
+    for (int m = 0; m < 4; ++m) etv[m] = kExp2TableDev[2 * (tid + kBlock * m)];   // kBlock == 256
+  }
   __syncthreads();   // every lane's lookups done: the slices are free
 #pragma unroll
   for (int r = 0; r < R; ++r) sq[r * kBlock + tid] = qv[r];
@@ -482,8 +496,138 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
     if (TPH >= 8) { mn = fminf(mn, dpp_movf<0x141>(mn)); mx = fmaxf(mx, dpp_movf<0x141>(mx)); }   // row_half_mirror
     if (TPH >= 16) { mn = fminf(mn, dpp_movf<0x140>(mn)); mx = fmaxf(mx, dpp_movf<0x140>(mx)); }  // row_mirror
     const int64_t hw2 = wb * (kBlock / 64) + h;
-    if (pp == 0 && r0 + r < rlim && hw2 < n_halves)
+    if constexpr (TAU) {
+      if (pp == 0) sqr[r * 4 + h] = q_range(mn, mx);
+    } else if (pp == 0 && r0 + r < rlim && hw2 < n_halves) {
       reinterpret_cast<float2*>(tq)[(int64_t)(r0 + r) * n_halves + hw2] = q_range(mn, mx);
+    }
+  }
+  if constexpr (TAU) {
+    __syncthreads();   // the Q staging is read: the slices' LDS takes the exp table and the record buffers
+    double* sexp = reinterpret_cast<double*>(slds);   // [1024]
+#pragma unroll
+    for (int m = 0; m < 4; ++m) sexp[tid + kBlock * m] = etv[m];
+    __syncthreads();
+    constexpr int K = Monos<1>::K;              // tail moments of one effective absorber
+    constexpr int RB = 2 * kHeavy;              // record doubles of a light window ({F, N} x <= kHeavy)
+    constexpr int WB = R * (RB + K);            // LDS doubles per wavefront: its rows' records and moments
+    static_assert(sizeof(double2) * 2 * kSigSeg >= sizeof(double) * (1024 + 4 * WB), "exp table + buffers fit");
+    const int hh = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wavefront's half tile of the block
+    const int lane = tid & 63;
+    double* srb = sexp + 1024 + WB * hh;        // [R][RB] records, then [R][K] moments
+    double* smm = srb + R * RB;
+    const int64_t tl = wb * 2 + (hh >> 1);                      // its 128-wavelength tile
+    const bool live1 = tl * kTW + 64 < n_wav;                   // the tile's second half holds wavelengths
+    const bool wave_live = tl < ta.n_tiles && ((hh & 1) == 0 || live1);
+    if (wave_live) {
+      // (A) lane r < rcap: row r's tile window (k_windows: the union of the tile's halves' Q ranges), flags and
+      //     transparent fraction; a heavy row's entry (its own half's window) goes to the lists here
+      int32_t wh = 0, wt = 0, wfl = 0;
+      double wtf = 0.0;
+      if (lane < rcap) {
+        const int32_t o = r0 + lane;
+        const int32_t* c = ta.counts + o * kCnt;
+        const int32_t nact = c[0], nnf = c[3], G = c[4];
+        const bool sorted = c[5] != 0, wtab = c[6] != 0;
+        wtf = ta.tfrac[o];
+        const int32_t pfl = (sorted ? 1 : 0) | (nnf ? 4 : 0);
+        const int32_t t_all = sorted ? G : nact;
+        const int32_t* hB = ta.wenv + (int64_t)o * 2 * kEnvN;
+        const int32_t* hA = hB + kEnvN;
+        auto window_of = [&](float ql, float qh, int32_t* hp, int32_t* tp) {
+          int32_t h = 0, t = t_all;
+          if (wtab && ql >= 0.0f) {
+            const int vt = env_floor((float)tail_eps<1>() / qh * (1.0f - 0x1p-20f));
+            const int vh = env_floor((float)kTauSat / ql * (1.0f + 0x1p-20f));
+            t = vt > kEnvVmax ? 0 : (vt < kEnvVmin ? G : hB[vt - kEnvVmin]);
+            h = vh >= kEnvVmax ? 0 : hA[vh + 1 < kEnvVmin ? 0 : vh + 1 - kEnvVmin];
+          }
+          *hp = h < t ? h : t;
+          *tp = t;
+        };
+        const float2 qa = sqr[lane * 4 + (hh & 2)], qb = sqr[lane * 4 + (hh | 1)];
+        const bool bad = qa.x < 0.0f || (live1 && qb.x < 0.0f);
+        const float ql = bad ? -1.0f : (live1 ? fminf(qa.x, qb.x) : qa.x);
+        const float qh = bad ? 0.0f : (live1 ? fmaxf(qa.y, qb.y) : qa.y);
+        window_of(ql, qh, &wh, &wt);
+        wfl = pfl | ((wtab && wt < G) ? 2 : 0);
+        if (!(wfl & 4) && wt - wh > kHeavy) {
+          const float2 qo = sqr[lane * 4 + hh];
+          int32_t h2, t2;
+          window_of(qo.x, qo.y, &h2, &t2);
+          const int32_t ff = pfl | ((wtab && t2 < G) ? 2 : 0);
+          const int big = t2 - h2 > kChunk ? 1 : 0;
+          const int32_t idx = atomicAdd(&ta.hcnt[big], 1);
+          ta.hlist[(big ? ta.hcap : 0) + idx] = make_int4((int32_t)(wb * 4 + hh), h2, t2, ff | (o << 8));
+        }
+      }
+      // (B) the light rows' records and tail moments into the wavefront's LDS, 64 / R lanes per row
+      {
+        constexpr int LPR = 64 / R;
+        const int gr = lane / LPR, j = lane % LPR;
+        const int32_t h = __shfl(wh, gr, 64), t = __shfl(wt, gr, 64), fl = __shfl(wfl, gr, 64);
+        if (gr < rcap && !(fl & 4) && t - h <= kHeavy) {
+          const int32_t o = r0 + gr;
+          const double* src = ((fl & 1) ? ta.mrecs : ta.recs) + ((int64_t)o * ta.n_pr + h) * 2;
+          for (int e = j; e < 2 * (t - h); e += LPR) srb[gr * RB + e] = src[e];
+          if (fl & 2) {
+            const double* mp = ta.wmom + ((int64_t)o * (ta.n_pr + 1) + t) * K;
+            for (int k = j; k < K; k += LPR) smm[gr * K + k] = mp[k];
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // (C) per row: the light window (k_tau_p's static unit: records in order, the tail polynomial, the
+      //     transparent sum), the exact chord-order path, or Y for a heavy half tile's entry
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r >= rcap) break;
+        const int32_t o = r0 + r;
+        double yv;
+        if constexpr (MG) yv = acc[r];
+        else yv = sv[r];
+        const int32_t h = lane_read(wh, r), t = lane_read(wt, r), fl = lane_read(wfl, r);
+        const double tf = lane_read(wtf, r);
+        const int32_t n = t - h;
+        if (!(fl & 4) && n <= kHeavy) {
+          const double* rb = srb + r * RB;
+          const double sy = yv * kM1024Ln2;
+          double a = 0.0;
+          for (int32_t q = 0; q < n; ++q) a = acc_exp1024(a, rb[2 * q], rb[2 * q + 1] * sy, sexp);
+          if (fl & 2) {
+            double mm[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) mm[k] = smm[r * K + k];
+            const double qv[1] = {yv * ta.nscale};
+            a += tail_eval<1>(mm, qv);
+          }
+          a += tf;
+          if (live) ta.R[(int64_t)o * n_wav + w] = a;
+          if (ta.evals) {
+            const int nl = __popcll(__ballot(live));
+            if (lane == 0) atomicAdd(&ta.evals[(blockIdx.x * 4 + hh) & 63], (unsigned long long)n * (unsigned long long)nl);
+          }
+        } else if (fl & 4) {
+          // non-finite column densities: the reference's chord order with ocml exp
+          const double* rb = ta.recs + (int64_t)o * ta.n_pr * 2;
+          const int32_t* ipl = ta.act_ip + (int64_t)o * ta.n_pr;
+          const bool zr = MG && ((zb >> r) & 1u);
+          double a = 0.0;
+          for (int32_t i = 0; i < t; ++i) {
+            const double N = rb[2 * i + 1];
+            double tau = N * yv;
+            if (zr && !__builtin_isfinite(N)) tau = __builtin_nan("");
+            a = a + ta.fout[ipl[i]] * exp(-tau);
+          }
+          const double fs = ta.fsum[o];
+          if (live) ta.R[(int64_t)o * n_wav + w] = (a + tf * fs) / fs;
+        } else if (live) {
+          ta.sigh[(int64_t)o * n_wav + w] = yv;   // heavy: k_tau_p integrates the entry from this row
+        }
+      }
+    }
   }
 #ifdef PROM_TRACE
   // per workgroup: start, end (wall clock, 10 ns), block | lds << 32 | front << 33, first row | HW_ID << 32
@@ -570,7 +714,8 @@ void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const d
 
 void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                        int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
-                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop,
+                       const TauArgs* tau) {
   const int32_t n_blk = (int32_t)grid_for(n_wav);
   // rows per workgroup: PROM_SIG_POLY_ROWS when set at build time, else 8 for several species (their lookups
   // fill the workgroup) and 4 for one (more workgroups in flight)
@@ -591,40 +736,40 @@ void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4&
   const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
   const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
   const PolyCoef& pc = poly_coef();
-#define PROM_SIGP(NS, DG)                                                                                          \
-  do {                                                                                                             \
-    if (merge_sp && R == 8)                                                                                        \
-      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, true, 8>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, tabv, \
-                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts, RF); \
-    else if (merge_sp)                                                                                             \
-      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, true, 4>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, tabv, \
-                            pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, parts, RF); \
-    else if (R == 8)                                                                                               \
-      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, false, 8>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0,   \
-                            tabv, pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, \
-                            parts, RF);                                                                                \
-    else                                                                                                           \
-      hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, false, 4>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0,   \
-                            tabv, pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, \
-                            parts, RF);                                                                                \
+  const TauArgs ta = tau ? *tau : TauArgs{};
+  PROM_REQUIRE(!tau || merge_sp || nsig == 1, "fused Doppler rows: one effective absorber only");
+#define PROM_SIGK(NS, DG, MGV, RV, TV)                                                                         \
+  hipExtLaunchKernelGGL((k_sigma_poly<NS, DG, MGV, RV, TV>), dim3(nb), dim3(kBlock), 0, s, ev_start, ev_stop, 0, \
+                        tabv, pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, sig, tq, merge_sp, nscale_m, zfl, \
+                        parts, RF, ta)
+  // the fused (TAU) instantiations: merged species (NS >= 2) and one unmerged species (NS == 1)
+#define PROM_SIGP(NS, DG, MGT)                                                                                 \
+  do {                                                                                                         \
+    if (tau) {                                                                                                 \
+      if (R == 8) PROM_SIGK(NS, DG, MGT, 8, true); else PROM_SIGK(NS, DG, MGT, 4, true);                     \
+    } else if (merge_sp && R == 8) PROM_SIGK(NS, DG, true, 8, false);                                         \
+    else if (merge_sp) PROM_SIGK(NS, DG, true, 4, false);                                                      \
+    else if (R == 8) PROM_SIGK(NS, DG, false, 8, false);                                                       \
+    else PROM_SIGK(NS, DG, false, 4, false);                                                                   \
   } while (0)
-#define PROM_SIGP_D(NS)                      \
+#define PROM_SIGP_D(NS, MGT)                 \
   switch (deg) {                             \
-    case 4: PROM_SIGP(NS, 4); break;         \
-    case 6: PROM_SIGP(NS, 6); break;         \
-    case 8: PROM_SIGP(NS, 8); break;         \
-    case 10: PROM_SIGP(NS, 10); break;       \
-    case 12: PROM_SIGP(NS, 12); break;       \
-    default: PROM_SIGP(NS, 14); break;       \
+    case 4: PROM_SIGP(NS, 4, MGT); break;    \
+    case 6: PROM_SIGP(NS, 6, MGT); break;    \
+    case 8: PROM_SIGP(NS, 8, MGT); break;    \
+    case 10: PROM_SIGP(NS, 10, MGT); break;  \
+    case 12: PROM_SIGP(NS, 12, MGT); break;  \
+    default: PROM_SIGP(NS, 14, MGT); break;  \
   }
   switch (nsig) {
-    case 1: PROM_SIGP_D(1) break;
-    case 2: PROM_SIGP_D(2) break;
-    case 3: PROM_SIGP_D(3) break;
-    default: PROM_SIGP_D(4) break;
+    case 1: PROM_SIGP_D(1, false) break;
+    case 2: PROM_SIGP_D(2, true) break;
+    case 3: PROM_SIGP_D(3, true) break;
+    default: PROM_SIGP_D(4, true) break;
   }
 #undef PROM_SIGP_D
 #undef PROM_SIGP
+#undef PROM_SIGK
   PROM_HIP(hipGetLastError());
 }
 

@@ -2166,6 +2166,13 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      fenv && std::atoi(fenv) != 0;
   const int32_t nsig = tr.n_atoms;                 // species the column kernel resamples
   const int32_t na = msp ? 1 : tr.n_atoms;         // species the ordering and tau kernels see
+  // fused Doppler rows (default; PROM_SIG_TAU=0: off): the polynomial row kernel runs after k_order and
+  // integrates every light (row, half tile) window itself -- no Y rows / zero flags in HBM, no k_windows --
+  // leaving the heavy half tiles to k_tau_p's entry lists.  One effective absorber (merged species or one
+  // species), planned windows.
+  const char* stenv = std::getenv("PROM_SIG_TAU");
+  const bool sig_tau = pre_sigma && !fused && !tr.uniform_shift && tr.sig_seg_ok && tr.sig_deg > 0 && tr.plan &&
+                       na == 1 && !(stenv && std::atoi(stenv) == 0);
   const ColArgs& cargs = msp ? tr.colargs_m : tr.colargs;
   const int32_t n_terms = msp ? 1 : tr.n_terms;
   const double* smax = msp ? tr.sigma_max_m.as<double>() : tr.sigma_max_dev.as<double>();
@@ -2192,7 +2199,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     const bool rows_seg = pre_sigma && !tr.uniform_shift && tr.sig_seg_ok;   // (one row per phase, even one phase)
     // fused with the polynomial rows: k_sigma_poly still gives the half-tile Q ranges (no rows stored)
     const bool fused_poly = fused && tr.sig_deg > 0;
-    const bool sig_fork = rows_seg && (!fused || fused_poly) && rs.aux && rs.ev_fork && rs.ev_join;
+    const bool sig_fork = rows_seg && !sig_tau && (!fused || fused_poly) && rs.aux && rs.ev_fork && rs.ev_join;
     const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
     const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
     // the sigma rows do not depend on the columns or the ordering: with a second stream for the slot they
@@ -2200,7 +2207,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // join before the tile windows.  The fork point is taken before the column kernel is queued (the rows
     // wait only for the slot's previous run); PROM_SIGMA_FIRST=1 queues them before the column kernel.
     const bool sig_first = !sig_fork || (std::getenv("PROM_SIGMA_FIRST") && std::atoi(std::getenv("PROM_SIGMA_FIRST")));
-    sig_after_order = rows_seg && !fused && !sig_fork && rs.sig_late && wpath;
+    sig_after_order = rows_seg && !fused && !sig_fork && (rs.sig_late || sig_tau) && wpath;
     if (sig_fork) {
       PROM_HIP(hipEventRecord(rs.ev_fork, s));
       PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
@@ -2292,7 +2299,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
   hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, kp_start(tr, PROM_K_ORDER, nullptr),    \
-                     kp_stop(tr, PROM_K_ORDER, pre_sigma ? nullptr : ev_ord), 0,                          \
+                     kp_stop(tr, PROM_K_ORDER, (pre_sigma && !sig_tau) ? nullptr : ev_ord), 0,             \
                      rs.flags.as<int32_t>(),                                                              \
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
                      tr.window ? 1 : 0, tabs4, rs.recs.as<double>(),                                     \
@@ -2313,8 +2320,40 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       default: PROM_CHW(4); break;
     }
 #undef PROM_CHW
-    if (sig_after_order) launch_rows(s, tr, rs, nsig, sig_rows, msp, nullptr);
-    if (pre_sigma) {
+    if (sig_tau) {
+      // 2b'. fused rows: sigma, Q ranges, windows and the light windows' integration in one kernel
+      TauArgs ta{};
+      ta.counts = rs.counts.as<int32_t>();
+      ta.wenv = rs.wenv.as<int32_t>();
+      ta.wmom = rs.wmom.as<double>();
+      ta.recs = rs.recs.as<double>();
+      ta.mrecs = rs.mrecs.as<double>();
+      ta.act_ip = rs.act_ip.as<int32_t>();
+      ta.fout = tr.cfout.as<double>();
+      ta.tfrac = rs.tsum.as<double>();
+      ta.fsum = rs.fsum.as<double>();
+      ta.R = rs.R.as<double>();
+      ta.sigh = rs.sig.as<double>();
+      ta.hlist = rs.hlist.as<int4>();
+      ta.hcnt = rs.hcnt.as<int32_t>();
+      ta.evals = tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr;
+      ta.hcap = hcap;
+      ta.n_pr = tr.n_pr;
+      ta.n_tiles = n_wtiles;
+      ta.nscale = tabs4.t[0].nscale;
+      hipEvent_t e0 = ev_tau0, e1 = nullptr;
+      if (tr.kprof) {
+        tr.kprof_mask |= 1u << PROM_K_SIGMA;
+        e0 = tr.kprof[2 * PROM_K_SIGMA];
+        e1 = tr.kprof[2 * PROM_K_SIGMA + 1];
+      }
+      launch_sigma_poly(s, nsig, tr.sig_deg, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
+                        tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb, nullptr,
+                        rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale, nullptr, e0, e1, &ta);
+    } else if (sig_after_order) {
+      launch_rows(s, tr, rs, nsig, sig_rows, msp, nullptr);
+    }
+    if (pre_sigma && !sig_tau) {
       // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
       if (!tr.uniform_shift && tr.sig_seg_ok && (!fused || tr.sig_deg > 0) && rs.aux && rs.ev_join)
         PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
@@ -2428,14 +2467,15 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
 #undef PROM_OCC
         resident = std::max(1, cus) * std::max(1, nb);   // workgroups resident at once
       }
-      const int64_t n_static = (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
+      // fused rows: the static units are done; the grid takes the heavy entries only
+      const int64_t n_static = sig_tau ? 0 : (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
       const int64_t blocks = std::max<int64_t>((n_static + kTP - 1) / kTP, resident);
-      *variant = 30 + (na <= 4 ? na : 0);
-      unsigned long long* tsp = (tr.ts_out && blocks <= tr.ts_cap) ? tr.ts_out : nullptr;
+      *variant = (sig_tau ? 70 : 30) + (na <= 4 ? na : 0);
+      unsigned long long* tsp = (tr.ts_out && blocks <= tr.ts_cap && !sig_tau) ? tr.ts_out : nullptr;
       tr.ts_blocks = tsp ? (int32_t)blocks : 0;
 #define PROM_TAUP(NSV, PHV, FSV)                                                                        \
   hipExtLaunchKernelGGL((k_tau_p<NSV, PHV, FSV>), dim3((unsigned)blocks), dim3(kBlock), 0, s,           \
-                        kp_start(tr, PROM_K_TAU, ev_tau0), kp_stop(tr, PROM_K_TAU, ev ? ev[3] : nullptr), 0, \
+                        kp_start(tr, PROM_K_TAU, sig_tau ? nullptr : ev_tau0), kp_stop(tr, PROM_K_TAU, ev ? ev[3] : nullptr), 0, \
                         tabs4, rs.sig.as<double>(),                                                      \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
                         rs.wmom.as<double>(), rs.trec.as<int4>(), n_wtiles, rs.hlist.as<int4>(),        \

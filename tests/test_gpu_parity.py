@@ -343,6 +343,7 @@ def test_planned_tau_within_window_bound(dev, name, monkeypatch):
         cfg = json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
     monkeypatch.setenv("PROM_FUSED", "0")   # both read the same sigma rows (test_fused_sigma: the fused path)
+    monkeypatch.setenv("PROM_SIG_TAU", "0")  # k_tau_p's static units (the fused rows: test_sigma_tau_bitwise)
     monkeypatch.setenv("PROM_TAU_PLAN", "1")
     R_p = tr.sumOverChords(devices=[0])
     st_p = tr.last_stats[-1]
@@ -370,6 +371,7 @@ def test_fused_sigma(dev, name, monkeypatch):
     from prometheus_amd import configs
     cfg = configs.get(name) if name == "C3" else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
+    monkeypatch.setenv("PROM_SIG_TAU", "0")   # the sigma-row path as the comparison
     monkeypatch.setenv("PROM_FUSED", "1")
     R_f = tr.sumOverChords(devices=[0])
     st_f = tr.last_stats[-1]
@@ -394,6 +396,39 @@ def test_fused_sigma(dev, name, monkeypatch):
     assert np.max(np.abs(R_fe - R_re)) <= 1e-13
 
 
+@pytest.mark.parametrize("name,merge", [("C3r", "1"), ("C3r", "0"), ("C4r", "1"), ("exomoon", "1"), ("C3", "1"),
+                                        ("C4", "1"), ("C4x10", "1")])
+def test_sigma_tau_bitwise(dev, name, merge, monkeypatch):
+    """The fused Doppler rows (default, variant 7x: k_sigma_poly integrates every light (row, half tile) window
+    itself after k_order and hands the heavy half tiles to k_tau_p's entry lists; no Y rows in HBM) against
+    the row path (PROM_SIG_TAU=0: Y rows, k_windows, k_tau_p's static units).  Same windows, records, order
+    and arithmetic: R is bitwise equal and the exponentials counted are the same.  Several unmerged species
+    (merge 0) and the exp10 rows keep the row path."""
+    from prometheus_amd import configs
+    cfg = configs.get(name) if name in ("C3", "C4", "C4x10") else json.loads(str(load("transit_" + name)["config"]))
+    tr = _product_transit(cfg)
+    monkeypatch.setenv("PROM_SPECIES_MERGE", merge)
+    monkeypatch.setenv("PROM_FUSED", "0")
+    monkeypatch.setenv("PROM_SIG_TAU", "1")
+    R_f = tr.sumOverChords(devices=[0])
+    st_f = tr.last_stats[-1]
+    monkeypatch.setenv("PROM_SIG_TAU", "0")
+    R_r = tr.sumOverChords(devices=[0])
+    st_r = tr.last_stats[-1]
+    print(name, "merge", merge, "variants", st_f["tau_kernel_variant"], st_r["tau_kernel_variant"], "exp evals",
+          st_f["exp_evals"], st_r["exp_evals"])
+    assert st_r["tau_kernel_variant"] // 10 == 3
+    # (reduced tables whose |a| bound needs too high a degree keep the exp10 rows, and with them the row path)
+    if merge == "0":
+        assert st_f["tau_kernel_variant"] // 10 == 3
+    elif name in ("C3", "C4", "C4x10", "exomoon"):
+        assert st_f["tau_kernel_variant"] // 10 == 7
+    assert np.array_equal(R_f, R_r, equal_nan=True)
+    assert st_f["exp_evals"] == st_r["exp_evals"]
+    if name not in ("C3", "C4", "C4x10"):
+        assert rel(R_f, load("transit_" + name)["R"]) < R_TOL
+
+
 @pytest.mark.parametrize("name", ["C2r", "C2"])
 def test_species_merge(dev, name, monkeypatch):
     """Constituents of one density scenario collapse into one effective absorber (tau = N Y with
@@ -416,7 +451,7 @@ def test_species_merge(dev, name, monkeypatch):
         assert rel(R_m, load("transit_" + name)["R"]) < R_TOL
 
 
-@pytest.mark.parametrize("plan", ["1", "0", "doppler"])
+@pytest.mark.parametrize("plan", ["1", "0", "doppler", "doppler_rows"])
 def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     """A user density plugin (host-tabulated n(c, x)) with one infinite sample: that chord's column is
     inf, its phase takes the exact chord-order path (ocml exp, no windows), e^{-inf sigma} = 0 and
@@ -426,10 +461,12 @@ def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     from prometheus_amd import configs
     # "doppler": orbital Doppler shift on, so the merged Na + K absorber takes the fused path (the tau kernel
     # looks sigma and the zero flags up itself)
-    monkeypatch.setenv("PROM_TAU_PLAN", "1" if plan == "doppler" else plan)
+    # fused rows (k_sigma_poly integrates the exact phase itself); "doppler_rows": the sigma-row path
+    monkeypatch.setenv("PROM_TAU_PLAN", "1" if plan.startswith("doppler") else plan)
+    monkeypatch.setenv("PROM_SIG_TAU", "0" if plan == "doppler_rows" else "1")
     cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
                           res_low=5e-9, res_high=1e-10)
-    cfg["Fundamentals"]["DopplerOrbitalMotion"] = plan == "doppler"
+    cfg["Fundamentals"]["DopplerOrbitalMotion"] = plan.startswith("doppler")
     tr = _product_transit(cfg)
     scen, dop, grids = O.from_setup(cfg)
     base = scen[0]
