@@ -1214,6 +1214,29 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
         for (float v : tqv) tqs += v;
         std::fprintf(stderr, "prom: windows sum %lld flags sum %lld heavy small %d big %d tq sum %.9g\n", win, fl, hc[0],
                      hc[1], tqs);
+        // heavy entries' record counts: small list, then big list (hcap = n_orb * 2 * n_tiles entries each)
+        const int64_t hcap = (int64_t)tr.n_orb * 2 * n_wtiles;
+        for (int b = 0; b < 2; ++b) {
+          const int32_t ne = hc[b];
+          if (ne <= 0 || !rs.hlist.p) continue;
+          std::vector<int32_t> hl(4 * (size_t)ne);
+          PROM_HIP(hipMemcpy(hl.data(), rs.hlist.as<int32_t>() + 4 * (b ? hcap : 0), sizeof(int32_t) * hl.size(),
+                             hipMemcpyDeviceToHost));
+          long long sum = 0;
+          int32_t mx = 0;
+          std::vector<int32_t> hist(8, 0);   // records: <=64, <=128, <=256, <=512, <=1024, <=2048, <=4096, more
+          for (int32_t i = 0; i < ne; ++i) {
+            const int32_t n = hl[4 * i + 2] - hl[4 * i + 1];
+            sum += n;
+            mx = std::max(mx, n);
+            int k = 0;
+            while (k < 7 && n > (64 << k)) ++k;
+            ++hist[k];
+          }
+          std::fprintf(stderr, "prom: %s entries %d records sum %lld max %d  hist(<=64,128,..,4096,more) %d %d %d %d %d %d %d %d\n",
+                       b ? "big" : "small", ne, sum, mx, hist[0], hist[1], hist[2], hist[3], hist[4], hist[5], hist[6],
+                       hist[7]);
+        }
       }
       if (std::getenv("PROM_DEBUG"))
         for (int32_t o = 0; o < tr.n_orb; ++o)
