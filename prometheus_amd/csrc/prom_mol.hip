@@ -10,7 +10,22 @@ namespace prom {
 // is formed once for every P node i into LDS; each (chord, sample) then costs one P interpolation
 // (uniform bracket from k_mol_prep), 10^v and an FMA.  Out-of-table samples (P, T or lambda) take the
 // fill value, i.e. sigma = 0, as in the reference.
-constexpr double kLog2Ten2048 = 0x1.a934f0979a371p+12;   // 2048 log2(10)
+constexpr double kLog2Ten256 = 0x1.a934f0979a371p+9;    // 256 log2(10)
+constexpr int kMolExpN = 256;                              // LDS exp table 2^(i/256) (2 KB: occupancy)
+
+// 2^(y/256) = 2^(k >> 8) T[k & 255] exp(d ln2/256), k = rint(y), d in [-1/2, 1/2], degree-5 Taylor
+// polynomial (truncation 9e-21 relative; acc_exp256's arithmetic without the accumulation)
+__device__ __forceinline__ double exp2_256(double y, const double* __restrict__ tab) {
+  const double k = __builtin_rint(y);
+  const int ki = (int)k;
+  const double d = y - k;
+  double p = __builtin_fma(d, kE256C5, kE256C4);
+  p = __builtin_fma(d, p, kE256C3);
+  p = __builtin_fma(d, p, kE256C2);
+  p = __builtin_fma(d, p, kE256C1);
+  p = __builtin_fma(d, p, 1.0);
+  return __builtin_amdgcn_ldexp(tab[ki & (kMolExpN - 1)], ki >> 8) * p;
+}
 
 template <int NSA, int EXPK>
 __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const SigTabDev* __restrict__ tabs,
@@ -27,10 +42,11 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
                                                     const int32_t* __restrict__ mip,
                                                     const double* __restrict__ mwp,
                                                     const double* __restrict__ mna, double* __restrict__ R) {
-  extern __shared__ double lds[];   // [2048] exp table | [n_mol][max_np][kBlock] u
+  extern __shared__ double lds[];   // [256] exp table 2^(i/256) | [n_mol][max_np][kBlock] u
   double* etab = lds;
-  double* ul = lds + PROM_EXP2_TABLE_N;
-  if (EXPK) fill_exp_table(etab);
+  double* ul = lds + kMolExpN;
+  if (EXPK)
+    for (int i = threadIdx.x; i < kMolExpN; i += kBlock) etab[i] = kExp2TableDev[i * (PROM_EXP2_TABLE_N / kMolExpN)];
   __syncthreads();
   const int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x;
   const bool live = w < n_wav;
@@ -99,7 +115,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
     }
     const int32_t* ipl = act_ip + (int64_t)o * n_pr;
     double acc = 0.0;
-    const double scale = exact ? 1.0 : kMinus2048OverLn2;
+    const double scale = exact ? 1.0 : kM256Ln2;
     int32_t ip_next = n_act > 0 ? ipl[0] : 0;
     for (int32_t ci = 0; ci < n_act; ++ci) {
       const double* r = rec + (int64_t)ci * ST;
@@ -115,20 +131,37 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
         const double* um = ul + (int64_t)m * max_np * kBlock + threadIdx.x;
         double sm = 0.0;
         // (uniform per wavefront: scalar loads, batched by the unroll)
+        if (EXPK && !exact) {
+          // table mode: v = u_i + t (u_{i+1} - u_i), 10^v = 2^(y/256) with y = v 256 log2(10) from the LDS table
+          // (relative error ~ |y| 2^-53 ln2/256 from the argument, ~1e-14 at the table's floor); the offset
+          // comes off once per chord, sum n (10^v - off) = sum n 10^v - off sum n (10^v >= off: no cancellation
+          // beyond off's own size)
+          double sn = 0.0;
 #pragma unroll 10
-        for (int32_t ix = 0; ix < n_x; ++ix) {
-          const int32_t pi = mip[base + ix];
-          if (pi < 0) continue;
-          const double tp = mwp[base + ix];
-          const double v = (1.0 - tp) * um[(int64_t)pi * kBlock] + tp * um[(int64_t)(pi + 1) * kBlock];
-          // 10^v: the LDS-table 2^(y/2048) with y = v 2048 log2(10) in table mode (relative error
-          // ~ |v| 2.3 2^-53 from the argument product, ~1e-14 at the table's floor), ocml otherwise
-          const double p10 = (EXPK && !exact) ? acc_exp2k(0.0, 1.0, v * kLog2Ten2048, etab) : exp10(v);
-          sm = __builtin_fma(mna[base + ix], p10 - d.offset, sm);
+          for (int32_t ix = 0; ix < n_x; ++ix) {
+            const int32_t pi = mip[base + ix];
+            if (pi < 0) continue;
+            const double tp = mwp[base + ix];
+            const double a = um[(int64_t)pi * kBlock], b = um[(int64_t)(pi + 1) * kBlock];
+            const double v = __builtin_fma(tp, b - a, a);
+            const double na = mna[base + ix];
+            sm = __builtin_fma(na, exp2_256(v * kLog2Ten256, etab), sm);
+            sn += na;
+          }
+          sm = __builtin_fma(-d.offset, sn, sm);
+        } else {
+#pragma unroll 10
+          for (int32_t ix = 0; ix < n_x; ++ix) {
+            const int32_t pi = mip[base + ix];
+            if (pi < 0) continue;
+            const double tp = mwp[base + ix];
+            const double v = (1.0 - tp) * um[(int64_t)pi * kBlock] + tp * um[(int64_t)(pi + 1) * kBlock];
+            sm = __builtin_fma(mna[base + ix], exp10(v) - d.offset, sm);
+          }
         }
         tau = tau + sm * delta_x;
       }
-      if (!exact) acc = acc_exp2k(acc, r[0], tau * scale, etab);
+      if (!exact) acc = acc_exp256(acc, r[0], tau * scale, etab);
       else acc = acc + fout[ip] * exp(-tau);
     }
     if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
@@ -148,7 +181,7 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
     PROM_REQUIRE(na <= 4, "transit: at most 4 atomic constituents next to molecular ones");
     int32_t max_np = 0;
     for (const auto& m : tr.mslots) max_np = std::max(max_np, m.n_p);
-    const size_t lds = PROM_EXP2_TABLE_N * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
+    const size_t lds = kMolExpN * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
     PROM_REQUIRE(lds <= 160 * 1024, "transit: molecular tables too large for the LDS staging (n_mol * n_p)");
     // prom_transit_kernel_ms: the kernel's own dispatch-packet events
     hipEvent_t kps = nullptr, kpe = nullptr;

@@ -429,27 +429,39 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
           if (r < rcap) emit(r, sigma_poly_of(tt[r], tb, pc, D));
       }
     } else {
-      double xk[R];
-      double2 el[R];
-      if (exact) {
+      // rows past rcap (a problem with fewer rows than R, e.g. one phase shard) are skipped; the guarded
+      // copy only runs then (the unguarded one keeps the rows' LDS reads free to overlap)
+      auto lds_rows = [&](auto guard) {
+        constexpr bool GD = decltype(guard)::value;
+        double xk[R];
+        double2 el[R];
+        if (exact) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            if (GD && r >= rcap) break;
+            const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
+            xk[r] = sx_[g].x;
+            el[r] = se_[g];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            if (GD && r >= rcap) break;
+            const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
+            const double2 xx = sx_[g];
+            const int32_t k = tt[r] < xx.x ? g - 1 : (tt[r] >= xx.y ? g + 1 : g);
+            xk[r] = sx_[k].x;
+            el[r] = se_[k];
+          }
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
-          xk[r] = sx_[g].x;
-          el[r] = se_[g];
+          if (GD && r >= rcap) break;
+          emit(r, __builtin_fma(el[r].x, exp_taylor<D>(el[r].y * (tt[r] - xk[r]), pc), -off));
         }
-      } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
-          const double2 xx = sx_[g];
-          const int32_t k = tt[r] < xx.x ? g - 1 : (tt[r] >= xx.y ? g + 1 : g);
-          xk[r] = sx_[k].x;
-          el[r] = se_[k];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) emit(r, __builtin_fma(el[r].x, exp_taylor<D>(el[r].y * (tt[r] - xk[r]), pc), -off));
+      };
+      if (rcap >= R) lds_rows(std::false_type{});
+      else lds_rows(std::true_type{});
     }
   }
   // rows' outputs, then their half-tile Q ranges through LDS (over the slices, no longer read)

@@ -1030,6 +1030,10 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
       PROM_TS(o * 16 + 9);
       // backward: moments
       int32_t tailB = 0;
+      // histogram counts run-length encoded per thread: its keys are consecutive in the sorted order, so their
+      // B and A slots are monotone and mostly shared -- one LDS atomic per run instead of one per key (lanes
+      // of a wavefront hitting one slot serialise)
+      int32_t runB = -1, nB = 0, runA = -1, nA = 0;
 #pragma unroll
       for (int k = kWPer - 1; k >= 0; --k) {
         if (k >= cnt) continue;
@@ -1067,9 +1071,26 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           // (tail records, unsorted behind every candidate: B = btail covers all of them)
           // (tail records share one B slot: counted per thread and added once per wavefront below)
           const double Ag = ak[k] * (1.0 - 0x1p-38);
-          if (i >= ncand) ++tailB;
-          else if (!(PROM_ORD_EXP & 4)) atomicAdd(&hB[env_slot(bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28))], 1);
-          if (!(PROM_ORD_EXP & 4)) atomicAdd(&hA[env_slot(Ag)], 1);
+          if (i >= ncand) {
+            ++tailB;
+          } else if (!(PROM_ORD_EXP & 4)) {
+            const int32_t sb = env_slot(bv[k] >= 1.0 ? ball : bv[k] * (1.0 + 0x1p-28));
+            if (sb != runB) {
+              if (nB) atomicAdd(&hB[runB], nB);
+              runB = sb;
+              nB = 0;
+            }
+            ++nB;
+          }
+          if (!(PROM_ORD_EXP & 4)) {
+            const int32_t sa = env_slot(Ag);
+            if (sa != runA) {
+              if (nA) atomicAdd(&hA[runA], nA);
+              runA = sa;
+              nA = 0;
+            }
+            ++nA;
+          }
           if (PROM_ORD_EXP & 2) {
           } else if constexpr (K % 2 == 0) {   // 16-byte stores (wmom rows are K doubles, 16-byte aligned)
             double2* mv = reinterpret_cast<double2*>(mm + (int64_t)gi * K);
@@ -1081,6 +1102,8 @@ __global__ void __launch_bounds__(kWBlock) k_order(const int32_t* __restrict__ f
           }
         }
       }
+      if (nB) atomicAdd(&hB[runB], nB);
+      if (nA) atomicAdd(&hA[runA], nA);
       PROM_TS(o * 16 + 10);
       {
         const int32_t tw = (int32_t)(wave_reduce_f((float)tailB, [](float a, float b) { return a + b; }) + 0.5f);
@@ -1670,6 +1693,14 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 6 : 4) k_tau_w(const SigTabs
 }
 
 // ---- planned tau integration ---------------------------------------------------------------------------
+// wavefronts per k_tau_p workgroup: a big heavy entry's 64-record chunks go round robin over them.  16 (one
+// 1024-thread workgroup per CU at the kernel's 92 VGPRs) measured no faster than 4 on C3's heavy entries
+// (17.2 against 16.1-16.4 us: half as many workgroups as big entries, so they take two each;
+// profiles/r03k_bench_C3.json), so 4 stays the default
+#ifndef PROM_TAU_WPG
+#define PROM_TAU_WPG 4
+#endif
+constexpr int kTauWpg = PROM_TAU_WPG;
 // k_tau_w gives every (128-wavelength tile, phase) one wavefront: the end of a run is set by the few
 // windows at line cores, which hold up to ~1,000 records (Doppler-shifted multi-line spectra) against a
 // median of zero.  k_tau_p instead takes k_order's plan:
@@ -1805,8 +1836,8 @@ __device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const 
 // blockIdx.x * 4 + wid < n_static): tile sw % n_tiles, phases 4 (sw / n_tiles) ...; round trip 1 = its
 // phases' tile records {h, t, flags, tail moments} (k_order), sigma at its 128 wavelengths (2 per lane), the
 // exp table; a second round trip only for the packed records of non-empty light windows.
-template <int NS, bool PH, int FS>
-__global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs4 tabv, const double* __restrict__ sig,
+template <int NS, bool PH, int FS, int WPG>
+__global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_tau_p(const SigTabs4 tabv, const double* __restrict__ sig,
                                                                    const double* __restrict__ recs,
                                                                    const double* __restrict__ mrecs,
                                                                    const int32_t* __restrict__ act_ip,
@@ -1834,19 +1865,21 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
   constexpr int MQ = (4 * K + 63) / 64;             // tail-moment loads per lane (four phases)
   constexpr int SR = PH ? 4 : 1;                    // sigma rows a static wavefront loads
   static_assert(4 * kHeavy * ST <= 2 * 64 * ST, "a group's packed records fit the wavefront's LDS slice");
-  __shared__ double srec[kTP][2 * 64 * ST];   // per wavefront: two chunks of 64 records
+  __shared__ double srec[WPG][2 * 64 * ST];   // per wavefront: two chunks of 64 records
   __shared__ double sexp[1024];                // 2^(i/1024)
-  __shared__ double spart[kTP][64];            // big entries: the wavefronts' partial sums
+  __shared__ double spart[WPG][64];            // big entries: the wavefronts' partial sums
 #ifdef PROM_TRACE
   const unsigned long long wt0 = wall_clock64();
   long long wrk = 0;
 #endif
-  double etv[4];
+  constexpr int NT = WPG * 64, EPT = 1024 / NT;   // threads, exp-table entries per thread
+  static_assert(EPT * NT == 1024, "the exp table splits evenly over the workgroup");
+  double etv[EPT];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) etv[m] = kExp2TableDev[2 * (threadIdx.x + kBlock * m)];   // kBlock == 256
+  for (int m = 0; m < EPT; ++m) etv[m] = kExp2TableDev[2 * (threadIdx.x + NT * m)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int32_t gw = blockIdx.x * kTP + wid;
+  const int32_t gw = blockIdx.x * WPG + wid;
   double* sr = srec[wid];
   // timed runs: the workgroup's first device-clock tick (the kernel's duration is the span over all)
   if (tstamp && threadIdx.x == 0) tstamp[2 * blockIdx.x] = wall_clock64();
@@ -1896,7 +1929,7 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
 #pragma unroll
   for (int p = 0; p < 4; ++p) tfv[p] = p < np ? tfrac[o0 + p] : 0.0;
 #pragma unroll
-  for (int m = 0; m < 4; ++m) sexp[threadIdx.x + kBlock * m] = etv[m];
+  for (int m = 0; m < EPT; ++m) sexp[threadIdx.x + NT * m] = etv[m];
   __syncthreads();
 
   // ---- big entries: one per workgroup at a time, chunks round robin over the four wavefronts
@@ -1921,9 +1954,9 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
 #pragma unroll
     for (int s = 0; s < NS; ++s) sy[0][s] = sgh[0][s] * kM1024Ln2;
     double acc[1] = {0.0};
-    tau_records<NS, 1>(sy, src, t - h, wid, kTP, nx, lane, sr, sexp, acc);
+    tau_records<NS, 1>(sy, src, t - h, wid, WPG, nx, lane, sr, sexp, acc);
     int32_t nrec = 0;   // records of the chunks this wavefront took
-    for (int32_t c0 = 64 * wid; c0 < t - h; c0 += 64 * kTP) nrec += min(64, t - h - c0);
+    for (int32_t c0 = 64 * wid; c0 < t - h; c0 += 64 * WPG) nrec += min(64, t - h - c0);
     const bool lva[1] = {lv};
     tau_count<1>(evals, gw, lane, nrec, lva);
 #ifdef PROM_TRACE
@@ -1932,7 +1965,9 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
     spart[wid][lane] = acc[0];
     __syncthreads();
     if (wid == 0) {
-      double r = ((spart[0][lane] + spart[1][lane]) + spart[2][lane]) + spart[3][lane];
+      double r = spart[0][lane];   // the wavefronts' partial sums in order: ((p0 + p1) + p2) + ...
+#pragma unroll
+      for (int q = 1; q < WPG; ++q) r += spart[q][lane];
       if (f4 & 2) {
         double qv[NS];
 #pragma unroll
@@ -1944,8 +1979,10 @@ __global__ void __launch_bounds__(kBlock, NS <= 2 ? 5 : 3) k_tau_p(const SigTabs
     }
     __syncthreads();
   }
-  // ---- small entries: one per wavefront
-  for (int32_t e = gw; e < nsmall; e += gridDim.x * kTP) {
+  // ---- small entries: one per wavefront, first to the wavefronts of workgroups that took no big entry
+  const int32_t nwv = (int32_t)gridDim.x * WPG;
+  const int32_t busy = (nbig < (int32_t)gridDim.x ? nbig : (int32_t)gridDim.x) * WPG;
+  for (int32_t e = (gw + nwv - busy) % nwv; e < nsmall; e += nwv) {
     const int4 en = hlist[e];
     const int32_t h = __builtin_amdgcn_readfirstlane(en.y), t = __builtin_amdgcn_readfirstlane(en.z);
     const int32_t f4 = __builtin_amdgcn_readfirstlane(en.w);
@@ -2447,7 +2484,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
         int dev = 0;
         PROM_HIP(hipGetDevice(&dev));
         PROM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-#define PROM_OCC(NSV, PHV, FSV) PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, PHV, FSV>, kBlock, 0))
+#define PROM_OCC(NSV, PHV, FSV) PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, PHV, FSV, kTauWpg>, kTauWpg * 64, 0))
         if (fused) {
           if (na == 1) {
             switch (fsv) { case 1: PROM_OCC(1, true, 1); break; case 2: PROM_OCC(1, true, 2); break;
@@ -2469,12 +2506,12 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       }
       // fused rows: the static units are done; the grid takes the heavy entries only
       const int64_t n_static = sig_tau ? 0 : (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
-      const int64_t blocks = std::max<int64_t>((n_static + kTP - 1) / kTP, resident);
+      const int64_t blocks = std::max<int64_t>((n_static + kTauWpg - 1) / kTauWpg, resident);
       *variant = (sig_tau ? 70 : 30) + (na <= 4 ? na : 0);
       unsigned long long* tsp = (tr.ts_out && blocks <= tr.ts_cap && !sig_tau) ? tr.ts_out : nullptr;
       tr.ts_blocks = tsp ? (int32_t)blocks : 0;
 #define PROM_TAUP(NSV, PHV, FSV)                                                                        \
-  hipExtLaunchKernelGGL((k_tau_p<NSV, PHV, FSV>), dim3((unsigned)blocks), dim3(kBlock), 0, s,           \
+  hipExtLaunchKernelGGL((k_tau_p<NSV, PHV, FSV, kTauWpg>), dim3((unsigned)blocks), dim3(kTauWpg * 64), 0, s, \
                         kp_start(tr, PROM_K_TAU, sig_tau ? nullptr : ev_tau0), kp_stop(tr, PROM_K_TAU, ev ? ev[3] : nullptr), 0, \
                         tabs4, rs.sig.as<double>(),                                                      \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
