@@ -382,7 +382,10 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
       const int32_t orow = r0 + r;
       if constexpr (MG) {
         const double cv = chi * v;
-        if (!(cv > 0.0)) zb |= 1u << r;
+        // (TAU: the zero flags are only needed by a phase with non-finite columns; its rows redo them there)
+        if constexpr (!TAU) {
+          if (!(cv > 0.0)) zb |= 1u << r;
+        }
         acc[r] += cv;
       } else {
         if constexpr (TAU) sv[r] = v;
@@ -625,7 +628,17 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_poly(const SigTa
           // non-finite column densities: the reference's chord order with ocml exp
           const double* rb = ta.recs + (int64_t)o * ta.n_pr * 2;
           const int32_t* ipl = ta.act_ip + (int64_t)o * ta.n_pr;
-          const bool zr = MG && ((zb >> r) & 1u);
+          // merged species: some chi_s sigma_s not > 0 at this (row, wavelength) -- the same records and
+          // arithmetic as the lookups above (sigma_seg_poly), so the same values
+          bool zr = false;
+          if constexpr (MG) {
+#pragma unroll
+            for (int s = 0; s < NSIG; ++s) {
+              const SigTabDev& tb = tabv.t[s];
+              const double v = sigma_seg_poly(tb.shift[o] * lam, tb, seg[wb * NSIG + s], pc, D);
+              zr = zr || !(tb.chi * v > 0.0);
+            }
+          }
           double a = 0.0;
           for (int32_t i = 0; i < t; ++i) {
             const double N = rb[2 * i + 1];
