@@ -437,7 +437,9 @@ def main():
     if mol:
         # SURVEY.md 8d rule (ii): per chord-wavelength n_x table lookups (P-lerp + 10^v + FMA) against the
         # measured table-exp rate (profiles/r02u_fp64_exp_peak.json: 2.8e12/s)
-        pow10 = st["active_chords"] * n_w * n_x
+        # (the device counts them in stats runs: exp_evals = the 10^v of in-table samples + one e^-tau per
+        # record and wavelength; out-of-table samples are skipped, k_mol_prep compacts them away)
+        pow10 = max(0, int(st["exp_evals"]) - int(st["tau_records"]) * n_w)
         kernels[tau_kernel].update(bound="fp64-exp", pow10_evals=pow10,
                                    pow10_per_s=pow10 / (tau_ms_iso * 1e-3) if tau_ms_iso else None,
                                    pow10_peak_per_s=2.815e12,

@@ -211,7 +211,8 @@ typedef struct prom_transit_stats {
   int64_t tau_records;         /* chord records the tau kernel integrates (after merging)     */
   int64_t exp_evals;           /* exp evaluations of the fused kernel (counted on the device:
                                   the windowed kernel evaluates only the records of each
-                                  wavefront's tau window; tau_records * n_wav without windows) */
+                                  wavefront's tau window; tau_records * n_wav without windows;
+                                  molecular problems add the 10^v of every in-table sample)   */
   int32_t tau_kernel_variant;  /* tens: 1 k_tau (table exp), 2 k_tau_w, 3 k_tau_p on sigma rows, 4 k_tau_rm
                                   (stellar spectrum), 5 / 6 k_tau_p with the Doppler sigma looked up in the
                                   kernel (exp10 / polynomial), 7 fused Doppler rows (k_sigma_poly integrates

@@ -41,7 +41,8 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
                                                     int32_t n_x, double delta_x,
                                                     const int32_t* __restrict__ mip,
                                                     const double* __restrict__ mwp,
-                                                    const double* __restrict__ mna, double* __restrict__ R) {
+                                                    const double* __restrict__ mna, double* __restrict__ R,
+                                                    unsigned long long* __restrict__ evals) {
   extern __shared__ double lds[];   // [256] exp table 2^(i/256) | [n_mol][max_np][kBlock] u
   double* etab = lds;
   double* ul = lds + kMolExpN;
@@ -59,6 +60,11 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
 #pragma unroll
   for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); sg[s] = 0.0; }
   int64_t whint[4] = {-1, -1, -1, -1};
+  unsigned long long npow = 0;   // stats runs: this lane's 10^v evaluations (in-table samples)
+  uint32_t inb = 0;              // bit m: molecular slot m has (T, lambda') inside its table
+  double lwprev[4];              // slot m's lambda' of the last u built in LDS (m < 4)
+#pragma unroll
+  for (int m = 0; m < 4; ++m) lwprev[m] = __builtin_nan("");
   const int64_t nc = (int64_t)n_orb * n_pr;
   for (int32_t o = o0; o < o1; ++o) {
     const bool exact = !EXPK || counts[o * kCnt + 3] != 0;
@@ -72,12 +78,18 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
         shv[s] = sh;
       }
     }
-    uint32_t inb = 0;   // bit m: molecular slot m has (T, lambda') inside its table
     for (int32_t m = 0; m < n_mol; ++m) {
       const MolSlotDev d = ms[m];
       int64_t it, iw;
       double tt, tw;
       const double lw = d.shift[o] * lam;
+      // the same lambda' as this lane's previous phase (no orbital Doppler shift, or an equal factor): u and
+      // the in-table bit are unchanged (T is the slot's own constant)
+      if (m < 4) {
+        if (lw == lwprev[m]) continue;
+        lwprev[m] = lw;
+      }
+      inb &= ~(1u << m);
       bool ok = rgi_bracket(d.T, d.n_t, d.temp, &it, &tt);
       if (ok) {
         // gallop the wavelength bracket from the previous phase's
@@ -130,6 +142,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
         const int64_t base = ((int64_t)m * nc + (int64_t)o * n_pr + ip) * n_x;
         const double* um = ul + (int64_t)m * max_np * kBlock + threadIdx.x;
         double sm = 0.0;
+        int32_t nin = 0;
         // (uniform per wavefront: scalar loads, batched by the unroll)
         if (EXPK && !exact) {
           // table mode: v = u_i + t (u_{i+1} - u_i), 10^v = 2^(y/256) with y = v 256 log2(10) from the LDS table
@@ -140,7 +153,8 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
 #pragma unroll 10
           for (int32_t ix = 0; ix < n_x; ++ix) {
             const int32_t pi = mip[base + ix];
-            if (pi < 0) continue;
+            if (pi < 0) break;   // (k_mol_prep: in-table samples first, then -1)
+            ++nin;
             const double tp = mwp[base + ix];
             const double a = um[(int64_t)pi * kBlock], b = um[(int64_t)(pi + 1) * kBlock];
             const double v = __builtin_fma(tp, b - a, a);
@@ -153,19 +167,22 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
 #pragma unroll 10
           for (int32_t ix = 0; ix < n_x; ++ix) {
             const int32_t pi = mip[base + ix];
-            if (pi < 0) continue;
+            if (pi < 0) break;
+            ++nin;
             const double tp = mwp[base + ix];
             const double v = (1.0 - tp) * um[(int64_t)pi * kBlock] + tp * um[(int64_t)(pi + 1) * kBlock];
             sm = __builtin_fma(mna[base + ix], exp10(v) - d.offset, sm);
           }
         }
         tau = tau + sm * delta_x;
+        npow += (unsigned)nin;
       }
       if (!exact) acc = acc_exp256(acc, r[0], tau * scale, etab);
       else acc = acc + fout[ip] * exp(-tau);
     }
     if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
   }
+  if (evals && live && npow) atomicAdd(&evals[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 63], npow);
 }
 
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg) {
@@ -193,7 +210,8 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
 #define PROM_TAUM(NSV, EK)                                                                                  \
   hipExtLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, kps, kpe, 0, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
                      max_np, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x,         \
-                     tr.delta_x, tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(), R)
+                     tr.delta_x, tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(), R, \
+                     tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr)
 #define PROM_TAUM_NS(EK)                \
   switch (na) {                         \
     case 0: PROM_TAUM(0, EK); break;    \

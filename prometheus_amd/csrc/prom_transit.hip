@@ -57,7 +57,11 @@ __global__ void k_mol_prep(const MolSlotDev* __restrict__ ms, int32_t n_mol, con
     const int64_t cc = c - (int64_t)m * nc;
     const MolSlotDev d = ms[m];
     const double* row = ntot + ((int64_t)d.scenario * nc + cc) * n_x;
+    // in-table samples are compacted to the front of the chord's row in sample order, then -1 (k_tau_mol
+    // stops there: out-of-table samples contribute nothing, so the sum over the kept ones is unchanged)
     double col = 0.0;
+    const int64_t k0 = ((int64_t)m * nc + cc) * n_x;
+    int32_t nin = 0;
     for (int32_t ix = 0; ix < n_x; ++ix) {
       const double n = row[ix];
       double P = n * d.k_B * d.temp;
@@ -65,13 +69,15 @@ __global__ void k_mol_prep(const MolSlotDev* __restrict__ ms, int32_t n_mol, con
       int64_t i;
       double t;
       const bool in = rgi_bracket(d.P, d.n_p, P, &i, &t);
-      const int64_t k = ((int64_t)m * nc + cc) * n_x + ix;
-      mip[k] = in ? (int32_t)i : -1;
-      mwp[k] = t;
+      if (!in) continue;
       const double na = n * d.chi;
-      mna[k] = na;
-      if (in) col += na * delta_x;
+      mip[k0 + nin] = (int32_t)i;
+      mwp[k0 + nin] = t;
+      mna[k0 + nin] = na;
+      ++nin;
+      col += na * delta_x;
     }
+    for (int32_t ix = nin; ix < n_x; ++ix) mip[k0 + ix] = -1;
     molcol[(int64_t)m * nc + cc] = col;
   }
 }
