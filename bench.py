@@ -391,9 +391,12 @@ def main():
     # variant // 10: 3 planned tau kernel on sigma rows, 5 / 6 planned with the Doppler sigma fused in (exp10 /
     # polynomial lookups), 7 fused Doppler rows (k_sigma_poly integrates the light windows; k_tau_p takes the
     # heavy half tiles only)
+    # 8 transmission curves (prom_tcurve.hip: k_tc_phase, k_tc_table, then k_sigma_tc looks sigma up and
+    # evaluates each phase's curve; no tau kernel)
     tv = st.get("tau_kernel_variant", 0) // 10
     fused = tv in (5, 6)
     sig_tau = tv == 7
+    tcurve = tv == 8
     mol = bool(getattr(prob, "n_molecules", 0))
     tau_kernel = "k_tau_mol" if mol else ("k_tau_p" if tv in (3, 5, 6, 7) else "k_tau_w")
     # k_tau_p in the pipelined loop: its span on the device clock (first workgroup start -> last workgroup end)
@@ -426,7 +429,9 @@ def main():
     tau_bytes = tau_bytes_per_launch(n_w, n_orb, 0 if fused else n_atoms, sigma_rows) + (8 * n_w if fused else 0)
     flops_unit = flops_per_eval(n_atoms) + (6 * n_x if mol else 0)
     tau_ms_iso = kms.get("tau")
-    if sig_tau:
+    if tcurve:
+        pass
+    elif sig_tau:
         # heavy half tiles only (line cores: windows of > 8 records, spread over the chip); their share of R and
         # of the exponentials is not counted on the host, so no byte roofline
         kernels[tau_kernel] = {"bound": "latency", "ms": tau_ms_iso, "role": "heavy half tiles of the fused rows"}
@@ -450,7 +455,13 @@ def main():
         out_rows = 1 if merged else prob.n_atoms
         nodes = table_nodes_in_range(tr, host, w0, w1)
         lookups = sigma_rows * n_w * prob.n_atoms
-        if sig_tau:
+        if tcurve:
+            # transmission curves: R written (every point), the wavelengths and the table nodes read; the
+            # per-phase curve tables (kTcD coefficients per octave) are L2-resident and not counted
+            sig_bytes = 8 * n_orb * n_w + 8 * n_w + 16 * nodes
+            kernels["k_sigma_tc"] = dict(hbm(sig_bytes, kms["sigma"]), ms=kms["sigma"], lookups=lookups,
+                                         table_nodes=nodes, lookups_per_s=lookups / (kms["sigma"] * 1e-3))
+        elif sig_tau:
             # fused rows: R written (every point but the heavy half tiles' -- counted whole), the wavelengths and
             # the table nodes read; no Y rows or zero flags
             sig_bytes = 8 * n_orb * n_w + 8 * n_w + 16 * nodes
@@ -466,10 +477,13 @@ def main():
         col_bytes = 8 * n_orb * n_pr * prob.n_atoms + 4 * n_orb * n_pr + 8 * (3 * n_pr + n_x)
         kernels["k_columns"] = dict(hbm(col_bytes, kms["columns"]), bound="latency", ms=kms["columns"],
                                     density_evals=dens, density_evals_per_s=dens / (kms["columns"] * 1e-3))
-    for k, name in (("order", "k_order"), ("windows", "k_windows")):
+    for k, name in (("order", "k_tc_build" if tcurve else "k_order"), ("windows", "k_windows")):
         if kms.get(k):
             kernels[name] = {"bound": "latency", "ms": kms[k],
-                             "workgroups": n_orb if k == "order" else None}
+                             "workgroups": n_orb if (k == "order" and not tcurve) else None}
+    if tcurve and kms.get("order"):
+        # every active chord at 16 Chebyshev nodes of each table octave (one table exp per four octaves)
+        kernels["k_tc_build"].update(node_evals=evals, node_evals_per_s=evals / (kms["order"] * 1e-3))
     # path level: what any implementation must move -- R written, wavelengths and table nodes read -- over
     # the measured step
     path_bytes = 8 * n_orb * n_w + 8 * n_w + (16 * table_nodes_in_range(tr, host, w0, w1) if prob.n_atoms else 0)
@@ -481,8 +495,8 @@ def main():
     dk = kernels[dom]
     # rocprofv3 kernel names: the fused rows are k_sigma_poly<..., true>, the row kernels k_sigma_poly<..., false>
     # (or k_sigma_rows)
-    sym, suffix = {"k_sigma_tau": ("prom::k_sigma_poly", ", true>"), "k_sigma": ("prom::k_sigma", "")}.get(
-        dom, ("prom::" + dom, ""))
+    sym, suffix = {"k_sigma_tau": ("prom::k_sigma_poly", ", true>"), "k_sigma": ("prom::k_sigma", ""),
+                   "k_sigma_tc": ("prom::k_sigma_tc", "")}.get(dom, ("prom::" + dom, ""))
     traffic = latest_profile_traffic(sym, cfg_name, suffix)
     # latency of one run alone on an idle device (host clock: submit, kernels, synchronize; no stats
     # instrumentation), median of 20 -- what one retrieval sample waits for with inputs resident; not `value`

@@ -7,7 +7,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = ["csrc/prom_api.hip", "csrc/prom_transit.hip", "csrc/prom_fn.hip", "csrc/prom_mol.hip",
+SOURCES = ["csrc/prom_api.hip", "csrc/prom_transit.hip", "csrc/prom_fn.hip", "csrc/prom_mol.hip", "csrc/prom_tcurve.hip",
            "csrc/prom_rm.hip", "csrc/prom_sigma.hip"]
 HEADERS = ["csrc/prom_internal.h", "csrc/prom_device.h", "csrc/faddeeva.h", "csrc/exp2_table.h",
            "csrc/exp2_table_body.h", "../include/prom_hip.h"]

@@ -50,8 +50,10 @@ prom::DensityDev to_dev(const prom_density_model& m) {
   d.kind = m.kind;
   for (int i = 0; i < 8; ++i) d.p[i] = m.p[i];
   // power law with a small integral exponent q (the setup files' q_esc, e.g. 6): (R / r)^q by repeated
-  // squaring on the device (pad = q + 1) instead of a general pow
-  if (m.kind == PROM_DENSITY_POWERLAW && m.p[2] >= 0.0 && m.p[2] <= 64.0 && m.p[2] == std::floor(m.p[2]))
+  // squaring on the device (pad = q + 1) instead of a general pow.  Each squaring doubles the relative error
+  // already carried, so the error grows about linearly in q: q <= 8 keeps it within ~8 ulp of pow
+  // (test_density_plugins, q = 6); larger exponents take pow
+  if (m.kind == PROM_DENSITY_POWERLAW && m.p[2] >= 0.0 && m.p[2] <= 8.0 && m.p[2] == std::floor(m.p[2]))
     d.pad = (int32_t)m.p[2] + 1;
   return d;
 }
@@ -611,6 +613,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       tr.plan = !(e && std::atoi(e) == 0);
       const char* m = std::getenv("PROM_SPECIES_MERGE");
       tr.species_merge_ok = !(m && std::atoi(m) == 0);   // narrowed below
+      const char* tc = std::getenv("PROM_TCURVE");
+      tr.tcurve = !(tc && std::atoi(tc) == 0);            // narrowed below
     }
     PROM_REQUIRE(pb->n_pr < (1 << 24), "transit: n_pr must be < 2^24");
     tr.terms.clear();
@@ -788,6 +792,24 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       stg.add(tr.sigtab, st.data(), (int64_t)st.size(), s);
       tr.qbound_v = 0.0;
       for (size_t i = 0; i < st.size(); ++i) tr.qbound_v += tr.atom_sigma_max[i] * st[i].nscale;
+      // transmission curves (prom_tcurve.hip): one effective absorber on the fast column path, windows allowed
+      // (PROM_OPT_NO_WINDOW / OCML_EXP keep the exact validation paths), no stellar spectrum
+      {
+        const bool cols8e = n_mol == 0 && tr.n_x <= 64 && (int32_t)tr.terms.size() <= 8 && tr.n_sc <= 4;
+        tr.tcurve = tr.tcurve && cols8e && tr.exp_mode && tr.window && !pb->has_star && n_atoms >= 1 &&
+                    (n_atoms == 1 || tr.species_merge_ok);
+        // Y bound (merged: sum_s chi_s sigma_max_s; one species: sigma_max) and the octave cap of the tables:
+        // q = Y N_max <= Y_bound * (the column bound 1 / c), one octave of margin
+        const double yb = !tr.tcurve ? 0.0 : (n_atoms == 1 ? tr.atom_sigma_max[0] : smax_m);
+        const double nb = !tr.tcurve ? 0.0 : (n_atoms == 1 ? st[0].nscale : tr.sigtab_m.t[0].nscale);
+        tr.tc_ybound = (std::isfinite(yb) && yb > 0.0) ? yb : 0.0;
+        const double qb = yb * nb;
+        int lg = prom::kTcMaxOctaves;
+        if (std::isfinite(qb) && qb > 0.0) lg = std::max(1, std::min(prom::kTcMaxOctaves, std::ilogb(qb) + 7 + 2));
+        // PROM_TC_LG (tests): a lower cap, so that points above the table take the exact per-point sum
+        if (const char* e = std::getenv("PROM_TC_LG")) lg = std::max(1, std::min(lg, std::atoi(e)));
+        tr.tc_lg = lg;
+      }
       // PROM_OPT_DOPPLER_ROWS: one sigma row per phase even when the factors are equal (a phase shard of a
       // problem with orbital Doppler shift takes the full problem's sigma path: bitwise equal rows)
       tr.uniform_shift = !(pb->options & PROM_OPT_DOPPLER_ROWS);
@@ -809,7 +831,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         key_gen.push_back(ctx->tables[t.table].gen);
         key_sh.insert(key_sh.end(), sh.begin() + t.scenario * n_orb, sh.begin() + (t.scenario + 1) * n_orb);
       }
-      const bool seg_reuse = !tr.uniform_shift && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
+      // (without orbital Doppler shift only the transmission-curve path reads them)
+      const bool want_seg = !tr.uniform_shift || tr.tcurve;
+      const bool seg_reuse = want_seg && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
                              key_sh == tr.seg_key_sh && (int64_t)tr.seg_key_wav.size() == tr.n_wav &&
                              std::memcmp(tr.seg_key_wav.data(), pb->wavelength, sizeof(double) * tr.n_wav) == 0;
       // reused segments stay valid only if this set completes; a throw below must not leave the key
@@ -818,7 +842,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       seg_key_keep = seg_reuse;   // the stored key stays as it is (re-validated at the end)
       if (seg_reuse) {
         tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
-      } else if (!tr.uniform_shift && n_atoms >= 1 && n_atoms <= 4) {
+      } else if (want_seg && n_atoms >= 1 && n_atoms <= 4) {
         tr.seg_key_valid = false;
         const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
         std::vector<prom::SigSeg> seg(nb * n_atoms, prom::SigSeg{0, 0, 0, 0, 0.0, 0.0});
@@ -929,7 +953,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       }
       am *= 1.0 + 1e-6;
       for (int D = 4; fin && D <= 14; D += 2) {
-        double term = 1.0;   // am^(D+1) / (D+1)!
+        // Lagrange remainder relative to e^a: am^(D+1) / (D+1)! e^|a| (a < 0 carries the e^|a| factor)
+        double term = std::exp(am);
         for (int i = 1; i <= D + 1; ++i) term *= am / (double)i;
         if (term <= std::ldexp(1.0, -53)) { tr.sig_deg = D; break; }
       }
@@ -1059,6 +1084,19 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       rs.tsum.ensure(sizeof(double) * n_orb);
       rs.fsum.ensure(sizeof(double) * n_orb);
       rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);
+      if (tr.tcurve) {
+        // k_tc_build: ~512 chords per part (at most 8), 4 octaves per chain
+        tr.tc_parts = (int32_t)std::max<int64_t>(1, std::min<int64_t>(8, tr.n_pr / 512));
+        const int64_t n_ch = (tr.tc_lg + 3) / 4;
+        rs.tc_hdr.ensure(sizeof(double) * n_orb * prom::kTcHdr);
+        rs.tc_tab.ensure(sizeof(double) * n_orb * tr.tc_lg * prom::kTcD);
+        rs.tc_part.ensure(sizeof(double) * n_orb * n_ch * 8 * (4 * prom::kTcD + 8));
+        const size_t cb = sizeof(int32_t) * n_orb * n_ch;
+        if (rs.tc_cnt.cap < cb) {
+          rs.tc_cnt.ensure(cb);
+          PROM_HIP(hipMemsetAsync(rs.tc_cnt.p, 0, rs.tc_cnt.cap, s));
+        }
+      }
     }
     tr.last = 0;
     stg.flush(ctx, s);

@@ -467,8 +467,8 @@ __device__ __forceinline__ double density_at(const DensityDev& m, double xv, dou
       const double xr = m.p[1] / r;
       double pw;
       if (m.pad > 0) {
-        // x^q for an integral q by binary exponentiation (q uniform): at most 2 log2(q) rounded products,
-        // within a few ulp of numpy's pow (gasProperties.py:241 (R/r)**q)
+        // x^q for an integral q <= 8 by binary exponentiation (q uniform): at most 2 log2(q) rounded products,
+        // within ~8 ulp of numpy's pow (gasProperties.py:241 (R/r)**q)
         pw = 1.0;
         double b = xr;
         for (int32_t e = m.pad - 1; e > 0; e >>= 1) {

@@ -200,6 +200,25 @@ struct TauArgs {
   double nscale;             // the effective absorber's 1 / c (tail polynomial argument q = Y nscale)
 };
 
+// The transmission-curve path (prom_tcurve.hip): per phase a header of kTcHdr doubles and kTcD Chebyshev
+// coefficients per octave of q = Y N_max.
+constexpr int kTcHdr = 16;
+constexpr int kTcD = 16;
+enum : int { kTcHNmax = 0, kTcHTfrac = 1, kTcHFsum = 2, kTcHT0 = 3 /* .. 8: tail coefficients t_0 .. t_5 */,
+             kTcHL = 9, kTcHFlags = 10 /* 1: opaque above the table, 2: non-finite columns */, kTcHNact = 11 };
+constexpr int kTcMaxOctaves = 64;
+
+struct TcArgs {
+  const double* hdr;         // [n_orb][kTcHdr]
+  const double* tab;         // [n_orb][lg][kTcD]
+  const int32_t* flags;      // [n_orb][n_pr] chord flags (0 active)
+  const double* ncol;        // [n_orb][n_pr] the effective absorber's columns
+  const double* fout;        // [n_pr]
+  double* R;                 // [n_orb][n_wav]
+  unsigned long long* evals; // [64] exp-evaluation counters (stats runs) or null
+  int32_t lg, n_pr;
+};
+
 struct AtomTable {
   bool live = false;     // slot in use (prom_table_free releases it for reuse)
   DevBuf x, y;
@@ -253,6 +272,10 @@ struct RunSlot {
                                             //     list [n_orb * 2 n_tiles], then big list [n_orb * 2 n_tiles] int4
   DevBuf hcnt;                              // ... their counts (int32 small, big; zeroed by k_columns8)
   DevBuf R;                                 // [n_orb][n_wav]
+  DevBuf tc_hdr;                            // transmission curves: [n_orb][kTcHdr] (k_tc_build)
+  DevBuf tc_tab;                            // ... [n_orb][tc_lg][kTcD] Chebyshev coefficients (k_tc_build)
+  DevBuf tc_part;                           // ... per (phase, chain, part) node sums and moments
+  DevBuf tc_cnt;                            // ... per (phase, chain) arrival counters (zero between runs)
   // second stream of the slot and its fork / join events (the Doppler sigma rows run beside the column
   // and ordering kernels); set per run by prom_transit_run, null: one stream
   hipStream_t aux = nullptr;
@@ -343,6 +366,12 @@ struct TransitDev {
   std::vector<double> seg_key_wav, seg_key_sh;
   std::vector<uint64_t> seg_key_gen;
   bool seg_key_valid = false;
+  // transmission-curve path (prom_tcurve.hip; PROM_TCURVE=0: off): set-time switch, the octave cap of the
+  // tables and the bound of Y (the effective absorber's sigma maximum) that sets each phase's table extent
+  bool tcurve = true;
+  int32_t tc_lg = 1;
+  int32_t tc_parts = 1;                     // chord parts per (phase, chain) of k_tc_build
+  double tc_ybound = 0.0;
   RunSlot slot[kMaxSlots];
   // PROM_GRAPH=1: a fast-path run is one hipGraph per slot, captured at the slot's first untimed run
   // and replayed (one host call instead of three launches; slower on ROCm 7.2, so off by default)
@@ -416,6 +445,10 @@ void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const d
 void launch_qbounds(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav, int32_t n_rows,
                     const SigSeg* seg, float4* tq, int32_t merge_sp, double nscale_m);
 // the fused tau kernels of the molecular and stellar-spectrum paths (prom_mol.hip, prom_rm.hip)
+// the transmission-curve path after the column kernel: k_tc_build, k_sigma_tc (prom_tcurve.hip);
+// the event pairs (may be null) ride on the two kernels' dispatch packets
+void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,
+                   hipEvent_t ev_sig1, hipEvent_t ev_tb0, hipEvent_t ev_tb1);
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);

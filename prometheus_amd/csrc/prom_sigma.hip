@@ -231,7 +231,9 @@ __global__ void __launch_bounds__(kBlock) PROM_SIG_ATTR k_sigma_rows(const SigTa
 //   sigma_s(t) = 10^(f_k + slope_k (t - x_k)) - offset = E_k e^a - offset,   a = L_k (t - x_k),
 // with E_k = 10^f_k and L_k = ln10 slope_k kept per node (AtomTable::rec, k_table_recs).  e^a is a degree-D
 // Taylor polynomial: the tables bound |a| on every interval by amax (AtomTable::amax) and prom_transit_set
-// takes the smallest even D with amax^(D+1)/(D+1)! <= 2^-53, so the truncation is below one rounding of e^a.
+// takes the smallest even D with e^amax amax^(D+1)/(D+1)! <= 2^-53, so the truncation is below one rounding of
+// e^a.
+// (The remainder relative to e^a carries e^|a| when a < 0: prom_transit_set's rule includes that factor.)
 // Against numpy's 10^v (v rounded once) sigma moves by ~|v| ln10 2^-53 (about 1e-14 relative); at an exact
 // node hit a = 0 and sigma is 10^f_k - offset as numpy's node rule gives it, and a flat interval at the
 // table floor (10^-50) gives exactly 0, so the exact path's zero pattern is kept.  No exp10, no division:
@@ -746,8 +748,17 @@ void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4&
   // fill the workgroup) and 4 for one (more workgroups in flight)
   const int R = kSigPolyRows > 0 ? kSigPolyRows : (nsig >= 2 ? 8 : 4);
   const int32_t n_rc = (n_rows + R - 1) / R;
-  // PROM_SIG_PARTS (profiling only: R is wrong without both): 1 = LDS workgroups, 2 = global-record ones
-  static const int32_t parts = std::getenv("PROM_SIG_PARTS") ? std::atoi(std::getenv("PROM_SIG_PARTS")) : 3;
+  // PROM_SIG_PARTS (profiling builds only, -DPROM_PROFILE_PARTS: R is wrong without both): 1 = LDS
+  // workgroups, 2 = global-record ones; the product library always runs both
+#ifdef PROM_PROFILE_PARTS
+  static const int32_t parts = [] {
+    const char* e = std::getenv("PROM_SIG_PARTS");
+    const int v = e ? std::atoi(e) : 3;
+    return (v >= 1 && v <= 3) ? v : 3;
+  }();
+#else
+  constexpr int32_t parts = 3;
+#endif
   // front: the oversize blocks' workgroups; then the XCD-aware grid over all blocks (none when every
   // block is oversize)
   // rows per front workgroup (measured, profiles/r03_sigma_rf_sweep.txt): R / 2 for several species (C3: 4

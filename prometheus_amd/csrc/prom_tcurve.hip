@@ -1,0 +1,609 @@
+// The transmission-curve path: the default for one effective absorber (merged species or one species).
+//
+// With one absorber every chord's optical depth is tau_c(o, w) = N_c Y(o, w): its column N_c times the
+// absorber's cross-section Y(o, w) = sum_s chi_s sigma_s(shift_o lambda_w) (gasProperties.py:941-954, the
+// reference's tau += N_s sigma_s).  The disk sum of sumOverChords (gasProperties.py:1241-1258) is then one
+// function of one variable per phase:
+//
+//   R(o, w) = T_o(Y(o, w)),   T_o(Y) = tfrac_o + sum_{active c} F_c exp(-N_c Y),   F_c = F_out,c / sum F_out,
+//
+// the phase's transmission curve.  Per run:
+//   k_columns8   columns and culling (prom_transit.hip);
+//   k_tc_build   per (phase, chain of 4 octaves of q = Y N_max, part of the chords): the phase's sums, tfrac,
+//                N_max, the tail polynomial's coefficients, and T_o at 16 Chebyshev nodes of log2 q per octave
+//                (exact sums over every active chord) turned into 16 Chebyshev coefficients;
+//   k_sigma_tc   per (phase, wavelength): Y from the Doppler-shifted table lookups, then T_o(Y) -> R.
+// T_o is evaluated three ways:
+//   q < 2^-7      every chord has tau = n_c q <= q (n_c = N_c / N_max <= 1): degree-5 Taylor polynomial of
+//                 exp(-tau) summed over the chords, t_e = (-1)^e sum_c F_c n_c^e / e!; truncation <= q^6/720
+//                 <= 3.2e-16 per unit weight (C3: 99 % of the points);
+//   octave j      q in [2^(j-7), 2^(j-6)): degree-15 Chebyshev series in v = log2(q) - (j - 7); the
+//                 interpolation error of g(s) = exp(-e^s) on one octave of s = ln q + ln n_c is below
+//                 2 max|g^(16)| (ln2/2)^16 / (2^15 16!) = 3e-17 per unit weight for any set of columns;
+//   above         q >= 40 N_max / N_min: every tau >= 40, T_o = tfrac within e^-40; otherwise (a table
+//                 truncated at the host's octave cap) the exact sum over the phase's chords.
+// So |R - R_exact| is a few 1e-16 plus the rounding of the sums, against the windowed path's 4e-14.  A phase
+// with a non-finite column takes the reference's chord order with ocml exp (the NaN pattern), as before.
+#include "prom_device.h"
+
+namespace prom {
+
+constexpr double kTcEps = 0x1p-7;        // tail threshold of q
+constexpr int kTcExpEps = -7;            // its binary exponent
+constexpr double kTcSat = 40.0;          // tau above which a chord is opaque (e^-40 = 4e-18)
+
+// q = Y N_max's binary exponent (q normal and >= 2^-7)
+__device__ __forceinline__ int32_t tc_exponent(double q) {
+  return (int32_t)((__builtin_bit_cast(unsigned long long, q) >> 52) & 0x7ff) - 1023;
+}
+
+// octaves [0, L) that cover q in [eps, qhi]: 0 when qhi < eps, INT32_MAX when not finite
+__device__ __forceinline__ int32_t tc_octaves(double qhi) {
+  if (!(qhi >= kTcEps)) return 0;
+  if (!(qhi <= 1.0e300)) return 0x7fffffff;
+  return tc_exponent(qhi) - kTcExpEps + 1;
+}
+
+// Reductions over the 64 lanes of a wavefront on DPP moves (quad permutes, half-row and row mirrors) and four
+// readlanes: no LDS round trips, a fixed combination order, a wave-uniform result.
+template <typename T, typename Op>
+__device__ __forceinline__ T tc_wred(T v, Op op) {
+  v = op(v, dpp_mov<0xB1>(v));    // quad_perm [1,0,3,2]
+  v = op(v, dpp_mov<0x4E>(v));    // quad_perm [2,3,0,1]
+  v = op(v, dpp_mov<0x141>(v));   // row_half_mirror
+  v = op(v, dpp_mov<0x140>(v));   // row_mirror: every lane of a row holds the row's fold
+  return op(op(lane_read(v, 0), lane_read(v, 16)), op(lane_read(v, 32), lane_read(v, 48)));
+}
+struct OpAddI { __device__ int32_t operator()(int32_t a, int32_t b) const { return a + b; } };
+
+// ---- per phase: sums, tail coefficients and the transmission-curve table, in one kernel ------------------
+// Grid (chain, part, phase).  Every workgroup first takes the phase's sums over all its chords (F_out sum,
+// transparent sum, N_max / N_min over the active finite columns, counts; one strided sweep, L2-resident
+// inputs) and the table extent L, identically.  Then part p of the chords [c_p, c_{p+1}) and chain ch of
+// octaves 4 ch .. 4 ch + 3: thread (k, g) = (t & 15, t >> 4) evaluates e = exp(-N q_k / N_max) at node k of
+// octave 4 ch for chords c_p + g, c_p + g + 16, ... and the next three octaves by squaring (q doubles from one
+// octave to the next: e^{-2x} = (e^{-x})^2; three squarings carry <= 2^3 (3u) + 7u = 31u = 3.4e-15 relative
+// error), so one table exp serves four octaves.  Chain 0 also sums the tail moments sum F n^e.  The parts'
+// node sums go to `part`; the last part to finish (atomic counter per (phase, chain), reset by it) adds them in
+// part order -- deterministic -- and writes the Chebyshev coefficients (and, chain 0, the header).
+constexpr int kTcB2 = 256;               // threads per workgroup
+constexpr int kTcChain = 4;              // octaves per table exp
+constexpr int kTcPartMax = 8;            // chord parts per (phase, chain)
+constexpr int kTcPartVals = kTcChain * kTcD + 8;   // doubles per part: node sums, then 6 moments
+
+__device__ __forceinline__ double exp256(double y, const double* __restrict__ tab) {
+  // 2^(y/256) for y = -x 256/ln2 (acc_exp256's arithmetic without the accumulation)
+  const double k = __builtin_rint(y);
+  const int ki = (int)k;
+  const double d = y - k;
+  double p = __builtin_fma(d, kE256C5, kE256C4);
+  p = __builtin_fma(d, p, kE256C3);
+  p = __builtin_fma(d, p, kE256C2);
+  p = __builtin_fma(d, p, kE256C1);
+  p = __builtin_fma(d, p, 1.0);
+  return __builtin_amdgcn_ldexp(tab[ki & 255], ki >> 8) * p;
+}
+
+__global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ flags, const double* __restrict__ fout,
+                                                   const double* __restrict__ ncol, int32_t n_pr, int32_t n_parts,
+                                                   double ybound, int32_t lg, double* __restrict__ hdr,
+                                                   double* __restrict__ tab, double* __restrict__ part,
+                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ counts,
+                                                   unsigned long long* __restrict__ evals) {
+  constexpr int NW = kTcB2 / 64;
+  const int32_t ch = blockIdx.x, pt = blockIdx.y, o = blockIdx.z;
+  const int32_t n_ch = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ double etab[256];
+  __shared__ double cm[kTcD * kTcD];
+  __shared__ double sd[4][NW];
+  __shared__ int32_t si[4][NW];
+  __shared__ double red[NW][kTcChain + 1][kTcD];
+  __shared__ double sf[kTcChain + 1][kTcD];
+  __shared__ int32_t s_last;
+  const int32_t* fl = flags + (int64_t)o * n_pr;
+  const double* nc = ncol + (int64_t)o * n_pr;
+  // the exp table and the Chebyshev matrix c_k = sum_j f_j cm[k][j] (one cosine per thread)
+  etab[tid] = kExp2TableDev[8 * tid];
+  {
+    const int k = tid >> 4, jj = tid & 15;
+    cm[tid] = cos(M_PI * (double)k * ((double)jj + 0.5) / (double)kTcD) * ((k == 0 ? 1.0 : 2.0) / (double)kTcD);
+  }
+  // 1. the phase's sums (every workgroup of the phase, the same order)
+  double fs = 0.0, ts = 0.0, nmax = 0.0, nmin = __builtin_inf();
+  int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0;
+  for (int32_t c = tid; c < n_pr; c += kTcB2) {
+    const int32_t f = fl[c];
+    const double fo = fout[c];
+    fs += fo;
+    if (f == 1) { ts += fo; ++ntr; }
+    else if (f == 2) ++nbl;
+    else if (f == 0) {
+      const double N = nc[c];
+      ++nact;
+      if (!__builtin_isfinite(N)) ++nnf;
+      else {
+        nmax = N > nmax ? N : nmax;
+        if (N > 0.0) nmin = N < nmin ? N : nmin;
+      }
+    }
+  }
+  fs = tc_wred<double>(fs, OpAdd());
+  ts = tc_wred<double>(ts, OpAdd());
+  nmax = tc_wred<double>(nmax, OpMax());
+  nmin = tc_wred<double>(nmin, OpMin());
+  nact = tc_wred<int32_t>(nact, OpAddI());
+  ntr = tc_wred<int32_t>(ntr, OpAddI());
+  nbl = tc_wred<int32_t>(nbl, OpAddI());
+  nnf = tc_wred<int32_t>(nnf, OpAddI());
+  if (lane == 0) {
+    sd[0][wid] = fs; sd[1][wid] = ts; sd[2][wid] = nmax; sd[3][wid] = nmin;
+    si[0][wid] = nact; si[1][wid] = ntr; si[2][wid] = nbl; si[3][wid] = nnf;
+  }
+  __syncthreads();
+  fs = sd[0][0]; ts = sd[1][0]; nmax = sd[2][0]; nmin = sd[3][0];
+  nact = si[0][0]; ntr = si[1][0]; nbl = si[2][0]; nnf = si[3][0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) {
+    fs += sd[0][w]; ts += sd[1][w];
+    nmax = sd[2][w] > nmax ? sd[2][w] : nmax;
+    nmin = sd[3][w] < nmin ? sd[3][w] : nmin;
+    nact += si[0][w]; ntr += si[1][w]; nbl += si[2][w]; nnf += si[3][w];
+  }
+  // table extent: octaves up to the host's bound of q = Y N_max, or up to q = 40 N_max / N_min (every chord
+  // opaque beyond it), whichever comes first; lg caps it
+  const bool fin = nnf == 0 && nmax > 0.0 && nact > 0;
+  int32_t L = 0, top_opaque = 0;
+  if (fin) {
+    const int32_t L1 = ybound > 0.0 ? tc_octaves(ybound * nmax * (1.0 + 0x1p-40)) : 0x7fffffff;
+    const int32_t L2 = tc_octaves(kTcSat * (nmax / nmin));
+    if (L2 <= L1 && L2 <= lg) {
+      L = L2;
+      top_opaque = 1;
+    } else {
+      L = L1 < lg ? L1 : lg;
+    }
+  }
+  const int32_t j0 = ch * kTcChain;
+  if (ch > 0 && j0 >= L) return;   // (chain 0 always runs: the moments and the header)
+  // 2. this part's chords at this chain's nodes (and, chain 0, the moments)
+  const int k = tid & 15, g = tid >> 4;
+  const int32_t c_lo = (int32_t)((int64_t)n_pr * pt / n_parts), c_hi = (int32_t)((int64_t)n_pr * (pt + 1) / n_parts);
+  double acc[kTcChain] = {0.0, 0.0, 0.0, 0.0};
+  double mom = 0.0;
+  const bool do_tab = fin && j0 < L;
+  const double inv_fs = 1.0 / fs;
+  const double inv_nmax = fin ? 1.0 / nmax : 0.0;
+  // node k of octave j0: q_k = 2^(j0 - 7 + v_k), v_k = (u_k + 1) / 2, u_k = cos(pi (k + 1/2) / 16);
+  // y = N q_k / N_max (-256 / ln2)
+  const double uk = cos(M_PI * ((double)k + 0.5) / (double)kTcD);
+  const double sk = ldexp(exp2(0.5 * (uk + 1.0)), j0 + kTcExpEps) * inv_nmax * kM256Ln2;
+  __syncthreads();   // etab, cm
+  if (fin) {
+    for (int32_t c = c_lo + g; c < c_hi; c += kTcB2 / 16) {
+      if (fl[c] != 0) continue;
+      const double F = fout[c] * inv_fs, N = nc[c];
+      if (do_tab) {
+        double e = exp256(N * sk, etab);
+        acc[0] = __builtin_fma(F, e, acc[0]);
+#pragma unroll
+        for (int m = 1; m < kTcChain; ++m) {
+          e = e * e;
+          acc[m] = __builtin_fma(F, e, acc[m]);
+        }
+      }
+      if (ch == 0 && k < 6) {
+        const double n = N * inv_nmax;
+        double pw = F;
+        for (int e2 = 0; e2 < k; ++e2) pw *= n;
+        mom += pw;
+      }
+    }
+  }
+  // fold the 16 groups: across the 4 rows of a wave (butterfly: every row the same sum), then the waves in LDS
+#pragma unroll
+  for (int m = 0; m < kTcChain; ++m) {
+    acc[m] += __shfl_xor(acc[m], 16, 64);
+    acc[m] += __shfl_xor(acc[m], 32, 64);
+  }
+  mom += __shfl_xor(mom, 16, 64);
+  mom += __shfl_xor(mom, 32, 64);
+  if (lane < 16) {
+#pragma unroll
+    for (int m = 0; m < kTcChain; ++m) red[wid][m][lane] = acc[m];
+    red[wid][kTcChain][lane] = mom;
+  }
+  __syncthreads();
+  const int32_t item = o * n_ch + ch;
+  double* pp = part + (int64_t)item * kTcPartMax * kTcPartVals;
+  // hand-off to the last part of this (phase, chain) (MI355X_MICROARCH.md, inter-workgroup visibility, first
+  // row of the sc1 table): write-through (sc1) stores, every storing wave's vmcnt(0), a barrier, one agent-scope
+  // atomic add per workgroup; the workgroup whose add comes last reads with sc1 loads after a barrier
+  if (tid < (kTcChain + 1) * kTcD) {
+    const int m = tid >> 4, kk = tid & 15;
+    double v = red[0][m][kk];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += red[w][m][kk];
+    __hip_atomic_store(&pp[pt * kTcPartVals + tid], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int32_t prev = __hip_atomic_fetch_add(&cnt[item], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == n_parts - 1 ? 1 : 0;
+    // ready for the next run of this slot (a later launch: the kernel boundary orders it)
+    if (s_last) __hip_atomic_store(&cnt[item], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (tid < (kTcChain + 1) * kTcD) {
+    double v = 0.0;
+    for (int q = 0; q < n_parts; ++q)
+      v += __hip_atomic_load(&pp[q * kTcPartVals + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sf[tid >> 4][tid & 15] = v;
+  }
+  __syncthreads();
+  if (tid < kTcChain * kTcD) {
+    const int m = tid >> 4, kk = tid & 15;
+    if (do_tab && j0 + m < L) {
+      double c = 0.0;
+#pragma unroll
+      for (int jj = 0; jj < kTcD; ++jj) c = __builtin_fma(sf[m][jj], cm[kk * kTcD + jj], c);
+      tab[((int64_t)o * lg + j0 + m) * kTcD + kk] = c;
+    }
+  }
+  if (ch == 0 && tid == 0) {
+    // t_e = (-1)^e m_e / e!
+    double t[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) t[e] = fin ? sf[kTcChain][e] : 0.0;
+    t[1] = -t[1];
+    t[2] = t[2] / 2.0;
+    t[3] = -t[3] / 6.0;
+    t[4] = t[4] / 24.0;
+    t[5] = -t[5] / 120.0;
+    double* h = hdr + (int64_t)o * kTcHdr;
+    h[kTcHNmax] = nmax;
+    h[kTcHTfrac] = ts / fs;
+    h[kTcHFsum] = fs;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) h[kTcHT0 + e] = t[e];
+    h[kTcHL] = (double)L;
+    h[kTcHFlags] = (double)(top_opaque | (nnf ? 2 : 0));
+    h[kTcHNact] = (double)nact;
+    if (counts) {
+      int32_t* cn = counts + o * kCnt;
+      cn[0] = nact; cn[1] = ntr; cn[2] = nbl; cn[3] = nnf;
+      cn[4] = nact; cn[5] = 0; cn[6] = 0; cn[7] = L;
+    }
+  }
+  if (evals && tid == 0 && do_tab)
+    atomicAdd(&evals[item & 63], (unsigned long long)nact * kTcD * (L - j0 < kTcChain ? L - j0 : kTcChain));
+}
+
+// T_o(Y) for a phase whose columns are finite (header h, its table rows tabo)
+__device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h, const double* __restrict__ tabo,
+                                          const int32_t* __restrict__ fl, const double* __restrict__ nc,
+                                          const double* __restrict__ fout, int32_t n_pr, unsigned long long* evals) {
+  const double q = Y * h[kTcHNmax];
+  const double tf = h[kTcHTfrac];
+  if (q < kTcEps) {
+    double p = h[kTcHT0 + 5];
+#pragma unroll
+    for (int e = 4; e >= 0; --e) p = __builtin_fma(p, q, h[kTcHT0 + e]);
+    return tf + p;
+  }
+  const int32_t nact = (int32_t)h[kTcHNact];
+  if (!(q == q)) return nact > 0 ? q : tf;   // NaN cross-section: NaN wherever a chord absorbs
+  const int32_t L = (int32_t)h[kTcHL];
+  const int32_t j = q <= 1.0e300 ? tc_exponent(q) - kTcExpEps : 0x7fffffff;
+  if (j < L) {
+    // v = log2 of q's mantissa, in [0, 1); Clenshaw in u = 2 v - 1
+    const double m = __builtin_bit_cast(double, (__builtin_bit_cast(unsigned long long, q) & 0x000fffffffffffffull) |
+                                                    0x3ff0000000000000ull);
+    const double u = __builtin_fma(2.0, log2(m), -1.0);
+    const double* c = tabo + (int64_t)j * kTcD;
+    double b1 = 0.0, b2 = 0.0;
+#pragma unroll
+    for (int k = kTcD - 1; k >= 1; --k) {
+      const double b0 = __builtin_fma(2.0 * u, b1, c[k] - b2);
+      b2 = b1;
+      b1 = b0;
+    }
+    return tf + (__builtin_fma(u, b1, c[0] - b2));
+  }
+  if ((int32_t)h[kTcHFlags] & 1) return tf;   // every chord opaque (tau >= 40)
+  // beyond a truncated table: the exact sum over the phase's active chords, in chord order
+  const double inv_fs = 1.0 / h[kTcHFsum];
+  double a = 0.0;
+  for (int32_t c = 0; c < n_pr; ++c)
+    if (fl[c] == 0) a += (fout[c] * inv_fs) * exp(-(nc[c] * Y));
+  if (evals) atomicAdd(&evals[threadIdx.x & 63], (unsigned long long)nact);
+  return tf + a;
+}
+
+// ---- sigma lookups + transmission curves -> R --------------------------------------------------------------
+// The lookups are k_sigma_poly's (prom_sigma.hip): one workgroup per (256-wavelength block, R rows), per species
+// the block's table slice staged in LDS ({x_k, x_{k+1}}, {10^y_k, ln10 slope_k}), one record per lookup when the
+// slice's linear guess is numpy's bracket (kind & 4), the degree-D Taylor e^a; oversize blocks first, reading
+// 32-byte records from the global table.  NT = R target rows with orbital Doppler shift, NT = 1 without (UNI:
+// the R phases of the workgroup share one Y per wavelength).  Then each (phase, wavelength): R = T_o(Y).
+template <int NSIG, int D, bool MG, int R, bool UNI>
+__global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
+                                                     int64_t n_wav, int32_t n_rows, const SigSeg* __restrict__ seg,
+                                                     const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
+                                                     int32_t n_rc, int32_t rf, const TcArgs ta) {
+  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per workgroup");
+  constexpr int NT = UNI ? 1 : R;
+  __shared__ double2 slds[2 * kSigSeg];
+  double2* sxr = slds;
+  double2* sel = slds + kSigSeg;
+  const int tid = threadIdx.x;
+  const int32_t RF = rf;
+  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * ((n_rows + RF - 1) / RF);
+  int64_t bid = blockIdx.x, wb;
+  int32_t r0, rcap = R;
+  bool lds_ok = true;
+  if (bid < n_front) {
+    const int64_t i = bid % n_fb8;
+    if (i >= n_fb) return;
+    wb = fb[i];
+    r0 = (int32_t)(bid / n_fb8) * RF;
+    rcap = RF;
+    lds_ok = false;
+  } else {
+    bid -= n_front;
+    const int64_t grp = bid / (8 * n_rc), rem = bid % (8 * n_rc);
+    wb = grp * 8 + rem % 8;
+    r0 = (int32_t)(rem / 8) * R;
+    if (wb >= n_blk) return;
+#pragma unroll
+    for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
+    if (!lds_ok) return;   // (a front workgroup's)
+  }
+  const int32_t rlim = r0 + rcap < n_rows ? r0 + rcap : n_rows;
+  rcap = rlim - r0;
+#ifdef PROM_TRACE
+  const unsigned long long tr_t0 = wall_clock64();
+#endif
+  const int64_t w = wb * kBlock + tid;
+  const bool live = w < n_wav;
+  const double lam = wav[live ? w : n_wav - 1];
+  double acc[NT];
+#pragma unroll
+  for (int r = 0; r < NT; ++r) acc[r] = 0.0;
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) {
+    const SigTabDev& tb = tabv.t[s];
+    const SigSeg sg = seg[wb * NSIG + s];
+    if constexpr (D == 0) {
+      // tables too coarse for a degree-14 e^a polynomial: numpy.interp + exp10 per target (sigma_seg: the
+      // block's verified guess into the global x / f arrays), bit for bit the per-target lookups
+#pragma unroll
+      for (int r = 0; r < NT; ++r) {
+        const double t = tb.shift[r0 + r < n_rows ? r0 + r : n_rows - 1] * lam;
+        const double v = sigma_seg(t, tb, sg);
+        if constexpr (MG) acc[r] += tb.chi * v;
+        else acc[r] = v;
+      }
+      continue;
+    }
+    if (lds_ok) {
+      if (s > 0) __syncthreads();   // the previous species' slice is no longer read
+      for (int32_t i = tid; i < sg.m; i += kBlock) {
+        const double4 q = tb.rec[sg.lo + i];
+        sxr[i] = make_double2(q.x, q.w);
+        sel[i] = make_double2(q.y, q.z);
+      }
+      __syncthreads();
+    }
+    const bool exact = (sg.kind & 4) != 0;
+    const double off = tb.offset, chi = tb.chi;
+    auto emit = [&](int r, double v) {
+      if constexpr (MG) acc[r] += chi * v;
+      else acc[r] = v;
+    };
+    double tt[NT];
+#pragma unroll
+    for (int r = 0; r < NT; ++r) tt[r] = tb.shift[r0 + r < n_rows ? r0 + r : n_rows - 1] * lam;
+    const int32_t ncap = UNI ? 1 : rcap;
+    if (!lds_ok) {
+      if ((sg.kind & 3) > 0) {
+        constexpr int G = NT < 4 ? NT : 4;
+        const double4* __restrict__ rr = tb.rec + sg.lo;
+#pragma unroll
+        for (int r0g = 0; r0g < NT; r0g += G) {
+          if (r0g >= ncap) break;
+          double4 q[G];
+#pragma unroll
+          for (int jj = 0; jj < G; ++jj) q[jj] = rr[seg_guess(tt[r0g + jj], sg.xs, sg.inv, sg.m)];
+          if (!exact) {
+#pragma unroll
+            for (int jj = 0; jj < G; ++jj) {
+              const double t = tt[r0g + jj];
+              const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+              const int32_t k = t < q[jj].x ? g - 1 : (t >= q[jj].w ? g + 1 : g);
+              if (k != g) q[jj] = rr[k];
+            }
+          }
+#pragma unroll
+          for (int jj = 0; jj < G; ++jj)
+            emit(r0g + jj, __builtin_fma(q[jj].y, exp_taylor<D>(q[jj].z * (tt[r0g + jj] - q[jj].x), pc), -off));
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < NT; ++r)
+          if (r < ncap) emit(r, sigma_poly_of(tt[r], tb, pc, D));
+      }
+    } else {
+      auto lds_rows = [&](auto guard) {
+        constexpr bool GD = decltype(guard)::value;
+        double xk[NT];
+        double2 el[NT];
+#pragma unroll
+        for (int r = 0; r < NT; ++r) {
+          if (GD && r >= ncap) break;
+          const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
+          if (exact) {
+            xk[r] = sxr[g].x;
+            el[r] = sel[g];
+          } else {
+            const double2 xx = sxr[g];
+            const int32_t k = tt[r] < xx.x ? g - 1 : (tt[r] >= xx.y ? g + 1 : g);
+            xk[r] = sxr[k].x;
+            el[r] = sel[k];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < NT; ++r) {
+          if (GD && r >= ncap) break;
+          emit(r, __builtin_fma(el[r].x, exp_taylor<D>(el[r].y * (tt[r] - xk[r]), pc), -off));
+        }
+      };
+      if (ncap >= NT) lds_rows(std::false_type{});
+      else lds_rows(std::true_type{});
+    }
+  }
+  // R = T_o(Y) per (phase, wavelength)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (r >= rcap) break;
+    const int32_t o = r0 + r;
+    const double Y = acc[UNI ? 0 : r];
+    const double* h = ta.hdr + (int64_t)o * kTcHdr;
+    double v;
+    if (!((int32_t)h[kTcHFlags] & 2)) {
+      v = tc_eval(Y, h, ta.tab + (int64_t)o * ta.lg * kTcD, ta.flags + (int64_t)o * ta.n_pr,
+                  ta.ncol + (int64_t)o * ta.n_pr, ta.fout, ta.n_pr, ta.evals);
+    } else {
+      // non-finite column densities: the reference's chord order with ocml exp.  Merged species: the
+      // reference's sum_s (N chi_s) sigma_s is NaN for an infinite N wherever some chi_s sigma_s is not > 0
+      bool zr = false;
+      if constexpr (MG) {
+#pragma unroll
+        for (int s = 0; s < NSIG; ++s) {
+          const SigTabDev& tb = tabv.t[s];
+          const double sv = D == 0 ? sigma_seg(tb.shift[o] * lam, tb, seg[wb * NSIG + s])
+                                   : sigma_seg_poly(tb.shift[o] * lam, tb, seg[wb * NSIG + s], pc, D);
+          zr = zr || !(tb.chi * sv > 0.0);
+        }
+      }
+      const int32_t* fl = ta.flags + (int64_t)o * ta.n_pr;
+      const double* nc = ta.ncol + (int64_t)o * ta.n_pr;
+      double a = 0.0;
+      for (int32_t c = 0; c < ta.n_pr; ++c) {
+        if (fl[c] != 0) continue;
+        const double N = nc[c];
+        double tau = N * Y;
+        if (zr && !__builtin_isfinite(N)) tau = __builtin_nan("");
+        a = a + ta.fout[c] * exp(-tau);
+      }
+      const double fs = h[kTcHFsum];
+      v = (a + h[kTcHTfrac] * fs) / fs;
+    }
+    if (live) ta.R[(int64_t)o * n_wav + w] = v;
+  }
+#ifdef PROM_TRACE
+  // per workgroup (tools/trace_sigma.py): start, end (wall clock, 10 ns), block | lds << 32 | front << 33,
+  // first row | species kinds << 32 | largest slice << 44
+  if (threadIdx.x == 0 && blockIdx.x < (1u << 18)) {
+    unsigned long long* tp = g_trace + 4ull * blockIdx.x;
+    tp[0] = tr_t0;
+    tp[1] = wall_clock64();
+    tp[2] = (unsigned long long)wb | ((unsigned long long)lds_ok << 32) | ((unsigned long long)(blockIdx.x < n_front) << 33);
+    unsigned long long kinds = 0;
+    int32_t mmax = 0;
+    for (int s = 0; s < NSIG; ++s) {
+      kinds |= (unsigned long long)(seg[wb * NSIG + s].kind & 7) << (3 * s);
+      mmax = seg[wb * NSIG + s].m > mmax ? seg[wb * NSIG + s].m : mmax;
+    }
+    tp[3] = (unsigned long long)(uint32_t)r0 | (kinds << 32) | ((unsigned long long)(mmax > 65535 ? 65535 : mmax) << 44);
+  }
+#endif
+}
+
+#ifdef PROM_TRACE
+extern "C" int32_t prom_tc_trace_read(unsigned long long* out, int32_t n, int32_t clear) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+  if (clear) {
+    static unsigned long long zeros[1 << 20];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace), zeros, sizeof(zeros)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
+void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,
+                   hipEvent_t ev_sig1, hipEvent_t ev_tb0, hipEvent_t ev_tb1) {
+  const int32_t lg = tr.tc_lg;
+  unsigned long long* evals = tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr;
+  const int32_t n_ch = (lg + kTcChain - 1) / kTcChain;
+  const int32_t n_parts = tr.tc_parts;
+  hipExtLaunchKernelGGL(k_tc_build, dim3((unsigned)n_ch, (unsigned)n_parts, (unsigned)tr.n_orb), dim3(kTcB2), 0, s,
+                        ev_tb0, ev_tb1, 0, rs.flags.as<int32_t>(), tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr,
+                        n_parts, tr.tc_ybound, lg, rs.tc_hdr.as<double>(), rs.tc_tab.as<double>(), rs.tc_part.as<double>(),
+                        rs.tc_cnt.as<int32_t>(), rs.counts.as<int32_t>(), evals);
+  PROM_HIP(hipGetLastError());
+  TcArgs ta{};
+  ta.hdr = rs.tc_hdr.as<double>();
+  ta.tab = rs.tc_tab.as<double>();
+  ta.flags = rs.flags.as<int32_t>();
+  ta.ncol = rs.ncol.as<double>();
+  ta.fout = tr.cfout.as<double>();
+  ta.R = rs.R.as<double>();
+  ta.evals = evals;
+  ta.lg = lg;
+  ta.n_pr = tr.n_pr;
+  const bool uni = tr.uniform_shift;
+  const int32_t n_rows = tr.n_orb;
+  const int64_t n_wav = tr.n_wav;
+  const int32_t n_blk = (int32_t)grid_for(n_wav);
+  // rows per workgroup: 8 for several species or one shared target row (their lookups fill the workgroup),
+  // 4 for one species with orbital Doppler shift (more workgroups in flight), never more than the problem's
+  // (instantiated: 8 rows with one shared target; 1, 4 or 8 with orbital Doppler shift -- the guarded copy
+  // of the lookups covers workgroups with fewer rows)
+  const int deg = tr.sig_deg;
+  const int Rmax = (nsig >= 2 || uni) ? 8 : 4;
+  const int R = (uni || deg == 0) ? 8 : (n_rows == 1 ? 1 : Rmax);
+  const int32_t n_rc = (n_rows + R - 1) / R;
+  // front workgroups (oversize blocks): R / 2 rows for several species, or for one species with fewer than
+  // 16384 (block, row) pairs of them (profiles/r03_sigma_rf_sweep.txt); one shared target: all R
+  int RF = R;
+  if (!uni && R >= 2 && (nsig >= 2 || (int64_t)tr.n_sig_fb * n_rows < 16384)) RF = R / 2;
+  const int32_t n_fb = tr.n_sig_fb;
+  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
+  const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
+  const PolyCoef& pc = poly_coef();
+  const SigTabs4& tabv = tr.sigtab_v;
+  const double* wav = tr.wav.as<double>();
+  const SigSeg* seg = tr.sig_seg.as<SigSeg>();
+  const int32_t* fb = tr.sig_fb.as<int32_t>();
+  PROM_REQUIRE(msp || nsig == 1, "transmission curves: one effective absorber only");
+#define PROM_TCK(NS, DG, MGV, RV, UV)                                                                         \
+  hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV>), dim3(nb), dim3(kBlock), 0, s, ev_sig0, ev_sig1, 0, tabv, \
+                        pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, RF, ta)
+#define PROM_TCR(NS, DG, MGV)                          \
+  do {                                                 \
+    if (uni) PROM_TCK(NS, DG, MGV, 8, true);           \
+    else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false);  \
+    else if (R <= 4) PROM_TCK(NS, DG, MGV, 4, false);  \
+    else PROM_TCK(NS, DG, MGV, 8, false);              \
+  } while (0)
+  // degree 8 covers every table with amax <= 0.07 (the high-resolution configs); 14 the rest (coarse tables)
+#define PROM_TCD(NS, MGV)                                                          \
+  if (deg == 0) { if (uni) PROM_TCK(NS, 0, MGV, 8, true); else PROM_TCK(NS, 0, MGV, 8, false); } \
+  else if (deg <= 8) PROM_TCR(NS, 8, MGV);                                       \
+  else PROM_TCR(NS, 14, MGV);
+  switch (nsig) {
+    case 1: PROM_TCD(1, false) break;
+    case 2: PROM_TCD(2, true) break;
+    case 3: PROM_TCD(3, true) break;
+    default: PROM_TCD(4, true) break;
+  }
+#undef PROM_TCD
+#undef PROM_TCR
+#undef PROM_TCK
+  PROM_HIP(hipGetLastError());
+}
+
+}  // namespace prom

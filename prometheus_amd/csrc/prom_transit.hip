@@ -2234,6 +2234,40 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // 1. densities -> column densities -> blocking/transparency flags
   const int64_t nc = (int64_t)tr.n_orb * tr.n_pr;
   bool sig_after_order = false;   // Doppler sigma rows still to queue, after k_order (rs.sig_late)
+#define PROM_COLS(SV, NSV)                                                                               \
+  hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
+                     dim3(col_blocks),                                                                    \
+                     dim3(kBlock), 0, s, kp_start(tr, PROM_K_COLUMNS, ev0), kp_stop(tr, PROM_K_COLUMNS, nullptr), 0, \
+                     cargs, n_terms,                                                                      \
+                     tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
+                     tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
+                     tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
+                     tr.moon_R.as<double>(), smax, tr.cull_tau, rs.ncol.as<double>(),                       \
+                     rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>(), \
+                     pre_sigma ? rs.tq.as<float4>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale,    \
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, rs.zfl.as<uint8_t>(), sig_rows)
+#define PROM_COLS_L(NSV)                       \
+  if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
+  else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
+  else if (tr.n_x <= 32) PROM_COLS(4, NSV);    \
+  else PROM_COLS(8, NSV);
+  // transmission-curve path (prom_tcurve.hip, the default for one effective absorber): k_columns8, then
+  // k_tc_build -> k_sigma_tc; no ordering, windows or heavy entries
+  const bool tcp = tr.tcurve && cols8 && wpath && tr.window && !tr.star && na == 1 && tr.sig_seg_ok;
+  if (tcp) {
+    const unsigned col_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
+    PROM_COLS_L(0)
+    PROM_HIP(hipGetLastError());
+    // stats runs: {columns start, tables done, sigma start, sigma done}; timed runs: the sigma kernel's
+    // interval opens at the table kernel's completion
+    hipEvent_t e_tb1 = ev ? (stage_events ? ev1 : ev[2]) : nullptr;
+    hipEvent_t e_sg0 = (ev && stage_events) ? ev[2] : nullptr;
+    hipEvent_t e_sg1 = ev ? ev[3] : nullptr;
+    launch_tcurve(s, tr, rs, nsig, msp, kp_start(tr, PROM_K_SIGMA, e_sg0), kp_stop(tr, PROM_K_SIGMA, e_sg1),
+                  kp_start(tr, PROM_K_ORDER, nullptr), kp_stop(tr, PROM_K_ORDER, e_tb1));
+    *variant = 80 + na;
+    return;
+  }
   if (cols8) {
     // with resampling: chord workgroups padded to a multiple of 8, sigma workgroups rounded up to one
     const unsigned chord_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
@@ -2256,7 +2290,12 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
     }
     auto sigma_rows = [&]() {
+#ifdef PROM_PROFILE_PARTS
+      // (profiling builds: PROM_FUSED_ROWS=1 also stores the sigma rows of the fused path)
       static const bool dbg_rows = std::getenv("PROM_FUSED_ROWS") && std::atoi(std::getenv("PROM_FUSED_ROWS"));
+#else
+      constexpr bool dbg_rows = false;
+#endif
       launch_rows(sig_fork ? rs.aux : s, tr, rs, nsig, sig_rows, msp, sig_fork ? nullptr : ev0, !fused || dbg_rows);
       if (sig_fork) PROM_HIP(hipEventRecord(rs.ev_join, rs.aux));
       else ev0 = nullptr;
@@ -2267,30 +2306,11 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     } else if (rows_seg && sig_first && !sig_after_order) {
       sigma_rows();
     }
-#define PROM_COLS(SV, NSV)                                                                               \
-  hipExtLaunchKernelGGL((k_columns8<SV, NSV>),                                                           \
-                     dim3(col_blocks),                                                                    \
-                     dim3(kBlock), 0, s, kp_start(tr, PROM_K_COLUMNS, ev0), kp_stop(tr, PROM_K_COLUMNS, nullptr), 0, \
-                     cargs, n_terms,                                                                      \
-                     tr.x.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x, tr.cy.as<double>(),        \
-                     tr.cz.as<double>(), tr.body_x.as<double>(), tr.body_y.as<double>(),                   \
-                     tr.planet_y.as<double>(), tr.planet_R, tr.n_moons, tr.moon_y.as<double>(),            \
-                     tr.moon_R.as<double>(), smax, tr.cull_tau, rs.ncol.as<double>(),                       \
-                     rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>(), \
-                     pre_sigma ? rs.tq.as<float4>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale,    \
-                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, rs.zfl.as<uint8_t>(), sig_rows)
-#define PROM_COLS_L(NSV)                       \
-  if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
-  else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
-  else if (tr.n_x <= 32) PROM_COLS(4, NSV);    \
-  else PROM_COLS(8, NSV);
     if (!pre_sigma || rows_seg) { PROM_COLS_L(0) }
     else if (nsig == 1) { PROM_COLS_L(1) }
     else if (nsig == 2) { PROM_COLS_L(2) }
     else if (nsig == 3) { PROM_COLS_L(3) }
     else { PROM_COLS_L(4) }
-#undef PROM_COLS_L
-#undef PROM_COLS
     PROM_HIP(hipGetLastError());
     if (rows_seg && (!fused || fused_poly) && !sig_first) sigma_rows();
     ev0 = nullptr;
@@ -2325,6 +2345,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     PROM_HIP(hipGetLastError());
     kp_rec(tr, PROM_K_COLUMNS, true, s);
   }
+#undef PROM_COLS_L
+#undef PROM_COLS
   if (tr.star) {
     // 2'. stellar spectrum: one exact chord-order kernel over the flags / columns
     if (ev1) PROM_HIP(hipEventRecord(ev1, s));

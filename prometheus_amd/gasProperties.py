@@ -588,20 +588,40 @@ def _star_lookup_table(fn) -> "LookupTable":
         return fn
     if _STAR_TABLES is None:
         _STAR_TABLES = weakref.WeakKeyDictionary()
+    x = np.ascontiguousarray(np.asarray(fn.x, dtype=np.float64))
+    y = np.ascontiguousarray(np.asarray(fn.y, dtype=np.float64))
+    # the cached device copy stays valid only while the spectrum's content is unchanged (arrays replaced or
+    # modified in place): a content fingerprint of both arrays is part of the key
+    fp = _content_fingerprint(x, y)
     try:
-        tab = _STAR_TABLES.get(fn)
+        hit = _STAR_TABLES.get(fn)
     except TypeError:   # not weak-referenceable: no cache
-        tab = None
-    if tab is None:
-        x = np.ascontiguousarray(np.asarray(fn.x, dtype=np.float64))
-        if np.any(x[1:] < x[:-1]):
-            raise ValueError("Fstar_function.x must be ascending (np.interp, gasProperties.py:1214)")
-        tab = LookupTable(x, np.ascontiguousarray(np.asarray(fn.y, dtype=np.float64)), 0.0)
-        try:
-            _STAR_TABLES[fn] = tab
-        except TypeError:
-            pass
+        hit = None
+    if hit is not None and hit[1] == fp:
+        return hit[0]
+    if np.any(x[1:] < x[:-1]):
+        raise ValueError("Fstar_function.x must be ascending (np.interp, gasProperties.py:1214)")
+    tab = LookupTable(x, y, 0.0)
+    try:
+        _STAR_TABLES[fn] = (tab, fp)
+    except TypeError:
+        pass
     return tab
+
+
+def _content_fingerprint(*arrays) -> tuple:
+    """(shape, 64-bit content hash) per array: xxhash when importable, else zlib's crc32."""
+    try:
+        import xxhash
+
+        def h(b):
+            return xxhash.xxh3_64_intdigest(b)
+    except ImportError:   # pragma: no cover
+        import zlib
+
+        def h(b):
+            return zlib.crc32(b)
+    return tuple((a.shape, h(memoryview(a).cast("B"))) for a in arrays)
 
 
 class Transit:

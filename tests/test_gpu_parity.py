@@ -143,6 +143,7 @@ def test_chord_merging(dev, name, monkeypatch):
     """Merging chords with equal (2^-40) column densities moves R by <= 2^-40/e.  Checked with
     every active chord sorted (PROM_NO_TAIL_SPLIT): always-tail chords are otherwise left unsorted behind
     the others, where equal neighbours are not adjacent (test_tail_split)."""
+    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
     from prometheus_amd import _native
     monkeypatch.setenv("PROM_NO_TAIL_SPLIT", "1")
     d = load("transit_" + name)
@@ -165,6 +166,7 @@ def test_tail_split(dev, name, monkeypatch):
     """k_order leaves chords with b Q_bound < the tail epsilon unsorted behind the sorted ones (their
     envelope is the threshold itself): R moves by no more than the windowed bound, and stays within the
     north-star tolerance of the reference."""
+    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
     d = load("transit_" + name)
     cfg = json.loads(str(d["config"]))
     R_s = _product_transit(cfg).sumOverChords(devices=[0])
@@ -204,9 +206,10 @@ def test_transit_c2_full_grid_sampled(dev):
 
 
 @pytest.mark.parametrize("name", ["C1", "C2r", "C3r", "C4r", "exomoon"])
-def test_windowed_integration(dev, name):
+def test_windowed_integration(dev, name, monkeypatch):
     """Windowed integration (saturated-head skip + cubic tail moments) against full
     evaluation of every record: |dR| <= 2^-40/24 + e^-40 (+ rounding), and fewer exp evaluations."""
+    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
     from prometheus_amd import _native
     d = load("transit_" + name)
     tr = _product_transit(json.loads(str(d["config"])))
@@ -336,6 +339,7 @@ def test_planned_tau_within_window_bound(dev, name, monkeypatch):
     against k_tau_w (PROM_TAU_PLAN=0: one window per 128-wavelength tile, records summed in order).  Light
     tiles are bitwise equal (most points); heavy halves differ by at most the two windows' truncation bounds
     plus the chunked summation's rounding, and never evaluate more exponentials."""
+    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
     from prometheus_amd import configs
     if name in ("C2", "C3"):
         cfg = configs.get(name)
@@ -368,6 +372,7 @@ def test_fused_sigma(dev, name, monkeypatch):
     ranges and the tau kernel's lookup is k_sigma_poly's arithmetic on the same record, so R is bitwise the
     row path's.  exp10 rows (PROM_SIG_POLY=0): node-range Q bounds (k_qbounds), both within the windowed
     integration's bound of the full evaluation, so within 1e-13 of each other.  And the reference's R."""
+    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
     from prometheus_amd import configs
     cfg = configs.get(name) if name == "C3" else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
@@ -404,6 +409,7 @@ def test_sigma_tau_bitwise(dev, name, merge, monkeypatch):
     the row path (PROM_SIG_TAU=0: Y rows, k_windows, k_tau_p's static units).  Same windows, records, order
     and arithmetic: R is bitwise equal and the exponentials counted are the same.  Several unmerged species
     (merge 0) and the exp10 rows keep the row path."""
+    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
     from prometheus_amd import configs
     cfg = configs.get(name) if name in ("C3", "C4", "C4x10") else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
@@ -433,7 +439,8 @@ def test_sigma_tau_bitwise(dev, name, merge, monkeypatch):
 def test_species_merge(dev, name, monkeypatch):
     """Constituents of one density scenario collapse into one effective absorber (tau = N Y with
     Y = sum_s chi_s sigma_s): R agrees with the per-species integration to rounding (1e-13 relative)
-    and with the reference to R_TOL; the merged run has one effective species (variant 31)."""
+    and with the reference to R_TOL; the merged run has one effective species: the transmission-curve path
+    (variant 81) by default, the windowed path's variant 31 with PROM_TCURVE=0."""
     from prometheus_amd import configs
     cfg = configs.get("C2") if name == "C2" else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
@@ -445,13 +452,18 @@ def test_species_merge(dev, name, monkeypatch):
     st_s = tr.last_stats[-1]
     print(name, "variants", st_m["tau_kernel_variant"], st_s["tau_kernel_variant"],
           "exp evals %d -> %d" % (st_s["exp_evals"], st_m["exp_evals"]), "max rel diff %.3e" % rel(R_m, R_s))
-    assert st_m["tau_kernel_variant"] == 31 and st_s["tau_kernel_variant"] == 32
+    assert st_m["tau_kernel_variant"] == 81 and st_s["tau_kernel_variant"] == 32
     assert rel(R_m, R_s) < 1e-13
     if name != "C2":
         assert rel(R_m, load("transit_" + name)["R"]) < R_TOL
+    monkeypatch.setenv("PROM_SPECIES_MERGE", "1")
+    monkeypatch.setenv("PROM_TCURVE", "0")
+    R_w = tr.sumOverChords(devices=[0])
+    assert tr.last_stats[-1]["tau_kernel_variant"] == 31
+    assert rel(R_w, R_s) < 1e-13
 
 
-@pytest.mark.parametrize("plan", ["1", "0", "doppler", "doppler_rows"])
+@pytest.mark.parametrize("plan", ["1", "0", "doppler", "doppler_rows", "tcurve", "tcurve_doppler"])
 def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     """A user density plugin (host-tabulated n(c, x)) with one infinite sample: that chord's column is
     inf, its phase takes the exact chord-order path (ocml exp, no windows), e^{-inf sigma} = 0 and
@@ -462,11 +474,14 @@ def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     # "doppler": orbital Doppler shift on, so the merged Na + K absorber takes the fused path (the tau kernel
     # looks sigma and the zero flags up itself)
     # fused rows (k_sigma_poly integrates the exact phase itself); "doppler_rows": the sigma-row path
-    monkeypatch.setenv("PROM_TAU_PLAN", "1" if plan.startswith("doppler") else plan)
+    # "tcurve", "tcurve_doppler": the transmission-curve path (k_sigma_tc integrates the exact phase itself)
+    tcurve = plan.startswith("tcurve")
+    monkeypatch.setenv("PROM_TCURVE", "1" if tcurve else "0")
+    monkeypatch.setenv("PROM_TAU_PLAN", "1" if (plan.startswith("doppler") or tcurve) else plan)
     monkeypatch.setenv("PROM_SIG_TAU", "0" if plan == "doppler_rows" else "1")
     cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
                           res_low=5e-9, res_high=1e-10)
-    cfg["Fundamentals"]["DopplerOrbitalMotion"] = plan.startswith("doppler")
+    cfg["Fundamentals"]["DopplerOrbitalMotion"] = plan.startswith("doppler") or plan == "tcurve_doppler"
     tr = _product_transit(cfg)
     scen, dop, grids = O.from_setup(cfg)
     base = scen[0]
@@ -507,6 +522,7 @@ def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     print("plan", plan, "exact phases", st["exact_phases"], "NaN points", int(np.isnan(Ro).sum()), "variant",
           st["tau_kernel_variant"])
     assert st["exact_phases"] == 1
+    assert (st["tau_kernel_variant"] == 81) == tcurve
     assert np.array_equal(np.isnan(R), np.isnan(Ro))
     m = ~np.isnan(Ro)
     assert rel(R[m], Ro[m]) < R_TOL
@@ -538,6 +554,7 @@ def test_sigma_rows_bitwise(dev, name, merge, monkeypatch):
     (Y = sum_s chi_s sigma_s) and per species: R is identical.  The polynomial rows (k_sigma_poly, the
     default: E_k e^a with a degree-D Taylor polynomial over the tables' {x, 10^y, ln10 slope} records) move
     sigma by ~1e-14 relative: R within 1e-13."""
+    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
     from prometheus_amd import configs
     cfg = configs.get(name) if name in ("C3", "C4") else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)

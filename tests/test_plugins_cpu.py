@@ -134,3 +134,25 @@ def test_lightcurve_oracle_matches_reference_script():
     planet = O.load_planet(cfg["Architecture"]["planetName"])
     lc = O.lightcurve(d["R"], d["wavelength"], d["orbphase"], planet)
     assert np.array_equal(lc, d["lightcurve"])
+
+
+def test_star_table_cache_follows_content():
+    """The device copy of an Fstar_function is cached per function object and content: replacing or
+    modifying its arrays in place gives a fresh table (no stale spectrum)."""
+    from prometheus_amd import gasProperties as gp
+
+    class Fn:
+        pass
+
+    fn = Fn()
+    fn.x = np.linspace(5e-5, 6e-5, 101)
+    fn.y = np.linspace(14.0, 14.5, 101)
+    t1 = gp._star_lookup_table(fn)
+    assert gp._star_lookup_table(fn) is t1            # unchanged: the cached table
+    fn.y[7] += 0.25                                    # in place
+    t2 = gp._star_lookup_table(fn)
+    assert t2 is not t1 and t2.y[7] == fn.y[7]
+    fn.y = fn.y.copy()                                 # replaced, same content: still valid
+    assert gp._star_lookup_table(fn) is t2
+    fn.x = fn.x * 1.0000001                            # replaced, new content
+    assert gp._star_lookup_table(fn) is not t2

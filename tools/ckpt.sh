@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-3 checkpoint on the committed tree: -m gpu suite, smoke, the default bench line (CPU legs +
+# Checkpoint on the committed tree: -m gpu suite, smoke, the default bench line (CPU legs +
 # strong-scaling projection), rocprofv3 kernel stats pipelined and isolated (one slot, no fork), FETCH /
 # WRITE traffic passes, the HBM microbenchmark.  Every GPU step has its own time limit; first failure ends it.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-T=${TAG:-r03ck}
+T=${TAG:-ckpt}
 O=$PWD/gpurun_out/$T
 mkdir -p $O
 has() { case " ${STEPS:-tests smoke bench stats traffic micro trace} " in *" $1 "*) return 0;; esac; return 1; }

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Workgroup timeline of k_sigma_poly (GPU box; libprom_hip_trace.so, every source built with -DPROM_TRACE):
-one run of a configuration in isolation, then per part (front = oversize blocks, global records; main =
-LDS blocks) the workgroups' start / end / duration percentiles on the wall clock (10 ns ticks).
+"""Workgroup timeline of the sigma kernel (k_sigma_tc on the transmission-curve path, k_sigma_poly with
+PROM_TCURVE=0; GPU box; libprom_hip_trace.so, every source built with -DPROM_TRACE): one run of a
+configuration in isolation, then per part (front = oversize blocks, global records; main = LDS blocks) the
+workgroups' start / end / duration percentiles on the wall clock (10 ns ticks).
     python tools/trace_sigma.py [C3]
 """
 import ctypes as C
@@ -23,22 +24,23 @@ dev = _native.get_device(0)
 host = tr._host_inputs()
 dev.transit_set(tr._problem(dev, host, 0, len(tr.wavelength), 0.0))
 lib = _native.load_library()
-lib.prom_sig_trace_read.restype = C.c_int32
-lib.prom_sig_trace_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int32, C.c_int32]
+rd = lib.prom_sig_trace_read if os.environ.get("PROM_TCURVE", "1") == "0" else lib.prom_tc_trace_read
+rd.restype = C.c_int32
+rd.argtypes = [C.POINTER(C.c_ulonglong), C.c_int32, C.c_int32]
 N = 1 << 20
 buf = (C.c_ulonglong * N)()
 for it in range(3):
-    lib.prom_sig_trace_read(buf, N, 1)
+    rd(buf, N, 1)
     dev.transit_run()
     dev.synchronize()
-lib.prom_sig_trace_read(buf, N, 0)
+rd(buf, N, 0)
 a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(-1, 4)
 a = a[a[:, 1] > 0]
 t0 = a[:, 0].min()
 st, en = (a[:, 0] - t0) * 0.01, (a[:, 1] - t0) * 0.01
 front = (a[:, 2] >> 33) & 1
 lds = (a[:, 2] >> 32) & 1
-print("%s k_sigma_poly: %d workgroups, span %.2f us" % (name, len(a), en.max()))
+print("%s sigma kernel: %d workgroups, span %.2f us" % (name, len(a), en.max()))
 for nm, m in (("front (oversize, global records)", front == 1), ("main (LDS slices)", (front == 0) & (lds == 1))):
     if not m.any():
         continue
