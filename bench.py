@@ -53,13 +53,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="C3")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--config", default=None,
+                    help="C1..C5, C4x10 (default: C3 on one GPU; C4x10, the 8-GPU configuration BASELINE.json names, "
+                         "for N > 1)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="N > 1: strong (default; the config's grid split into N shards) or weak (the grid at N x "
+                         "finer resolution, shard r on rank r)")
     ap.add_argument("--shard", default=None, metavar="r/N",
                     help="time only shard r of an N-way split of the config's grid (strong scaling, one process)")
-    ap.add_argument("--shard-axis", choices=("wavelength", "phase"), default="wavelength",
-                    help="strong splits (--shard, --scaling strong): contiguous wavelength ranges (default) or "
-                         "orbital-phase ranges (every wavelength, phases [o0, o1))")
+    ap.add_argument("--shard-axis", choices=("wavelength", "phase", "auto"), default="auto",
+                    help="strong splits (--shard, --scaling strong): contiguous wavelength ranges, orbital-phase "
+                         "ranges (every wavelength, phases [o0, o1)), or auto (default): phases when every rank "
+                         "gets the same number of them, else wavelengths")
     ap.add_argument("--no-projection", action="store_true",
                     help="skip the strong-scaling projection (C4x10 and C5, full grid vs shard 0 of 8)")
     ap.add_argument("--kernel-runs", type=int, default=20,
@@ -72,7 +77,21 @@ def parse():
                          "(tests: the gathered shards against a single-rank run)")
     ap.add_argument("--cpu-sample-wavelengths", type=int, default=None,
                     help="oracle sample size (default: ~10 s of reference-speed CPU work per config)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if a.config is None:
+        a.config = "C4x10" if (world > 1 and a.scaling != "weak") else "C3"
+    if a.scaling is None:
+        a.scaling = "strong" if world > 1 else "weak"
+    return a
+
+
+def resolve_axis(axis: str, n_orb: int, parts: int) -> str:
+    """auto: orbital phases when the phases split evenly over the parts (no rank repeats another's per-phase
+    chord work and the shards are equal), else wavelengths."""
+    if axis != "auto":
+        return axis
+    return "phase" if parts > 1 and n_orb % parts == 0 else "wavelength"
 
 
 def dist_env():
@@ -336,6 +355,7 @@ def main():
         sr, sn = rank, world
     o0, o1 = 0, n_orb_global
     opts = 0
+    args.shard_axis = resolve_axis(args.shard_axis, n_orb_global, sn)
     if args.shard_axis == "phase" and (args.shard or scaling == "strong"):
         w0, w1 = 0, n_wav_global
         o0, o1 = sharding.shard_for_rank(n_orb_global, sn, sr, align=1)

@@ -1054,9 +1054,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       rs.ncol.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * nc);
       tr.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
       if (n_mol > 0) {
-        tr.mol_ip.ensure(sizeof(int32_t) * n_mol * nc * tr.n_x);
-        tr.mol_wp.ensure(sizeof(double) * n_mol * nc * tr.n_x);
-        tr.mol_na.ensure(sizeof(double) * n_mol * nc * tr.n_x);
+        tr.mol_smp.ensure(sizeof(double) * 4 * n_mol * nc * tr.n_x);
+        tr.mol_nin.ensure(sizeof(int32_t) * n_mol * nc);
+        tr.mol_lst.ensure(sizeof(double) * 4 * n_mol * nc * tr.n_x);
+        tr.mol_rend.ensure(sizeof(int32_t) * nc);
       }
       rs.flags.ensure(sizeof(int32_t) * nc);
       rs.recs.ensure(sizeof(double) * nc * (1 + n_atoms));
@@ -1080,17 +1081,17 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       rs.hcnt.ensure(sizeof(int32_t) * 4);
       rs.trec.ensure(sizeof(int32_t) * 4 * n_orb * n_wtiles);   // {h, t, flags, 0} per (phase, tile)
       tr.taup_resident = 0;
-      tr.taup_resident_f = 0;
       rs.tsum.ensure(sizeof(double) * n_orb);
       rs.fsum.ensure(sizeof(double) * n_orb);
       rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);
       if (tr.tcurve) {
-        // k_tc_build: ~512 chords per part (at most 8), 4 octaves per chain
-        tr.tc_parts = (int32_t)std::max<int64_t>(1, std::min<int64_t>(8, tr.n_pr / 512));
-        const int64_t n_ch = (tr.tc_lg + 3) / 4;
+        // k_tc_build: ~512 chords per part, at most 1024 (a part's LDS stage) unless that needs more than 8 parts
+        tr.tc_parts = (int32_t)std::max<int64_t>(1, std::min<int64_t>(prom::kTcPartMax,
+                                                                      std::max<int64_t>(tr.n_pr / 512, (tr.n_pr + 1023) / 1024)));
+        const int64_t n_ch = (tr.tc_lg + prom::kTcChain - 1) / prom::kTcChain;
         rs.tc_hdr.ensure(sizeof(double) * n_orb * prom::kTcHdr);
         rs.tc_tab.ensure(sizeof(double) * n_orb * tr.tc_lg * prom::kTcD);
-        rs.tc_part.ensure(sizeof(double) * n_orb * n_ch * 8 * (4 * prom::kTcD + 8));
+        rs.tc_part.ensure(sizeof(double) * n_orb * n_ch * prom::kTcPartMax * prom::kTcPartVals);
         const size_t cb = sizeof(int32_t) * n_orb * n_ch;
         if (rs.tc_cnt.cap < cb) {
           rs.tc_cnt.ensure(cb);

@@ -284,36 +284,6 @@ __device__ __forceinline__ double sigma_seg_poly(double t, const SigTabDev& tb, 
   return sigma_poly_of(t, tb, pc, deg);
 }
 
-// The tau kernel's cross sections at (phase o, wavelength lam) on the fused path: FS table species; NS == 1
-// with FS > 1 is the merged absorber Y = sum_s chi_s sigma_s (and z: some chi_s sigma_s not > 0), else the
-// species' sigma_s.
-template <int FS, int NS>
-__device__ __forceinline__ void fused_sigma(const SigTabs4& tabf, const SigSeg* __restrict__ sg, int32_t o, double lam,
-                                            double (&out)[NS], bool* z, const PolyCoef& pc, int32_t deg) {
-  double v[FS];
-#pragma unroll
-  for (int s = 0; s < FS; ++s) {
-    const double t = tabf.t[s].shift[o] * lam;
-    v[s] = deg > 0 ? sigma_seg_poly(t, tabf.t[s], sg[s], pc, deg) : sigma_seg(t, tabf.t[s], sg[s]);
-  }
-  if constexpr (NS == 1 && FS > 1) {
-    double Y = 0.0;
-    bool zz = false;
-#pragma unroll
-    for (int s = 0; s < FS; ++s) {
-      const double cv = tabf.t[s].chi * v[s];
-      zz = zz || !(cv > 0.0);
-      Y += cv;
-    }
-    out[0] = Y;
-    *z = zz;
-  } else {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) out[s] = v[s];
-    *z = false;
-  }
-}
-
 // sigma_of for NS tables at once (the species of one wavelength): every table's directory load goes
 // out first, then every table's 4-node window (x and f, 64 B per target: the resampling kernel is bound
 // by the vector L1's bytes, so numpy.interp's slope is divided here rather than fetched), so a thread

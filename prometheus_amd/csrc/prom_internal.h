@@ -178,28 +178,6 @@ struct SigTabs4 {
   SigTabDev t[4];
 };
 
-// The integration half of the fused Doppler-row kernel (k_sigma_poly with TAU, prom_sigma.hip): k_order's
-// per-phase plan and the run's outputs.  One effective absorber (merged species, or one species).
-struct TauArgs {
-  const int32_t* counts;     // [n_orb][kCnt]
-  const int32_t* wenv;       // [n_orb][2][kEnvN] threshold -> record tables
-  const double* wmom;        // [n_orb][n_pr + 1][K] suffix tail moments
-  const double* recs;        // chord-order records {F, N} [n_orb][n_pr][2]
-  const double* mrecs;       // sorted / merged records, same layout
-  const int32_t* act_ip;     // [n_orb][n_pr] chord positions (exact path)
-  const double* fout;        // [n_pr] F_out (exact path)
-  const double* tfrac;       // [n_orb] transparent fraction
-  const double* fsum;        // [n_orb] F_out sum (exact path)
-  double* R;                 // [n_orb][n_wav]
-  double* sigh;              // [n_orb][n_wav]: Y of the heavy half tiles (read by k_tau_p's heavy entries)
-  int4* hlist;               // heavy entries: small list [hcap], then big list [hcap]
-  int32_t* hcnt;             // their counts (zeroed by k_columns8)
-  unsigned long long* evals; // [64] exp-evaluation counters (stats runs) or null
-  int64_t hcap;
-  int32_t n_pr, n_tiles;     // chords per phase, 128-wavelength tiles
-  double nscale;             // the effective absorber's 1 / c (tail polynomial argument q = Y nscale)
-};
-
 // The transmission-curve path (prom_tcurve.hip): per phase a header of kTcHdr doubles and kTcD Chebyshev
 // coefficients per octave of q = Y N_max.
 constexpr int kTcHdr = 16;
@@ -207,6 +185,9 @@ constexpr int kTcD = 16;
 enum : int { kTcHNmax = 0, kTcHTfrac = 1, kTcHFsum = 2, kTcHT0 = 3 /* .. 8: tail coefficients t_0 .. t_5 */,
              kTcHL = 9, kTcHFlags = 10 /* 1: opaque above the table, 2: non-finite columns */, kTcHNact = 11 };
 constexpr int kTcMaxOctaves = 64;
+constexpr int kTcChain = 4;                          // octaves per table exp (k_tc_build)
+constexpr int kTcPartMax = 8;                        // chord parts per (phase, chain)
+constexpr int kTcPartVals = (kTcChain + 1) * kTcD;   // doubles per part: node sums per octave, then the moments
 
 struct TcArgs {
   const double* hdr;         // [n_orb][kTcHdr]
@@ -328,7 +309,6 @@ struct TransitDev {
   // upper bounds of the normalised Q = sum_s sigma_s / c_s over every wavelength and phase (per species /
   // merged): k_order's always-tail threshold btail = tail epsilon / Q bound
   double qbound_v = 0.0, qbound_m = 0.0;
-  int taup_resident_f = 0;                  // resident workgroups of the fused planned tau kernel
   int32_t taup_resident = 0;                // k_tau_p wavefronts resident at once (set at the first run)
   // timed runs: k_tau_p stamps each workgroup's first and last device-clock tick into ts_out[2 b],
   // ts_out[2 b + 1] when it has at most ts_cap workgroups; ts_blocks reports the count (0: no stamps)
@@ -339,9 +319,12 @@ struct TransitDev {
   hipEvent_t* kprof = nullptr;
   uint32_t kprof_mask = 0;
   DevBuf molslot;                           // [n_mol] MolSlotDev
-  DevBuf mol_ip;                            // [n_mol][n_orb][n_pr][n_x] int32 P bracket (-1: out of table)
-  DevBuf mol_wp;                            // [n_mol][n_orb][n_pr][n_x] P weight
-  DevBuf mol_na;                            // [n_mol][n_orb][n_pr][n_x] n_abs = n chi
+  DevBuf mol_smp;                           // [n_mol][n_orb][n_pr][n_x] double4 {P weight, n_abs = n chi, P bracket,
+                                            //     0} of the in-table samples, compacted to the front of each chord
+  DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
+  DevBuf mol_lst;                           // [n_orb][n_pr n_mol n_x] double4: each phase's records' in-table
+                                            //     samples, one flat list (k_mol_list)
+  DevBuf mol_rend;                          // [n_orb][n_pr] int32: end of each record's samples in the list
   std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
   int32_t star_table_id = -1;               // prom_transit_problem.star_table (invalidation on free)
@@ -436,15 +419,10 @@ void launch_sigma_rows(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const 
 // the same rows with e^a polynomials over the tables' {x, 10^y, ln10 slope, x_next} records (prom_sigma.hip)
 void launch_sigma_poly(hipStream_t s, int32_t nsig, int32_t deg, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                        int32_t n_rows, const SigSeg* seg, const int32_t* fb, int32_t n_fb, double* sig, float4* tq,
-                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop,
-                       const TauArgs* tau = nullptr);
+                       int32_t merge_sp, double nscale_m, uint8_t* zfl, hipEvent_t ev_start, hipEvent_t ev_stop);
 // prom_transit_set: mark the sigma segments whose guess is numpy's bracket for every target (kind |= 4)
 void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav,
                       int32_t n_rows, SigSeg* seg, int32_t* flags);
-// fused Doppler path: half-tile Q bounds from the table nodes instead of the sigma rows (prom_sigma.hip)
-void launch_qbounds(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const double* wav, int64_t n_wav, int32_t n_rows,
-                    const SigSeg* seg, float4* tq, int32_t merge_sp, double nscale_m);
-// the fused tau kernels of the molecular and stellar-spectrum paths (prom_mol.hip, prom_rm.hip)
 // the transmission-curve path after the column kernel: k_tc_build, k_sigma_tc (prom_tcurve.hip);
 // the event pairs (may be null) ride on the two kernels' dispatch packets
 void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,

@@ -30,7 +30,8 @@ __device__ __forceinline__ double exp2_256(double y, const double* __restrict__ 
 template <int NSA, int EXPK>
 __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const SigTabDev* __restrict__ tabs,
                                                     const MolSlotDev* __restrict__ ms, int32_t n_mol,
-                                                    int32_t max_np, const double* __restrict__ wav,
+                                                    int32_t max_np, int64_t lst_stride,
+                                                    const double* __restrict__ wav,
                                                     const double* __restrict__ recs,
                                                     const int32_t* __restrict__ act_ip,
                                                     const double* __restrict__ fout,
@@ -39,9 +40,8 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
                                                     const double* __restrict__ fsum, int32_t n_pr,
                                                     int32_t n_orb, int32_t phases_per_group, int64_t n_wav,
                                                     int32_t n_x, double delta_x,
-                                                    const int32_t* __restrict__ mip,
-                                                    const double* __restrict__ mwp,
-                                                    const double* __restrict__ mna, double* __restrict__ R,
+                                                    const double4* __restrict__ lst,
+                                                    const int32_t* __restrict__ rend, double* __restrict__ R,
                                                     unsigned long long* __restrict__ evals) {
   extern __shared__ double lds[];   // [256] exp table 2^(i/256) | [n_mol][max_np][kBlock] u
   double* etab = lds;
@@ -61,11 +61,11 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
   for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); sg[s] = 0.0; }
   int64_t whint[4] = {-1, -1, -1, -1};
   unsigned long long npow = 0;   // stats runs: this lane's 10^v evaluations (in-table samples)
+
   uint32_t inb = 0;              // bit m: molecular slot m has (T, lambda') inside its table
   double lwprev[4];              // slot m's lambda' of the last u built in LDS (m < 4)
 #pragma unroll
   for (int m = 0; m < 4; ++m) lwprev[m] = __builtin_nan("");
-  const int64_t nc = (int64_t)n_orb * n_pr;
   for (int32_t o = o0; o < o1; ++o) {
     const bool exact = !EXPK || counts[o * kCnt + 3] != 0;
     const int32_t n_act = counts[o * kCnt + 0];
@@ -128,61 +128,113 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
     const int32_t* ipl = act_ip + (int64_t)o * n_pr;
     double acc = 0.0;
     const double scale = exact ? 1.0 : kM256Ln2;
-    int32_t ip_next = n_act > 0 ? ipl[0] : 0;
-    for (int32_t ci = 0; ci < n_act; ++ci) {
-      const double* r = rec + (int64_t)ci * ST;
-      const int32_t ip = ip_next;
-      if (ci + 1 < n_act) ip_next = ipl[ci + 1];   // the next chord's index is in flight meanwhile
+    // The phase's in-table samples are one flat list in record order (k_mol_list: {P weight, n_abs, slot << 16 |
+    // P bracket, offset}, record r's samples ending at rend[r]), read with wave-uniform scalar loads four at a
+    // time: the four samples' u reads, 10^v and products are independent; then they are added into the current
+    // record's sum, finishing records (e^-tau) at their ends.  Per sample n_abs (10^v - offset), the reference's
+    // order of the subtraction (gasProperties.py:811-818, 10**interp - offset).
+    const double4* __restrict__ lo = lst + (int64_t)o * lst_stride;
+    const int32_t* __restrict__ ro = rend + (int64_t)o * n_pr;
+    const int32_t K = n_act > 0 ? ro[n_act - 1] : 0;
+    int32_t r = 0;
+    int32_t end_r = n_act > 0 ? ro[0] : 0;
+    double sm = 0.0;
+    auto finish = [&](int32_t ri) {
+      const double* rr = rec + (int64_t)ri * ST;
       double tau = 0.0;
 #pragma unroll
-      for (int s = 0; s < NSA; ++s) tau = tau + r[1 + s] * sg[s];
-      for (int32_t m = 0; m < n_mol; ++m) {
-        if (!((inb >> m) & 1u)) continue;
-        const MolSlotDev d = ms[m];
-        const int64_t base = ((int64_t)m * nc + (int64_t)o * n_pr + ip) * n_x;
-        const double* um = ul + (int64_t)m * max_np * kBlock + threadIdx.x;
-        double sm = 0.0;
-        int32_t nin = 0;
-        // (uniform per wavefront: scalar loads, batched by the unroll)
+      for (int s = 0; s < NSA; ++s) tau = tau + rr[1 + s] * sg[s];
+      tau = tau + sm * delta_x;
+      sm = 0.0;
+      if (!exact) acc = acc_exp256(acc, rr[0], tau * scale, etab);
+      else acc = acc + fout[ipl[ri]] * exp(-tau);
+    };
+    for (int32_t k0 = 0; k0 < K; k0 += 4) {
+      double c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t k = k0 + j < K ? k0 + j : K - 1;
+        const double4 q = lo[k];
+        const int32_t code = (int32_t)q.z;
+        const int32_t m = code >> 16, pi = code & 0xffff;
+        const double* um = ul + ((int64_t)m * max_np + pi) * kBlock + threadIdx.x;
+        const double a = um[0], b = um[kBlock];
+        double e;
         if (EXPK && !exact) {
-          // table mode: v = u_i + t (u_{i+1} - u_i), 10^v = 2^(y/256) with y = v 256 log2(10) from the LDS table
-          // (relative error ~ |y| 2^-53 ln2/256 from the argument, ~1e-14 at the table's floor); the offset
-          // comes off once per chord, sum n (10^v - off) = sum n 10^v - off sum n (10^v >= off: no cancellation
-          // beyond off's own size)
-          double sn = 0.0;
-#pragma unroll 10
-          for (int32_t ix = 0; ix < n_x; ++ix) {
-            const int32_t pi = mip[base + ix];
-            if (pi < 0) break;   // (k_mol_prep: in-table samples first, then -1)
-            ++nin;
-            const double tp = mwp[base + ix];
-            const double a = um[(int64_t)pi * kBlock], b = um[(int64_t)(pi + 1) * kBlock];
-            const double v = __builtin_fma(tp, b - a, a);
-            const double na = mna[base + ix];
-            sm = __builtin_fma(na, exp2_256(v * kLog2Ten256, etab), sm);
-            sn += na;
-          }
-          sm = __builtin_fma(-d.offset, sn, sm);
+          // 10^v = 2^(y/256), y = v 256 log2(10), from the LDS table (relative error ~ |y| 2^-53 ln2/256 from the
+          // argument, ~1e-14 at the table's floor)
+          e = exp2_256(__builtin_fma(q.x, b - a, a) * kLog2Ten256, etab);
         } else {
-#pragma unroll 10
-          for (int32_t ix = 0; ix < n_x; ++ix) {
-            const int32_t pi = mip[base + ix];
-            if (pi < 0) break;
-            ++nin;
-            const double tp = mwp[base + ix];
-            const double v = (1.0 - tp) * um[(int64_t)pi * kBlock] + tp * um[(int64_t)(pi + 1) * kBlock];
-            sm = __builtin_fma(mna[base + ix], exp10(v) - d.offset, sm);
-          }
+          e = exp10((1.0 - q.x) * a + q.x * b);
         }
-        tau = tau + sm * delta_x;
-        npow += (unsigned)nin;
+        const bool in = ((inb >> m) & 1u) != 0;
+        c[j] = in ? q.y * (e - q.w) : 0.0;
+        npow += (in && k0 + j < K) ? 1u : 0u;
       }
-      if (!exact) acc = acc_exp256(acc, r[0], tau * scale, etab);
-      else acc = acc + fout[ip] * exp(-tau);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t k = k0 + j;
+        if (k >= K) break;
+        while (k >= end_r) {
+          finish(r);
+          ++r;
+          end_r = ro[r];
+        }
+        sm += c[j];
+      }
     }
+    for (; r < n_act; ++r) finish(r);
     if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
   }
   if (evals && live && npow) atomicAdd(&evals[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 63], npow);
+}
+
+// Per phase: the in-table samples of its records (k_chords' active chords, chord order) as one flat list for
+// k_tau_mol: record r's samples of every molecular slot (k_mol_prep's compacted rows) at [rend[r - 1], rend[r]),
+// each {P weight, n_abs, slot << 16 | P bracket, the slot's offset}.  One workgroup per phase.
+__global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restrict__ ms, int32_t n_mol,
+                                                     const int32_t* __restrict__ counts,
+                                                     const int32_t* __restrict__ act_ip,
+                                                     const double4* __restrict__ msmp,
+                                                     const int32_t* __restrict__ mnin, int32_t n_pr, int32_t n_orb,
+                                                     int32_t n_x, int64_t lst_stride, double4* __restrict__ lst,
+                                                     int32_t* __restrict__ rend) {
+  __shared__ int32_t wsum[kBlock / 64];
+  const int32_t o = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int32_t n_act = counts[o * kCnt];
+  const int64_t nc = (int64_t)n_orb * n_pr;
+  double4* lo = lst + (int64_t)o * lst_stride;
+  int32_t base = 0;
+  for (int32_t r0 = 0; r0 < n_act; r0 += kBlock) {
+    const int32_t r = r0 + tid;
+    const int32_t ip = r < n_act ? act_ip[(int64_t)o * n_pr + r] : 0;
+    int32_t cnt = 0;
+    for (int32_t m = 0; m < n_mol; ++m) cnt += r < n_act ? mnin[(int64_t)m * nc + (int64_t)o * n_pr + ip] : 0;
+    const int32_t inc = wave_prefix<int32_t>(cnt, OpAdd());
+    __syncthreads();
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int32_t pos = base + inc - cnt, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      if (w < wid) pos += wsum[w];
+      tot += wsum[w];
+    }
+    if (r < n_act) {
+      for (int32_t m = 0; m < n_mol; ++m) {
+        const int64_t cidx = (int64_t)m * nc + (int64_t)o * n_pr + ip;
+        const int32_t nin = mnin[cidx];
+        const double off = ms[m].offset;
+        for (int32_t k = 0; k < nin; ++k) {
+          const double4 q = msmp[cidx * n_x + k];
+          lo[pos++] = make_double4(q.x, q.y, (double)((m << 16) | (int32_t)q.z), off);
+        }
+      }
+      rend[(int64_t)o * n_pr + r] = pos;
+    }
+    base += tot;
+  }
 }
 
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg) {
@@ -200,6 +252,7 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
     for (const auto& m : tr.mslots) max_np = std::max(max_np, m.n_p);
     const size_t lds = kMolExpN * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
     PROM_REQUIRE(lds <= 160 * 1024, "transit: molecular tables too large for the LDS staging (n_mol * n_p)");
+    PROM_REQUIRE(tr.n_mol <= 4, "transit: at most 4 molecular constituents");
     // prom_transit_kernel_ms: the kernel's own dispatch-packet events
     hipEvent_t kps = nullptr, kpe = nullptr;
     if (tr.kprof) {
@@ -207,10 +260,15 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
       kps = tr.kprof[2 * PROM_K_TAU];
       kpe = tr.kprof[2 * PROM_K_TAU + 1];
     }
+    const int64_t lst_stride = (int64_t)tr.n_pr * tr.n_mol * tr.n_x;
+    hipLaunchKernelGGL(k_mol_list, dim3((unsigned)tr.n_orb), dim3(kBlock), 0, s, tr.molslot.as<MolSlotDev>(), tr.n_mol,
+                       counts, aip, tr.mol_smp.as<double4>(), tr.mol_nin.as<int32_t>(), tr.n_pr, tr.n_orb, tr.n_x,
+                       lst_stride, tr.mol_lst.as<double4>(), tr.mol_rend.as<int32_t>());
+    PROM_HIP(hipGetLastError());
 #define PROM_TAUM(NSV, EK)                                                                                  \
   hipExtLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, kps, kpe, 0, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
-                     max_np, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x,         \
-                     tr.delta_x, tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(), R, \
+                     max_np, lst_stride, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x, \
+                     tr.delta_x, tr.mol_lst.as<double4>(), tr.mol_rend.as<int32_t>(), R,                     \
                      tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr)
 #define PROM_TAUM_NS(EK)                \
   switch (na) {                         \

@@ -67,9 +67,8 @@ struct OpAddI { __device__ int32_t operator()(int32_t a, int32_t b) const { retu
 // node sums go to `part`; the last part to finish (atomic counter per (phase, chain), reset by it) adds them in
 // part order -- deterministic -- and writes the Chebyshev coefficients (and, chain 0, the header).
 constexpr int kTcB2 = 256;               // threads per workgroup
-constexpr int kTcChain = 4;              // octaves per table exp
-constexpr int kTcPartMax = 8;            // chord parts per (phase, chain)
-constexpr int kTcPartVals = kTcChain * kTcD + 8;   // doubles per part: node sums, then 6 moments
+constexpr int kTcPartLds = 1024;         // a part's chords staged in LDS up to this many (16 KB)
+static_assert(kTcPartVals == (kTcChain + 1) * kTcD, "per part: 4 octaves' node sums, then the moments' row");
 
 __device__ __forceinline__ double exp256(double y, const double* __restrict__ tab) {
   // 2^(y/256) for y = -x 256/ln2 (acc_exp256's arithmetic without the accumulation)
@@ -101,6 +100,7 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   __shared__ double red[NW][kTcChain + 1][kTcD];
   __shared__ double sf[kTcChain + 1][kTcD];
   __shared__ int32_t s_last;
+  __shared__ double2 spart[kTcPartLds];
   const int32_t* fl = flags + (int64_t)o * n_pr;
   const double* nc = ncol + (int64_t)o * n_pr;
   // the exp table and the Chebyshev matrix c_k = sum_j f_j cm[k][j] (one cosine per thread)
@@ -109,23 +109,42 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
     const int k = tid >> 4, jj = tid & 15;
     cm[tid] = cos(M_PI * (double)k * ((double)jj + 0.5) / (double)kTcD) * ((k == 0 ? 1.0 : 2.0) / (double)kTcD);
   }
-  // 1. the phase's sums (every workgroup of the phase, the same order)
+  // 1. the phase's sums (every workgroup of the phase, the same order).  Sweeps of kTcB2 x U chords, every load
+  // of a sweep issued before any is used (one round trip per sweep, no load behind a flag test); this part's
+  // chords [c_lo, c_hi) are kept in LDS on the way ({F_out, N}, zero for inactive chords) for step 2
+  const int32_t c_lo = (int32_t)((int64_t)n_pr * pt / n_parts), c_hi = (int32_t)((int64_t)n_pr * (pt + 1) / n_parts);
+  const bool in_lds = c_hi - c_lo <= kTcPartLds;
   double fs = 0.0, ts = 0.0, nmax = 0.0, nmin = __builtin_inf();
   int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0;
-  for (int32_t c = tid; c < n_pr; c += kTcB2) {
-    const int32_t f = fl[c];
-    const double fo = fout[c];
-    fs += fo;
-    if (f == 1) { ts += fo; ++ntr; }
-    else if (f == 2) ++nbl;
-    else if (f == 0) {
-      const double N = nc[c];
-      ++nact;
-      if (!__builtin_isfinite(N)) ++nnf;
-      else {
-        nmax = N > nmax ? N : nmax;
-        if (N > 0.0) nmin = N < nmin ? N : nmin;
+  constexpr int U = 8;
+  for (int32_t c0 = 0; c0 < n_pr; c0 += kTcB2 * U) {
+    int32_t f[U];
+    double fo[U], N[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t c = c0 + u * kTcB2 + tid;
+      const bool in = c < n_pr;
+      f[u] = in ? fl[c] : 3;
+      fo[u] = in ? fout[c] : 0.0;
+      N[u] = in ? nc[c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t c = c0 + u * kTcB2 + tid;
+      if (f[u] == 3) continue;
+      fs += fo[u];
+      if (f[u] == 1) { ts += fo[u]; ++ntr; }
+      else if (f[u] == 2) ++nbl;
+      else if (f[u] == 0) {
+        ++nact;
+        if (!__builtin_isfinite(N[u])) ++nnf;
+        else {
+          nmax = N[u] > nmax ? N[u] : nmax;
+          if (N[u] > 0.0) nmin = N[u] < nmin ? N[u] : nmin;
+        }
       }
+      if (in_lds && c >= c_lo && c < c_hi)
+        spart[c - c_lo] = f[u] == 0 ? make_double2(fo[u], N[u]) : make_double2(0.0, 0.0);
     }
   }
   fs = tc_wred<double>(fs, OpAdd());
@@ -166,9 +185,9 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   }
   const int32_t j0 = ch * kTcChain;
   if (ch > 0 && j0 >= L) return;   // (chain 0 always runs: the moments and the header)
-  // 2. this part's chords at this chain's nodes (and, chain 0, the moments)
+  // 2. this part's chords at this chain's nodes (and, chain 0, the moments); thread (k, g): node k, chords
+  // c_lo + g + 16 m from LDS (the 16 threads of a group read the same entry: a broadcast)
   const int k = tid & 15, g = tid >> 4;
-  const int32_t c_lo = (int32_t)((int64_t)n_pr * pt / n_parts), c_hi = (int32_t)((int64_t)n_pr * (pt + 1) / n_parts);
   double acc[kTcChain] = {0.0, 0.0, 0.0, 0.0};
   double mom = 0.0;
   const bool do_tab = fin && j0 < L;
@@ -181,8 +200,10 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   __syncthreads();   // etab, cm
   if (fin) {
     for (int32_t c = c_lo + g; c < c_hi; c += kTcB2 / 16) {
-      if (fl[c] != 0) continue;
-      const double F = fout[c] * inv_fs, N = nc[c];
+      double2 fn;
+      if (in_lds) fn = spart[c - c_lo];
+      else fn = fl[c] == 0 ? make_double2(fout[c], nc[c]) : make_double2(0.0, 0.0);
+      const double F = fn.x * inv_fs, N = fn.y;
       if (do_tab) {
         double e = exp256(N * sk, etab);
         acc[0] = __builtin_fma(F, e, acc[0]);
@@ -357,9 +378,16 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
     wb = grp * 8 + rem % 8;
     r0 = (int32_t)(rem / 8) * R;
     if (wb >= n_blk) return;
+    if constexpr (NT == 1) {
+      // one target row (one phase, or phases sharing one Doppler factor): no LDS slices -- each lane reads its
+      // own 32-byte record from the global table, adjacent wavelengths' records adjacent (coalesced), no
+      // barriers; every block here (the launcher passes no front)
+      lds_ok = false;
+    } else {
 #pragma unroll
-    for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
-    if (!lds_ok) return;   // (a front workgroup's)
+      for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
+      if (!lds_ok) return;   // (a front workgroup's)
+    }
   }
   const int32_t rlim = r0 + rcap < n_rows ? r0 + rcap : n_rows;
   rcap = rlim - r0;
@@ -369,9 +397,17 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
   const int64_t w = wb * kBlock + tid;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
+  // the rows' targets, once: every species of the effective absorber belongs to one density scenario (species
+  // merging) or there is one species, so they share the Doppler factors
+  double tt[NT];
+#pragma unroll
+  for (int r = 0; r < NT; ++r) tt[r] = tabv.t[0].shift[r0 + r < n_rows ? r0 + r : n_rows - 1] * lam;
+  // merged: acc = sum_s fl(chi_s E_k) e^a over the species, minus choff = sum_s fl(chi_s offset_s) once at the
+  // end (the same roundings: where every sigma_s is at the table floor, E_k = offset and a = 0, Y is exactly 0)
   double acc[NT];
 #pragma unroll
   for (int r = 0; r < NT; ++r) acc[r] = 0.0;
+  double choff = 0.0;
 #pragma unroll
   for (int s = 0; s < NSIG; ++s) {
     const SigTabDev& tb = tabv.t[s];
@@ -381,31 +417,29 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
       // block's verified guess into the global x / f arrays), bit for bit the per-target lookups
 #pragma unroll
       for (int r = 0; r < NT; ++r) {
-        const double t = tb.shift[r0 + r < n_rows ? r0 + r : n_rows - 1] * lam;
-        const double v = sigma_seg(t, tb, sg);
+        const double v = sigma_seg(tt[r], tb, sg);
         if constexpr (MG) acc[r] += tb.chi * v;
         else acc[r] = v;
       }
       continue;
     }
+    const double off = tb.offset, chi = tb.chi;
+    if constexpr (MG) choff += chi * off;
     if (lds_ok) {
       if (s > 0) __syncthreads();   // the previous species' slice is no longer read
       for (int32_t i = tid; i < sg.m; i += kBlock) {
         const double4 q = tb.rec[sg.lo + i];
         sxr[i] = make_double2(q.x, q.w);
-        sel[i] = make_double2(q.y, q.z);
+        sel[i] = make_double2(MG ? chi * q.y : q.y, q.z);
       }
       __syncthreads();
     }
     const bool exact = (sg.kind & 4) != 0;
-    const double off = tb.offset, chi = tb.chi;
-    auto emit = [&](int r, double v) {
-      if constexpr (MG) acc[r] += chi * v;
-      else acc[r] = v;
+    // v = (chi) E_k e^a: merged, accumulated; one species, sigma = E_k e^a - offset
+    auto emit = [&](int r, double ce, double p) {
+      if constexpr (MG) acc[r] = __builtin_fma(ce, p, acc[r]);
+      else acc[r] = __builtin_fma(ce, p, -off);
     };
-    double tt[NT];
-#pragma unroll
-    for (int r = 0; r < NT; ++r) tt[r] = tb.shift[r0 + r < n_rows ? r0 + r : n_rows - 1] * lam;
     const int32_t ncap = UNI ? 1 : rcap;
     if (!lds_ok) {
       if ((sg.kind & 3) > 0) {
@@ -428,12 +462,16 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
           }
 #pragma unroll
           for (int jj = 0; jj < G; ++jj)
-            emit(r0g + jj, __builtin_fma(q[jj].y, exp_taylor<D>(q[jj].z * (tt[r0g + jj] - q[jj].x), pc), -off));
+            emit(r0g + jj, MG ? chi * q[jj].y : q[jj].y, exp_taylor<D>(q[jj].z * (tt[r0g + jj] - q[jj].x), pc));
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < NT; ++r)
-          if (r < ncap) emit(r, sigma_poly_of(tt[r], tb, pc, D));
+        for (int r = 0; r < NT; ++r) {
+          if (r >= ncap) continue;
+          const double v = sigma_poly_of(tt[r], tb, pc, D);
+          if constexpr (MG) acc[r] = __builtin_fma(chi, v + off, acc[r]);   // (sigma + offset = E_k e^a)
+          else acc[r] = v;
+        }
       }
     } else {
       auto lds_rows = [&](auto guard) {
@@ -457,12 +495,16 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
 #pragma unroll
         for (int r = 0; r < NT; ++r) {
           if (GD && r >= ncap) break;
-          emit(r, __builtin_fma(el[r].x, exp_taylor<D>(el[r].y * (tt[r] - xk[r]), pc), -off));
+          emit(r, el[r].x, exp_taylor<D>(el[r].y * (tt[r] - xk[r]), pc));
         }
       };
       if (ncap >= NT) lds_rows(std::false_type{});
       else lds_rows(std::true_type{});
     }
+  }
+  if constexpr (MG && D > 0) {
+#pragma unroll
+    for (int r = 0; r < NT; ++r) acc[r] -= choff;
   }
   // R = T_o(Y) per (phase, wavelength)
 #pragma unroll
@@ -570,7 +612,10 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   // 16384 (block, row) pairs of them (profiles/r03_sigma_rf_sweep.txt); one shared target: all R
   int RF = R;
   if (!uni && R >= 2 && (nsig >= 2 || (int64_t)tr.n_sig_fb * n_rows < 16384)) RF = R / 2;
-  const int32_t n_fb = tr.n_sig_fb;
+  // one target row (NT == 1: no Doppler shift between the phases, or one phase): every block reads the global
+  // records directly, no front of oversize blocks
+  const bool direct = uni || R == 1;
+  const int32_t n_fb = direct ? 0 : tr.n_sig_fb;
   const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
   const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
   const PolyCoef& pc = poly_coef();

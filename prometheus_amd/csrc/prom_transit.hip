@@ -48,8 +48,8 @@ __global__ void k_ntot(DensityDev m, int32_t sc, const double* __restrict__ x, i
 // outside: RegularGridInterpolator's fill, 10^fill - offset = 0), the P weight, and n_abs = n_tot chi.
 // molcol[m][o][ip] = sum_x n_abs dx over in-table samples (the chord's bound / sigma_max).
 __global__ void k_mol_prep(const MolSlotDev* __restrict__ ms, int32_t n_mol, const double* __restrict__ ntot,
-                           int32_t n_x, int32_t n_pr, int32_t n_orb, double delta_x, int32_t* __restrict__ mip,
-                           double* __restrict__ mwp, double* __restrict__ mna, double* __restrict__ molcol) {
+                           int32_t n_x, int32_t n_pr, int32_t n_orb, double delta_x, double4* __restrict__ msmp,
+                           int32_t* __restrict__ mnin, double* __restrict__ molcol) {
   const int64_t nc = (int64_t)n_orb * n_pr;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc * n_mol;
        c += (int64_t)gridDim.x * blockDim.x) {
@@ -57,8 +57,9 @@ __global__ void k_mol_prep(const MolSlotDev* __restrict__ ms, int32_t n_mol, con
     const int64_t cc = c - (int64_t)m * nc;
     const MolSlotDev d = ms[m];
     const double* row = ntot + ((int64_t)d.scenario * nc + cc) * n_x;
-    // in-table samples are compacted to the front of the chord's row in sample order, then -1 (k_tau_mol
-    // stops there: out-of-table samples contribute nothing, so the sum over the kept ones is unchanged)
+    // in-table samples are compacted to the front of the chord's row in sample order as {P weight, n_abs,
+    // P bracket, 0}, their count in mnin (out-of-table samples contribute nothing, so the sum over the kept
+    // ones is unchanged)
     double col = 0.0;
     const int64_t k0 = ((int64_t)m * nc + cc) * n_x;
     int32_t nin = 0;
@@ -71,13 +72,11 @@ __global__ void k_mol_prep(const MolSlotDev* __restrict__ ms, int32_t n_mol, con
       const bool in = rgi_bracket(d.P, d.n_p, P, &i, &t);
       if (!in) continue;
       const double na = n * d.chi;
-      mip[k0 + nin] = (int32_t)i;
-      mwp[k0 + nin] = t;
-      mna[k0 + nin] = na;
+      msmp[k0 + nin] = make_double4(t, na, (double)i, 0.0);
       ++nin;
       col += na * delta_x;
     }
-    for (int32_t ix = nin; ix < n_x; ++ix) mip[k0 + ix] = -1;
+    mnin[(int64_t)m * nc + cc] = nin;
     molcol[(int64_t)m * nc + cc] = col;
   }
 }
@@ -1809,22 +1808,16 @@ __device__ __forceinline__ void tau_count(unsigned long long* __restrict__ evals
 
 // One heavy entry {half tile, h, t, flags | phase << 8}: this lane's wavelength, its cross-sections (row of
 // the entry's phase when PH), the record source, the first chunk `first` preloaded into nx.
-template <int NS, bool PH, int FS>
+template <int NS, bool PH>
 __device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const double* __restrict__ sig,
                                             const double* __restrict__ recs, const double* __restrict__ mrecs,
                                             int32_t n_pr, int64_t n_wav, int lane, int64_t* w, bool* live,
-                                            double (&sg)[1][NS], const double** src, double (&nx)[1 + NS],
-                                            const SigTabs4& tabf, const SigSeg* __restrict__ fseg,
-                                            const double* __restrict__ wav, const PolyCoef& pc, int32_t sdeg) {
+                                            double (&sg)[1][NS], const double** src, double (&nx)[1 + NS]) {
   constexpr int ST = 1 + NS;
   const int32_t o = en.w >> 8;
   *w = (int64_t)en.x * 64 + lane;
   *live = *w < n_wav;
-  if constexpr (FS > 0) {
-    const int64_t wc = *live ? *w : n_wav - 1;
-    bool z;
-    fused_sigma<FS, NS>(tabf, fseg + ((int64_t)en.x * 64 / kBlock) * FS, o, wav[wc], sg[0], &z, pc, sdeg);
-  } else {
+  {
     const double* so = sig + (PH ? (int64_t)o * NS * n_wav : 0);
 #pragma unroll
     for (int s = 0; s < NS; ++s) sg[0][s] = so[(int64_t)s * n_wav + (*live ? *w : n_wav - 1)];
@@ -1842,7 +1835,7 @@ __device__ __forceinline__ void heavy_setup(const int4 en, int32_t first, const 
 // blockIdx.x * 4 + wid < n_static): tile sw % n_tiles, phases 4 (sw / n_tiles) ...; round trip 1 = its
 // phases' tile records {h, t, flags, tail moments} (k_order), sigma at its 128 wavelengths (2 per lane), the
 // exp table; a second round trip only for the packed records of non-empty light windows.
-template <int NS, bool PH, int FS, int WPG>
+template <int NS, bool PH, int WPG>
 __global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_tau_p(const SigTabs4 tabv, const double* __restrict__ sig,
                                                                    const double* __restrict__ recs,
                                                                    const double* __restrict__ mrecs,
@@ -1859,12 +1852,7 @@ __global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_
                                                                    int32_t n_static, const uint8_t* __restrict__ zfl,
                                                                    unsigned long long* __restrict__ evals,
                                                                    unsigned long long* __restrict__ tstamp,
-                                                                   double* __restrict__ R, const SigTabs4 tabf,
-                                                                   const SigSeg* __restrict__ fseg,
-                                                                   const double* __restrict__ wav,
-                                                                   const PolyCoef pc, int32_t sdeg) {
-  // FS > 0 (fused Doppler path): the cross sections of the FS table species are looked up here
-  // (fused_sigma) instead of read from sigma rows; merged absorbers also get their zero flags here
+                                                                   double* __restrict__ R) {
   constexpr int K = Monos<NS>::K;
   constexpr int ST = 1 + NS;
   constexpr int PQ = (4 * kHeavy * ST + 63) / 64;   // packed record loads per lane
@@ -1899,36 +1887,15 @@ __global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_
   const int4 tv = lane < np ? trec[(int64_t)(o0 + lane) * n_tiles + tile] : make_int4(0, 0, 0, 0);
   bool live[2];
   double sg[SR][2][NS];
-  bool zb[SR][2];
-  if constexpr (FS > 0) {
-    const SigSeg* fs_tile = fseg + ((int64_t)tile * kTW / kBlock) * FS;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
-      live[j] = w < n_wav;
-      const double lam = wav[live[j] ? w : n_wav - 1];
+  for (int j = 0; j < 2; ++j) {
+    const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
+    live[j] = w < n_wav;
 #pragma unroll
-      for (int r = 0; r < SR; ++r) {
-        if (r < np) fused_sigma<FS, NS>(tabf, fs_tile, o0 + r, lam, sg[r][j], &zb[r][j], pc, sdeg);
-        else {
+    for (int r = 0; r < SR; ++r) {
+      const double* so = sig + (PH ? (int64_t)(o0 + r) * NS * n_wav : 0);
 #pragma unroll
-          for (int s = 0; s < NS; ++s) sg[r][j][s] = 0.0;
-          zb[r][j] = false;
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t w = (int64_t)tile * kTW + 64 * j + lane;
-      live[j] = w < n_wav;
-#pragma unroll
-      for (int r = 0; r < SR; ++r) {
-        const double* so = sig + (PH ? (int64_t)(o0 + r) * NS * n_wav : 0);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) sg[r][j][s] = r < np ? so[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)] : 0.0;
-        zb[r][j] = false;
-      }
+      for (int s = 0; s < NS; ++s) sg[r][j][s] = r < np ? so[(int64_t)s * n_wav + (live[j] ? w : n_wav - 1)] : 0.0;
     }
   }
   double tfv[4];
@@ -1948,8 +1915,8 @@ __global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_
     bool lv;
     double sgh[1][NS], nx[ST];
     const double* src;
-    heavy_setup<NS, PH, FS>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), wid, sig, recs, mrecs, n_pr,
-                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav, pc, sdeg);
+    heavy_setup<NS, PH>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), wid, sig, recs, mrecs, n_pr,
+                        n_wav, lane, &w, &lv, sgh, &src, nx);
     double mm[K];
     if (wid == 0 && (f4 & 2)) {
       const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;   // t <= G <= n_pr: the row exists
@@ -1997,8 +1964,8 @@ __global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_
     bool lv;
     double sgh[1][NS], nx[ST];
     const double* src;
-    heavy_setup<NS, PH, FS>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), 0, sig, recs, mrecs, n_pr,
-                            n_wav, lane, &w, &lv, sgh, &src, nx, tabf, fseg, wav, pc, sdeg);
+    heavy_setup<NS, PH>(make_int4(__builtin_amdgcn_readfirstlane(en.x), h, t, f4), 0, sig, recs, mrecs, n_pr,
+                        n_wav, lane, &w, &lv, sgh, &src, nx);
     const double* mp = wmom + ((int64_t)o * (n_pr + 1) + t) * K;
     double mm[K];
 #pragma unroll
@@ -2120,9 +2087,7 @@ __global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_
             double tau = rr[1] * sg[r][j][0];
 #pragma unroll
             for (int s = 1; s < NS; ++s) tau = tau + rr[1 + s] * sg[r][j][s];
-            if constexpr (FS > 1 && NS == 1) {
-              if (!__builtin_isfinite(rr[1]) && zb[r][j]) tau = __builtin_nan("");
-            } else if (NS == 1 && zo) {
+            if (NS == 1 && zo) {
               tau = exact_tau_merged(rr[1], sg[r][j][0], zo, live[j] ? (int64_t)tile * kTW + 64 * j + lane : n_wav - 1);
             }
             acc[j] = acc[j] + F * exp(-tau);
@@ -2156,7 +2121,7 @@ __global__ void __launch_bounds__(WPG * 64, WPG == 4 ? (NS <= 2 ? 5 : 3) : 1) k_
 // The Doppler cross-section rows of one run: polynomial rows (k_sigma_poly) when the problem's tables allow
 // them (TransitDev::sig_deg), else the exp10 rows (k_sigma_rows)
 static void launch_rows(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, int32_t sig_rows, bool msp,
-                        hipEvent_t ev_start, bool rows_out = true) {
+                        hipEvent_t ev_start) {
   hipEvent_t ev_stop = nullptr;
   if (tr.kprof) {
     tr.kprof_mask |= 1u << PROM_K_SIGMA;
@@ -2166,8 +2131,8 @@ static void launch_rows(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig
   if (tr.sig_deg > 0)
     launch_sigma_poly(s, nsig, tr.sig_deg, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
                       tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb,
-                      rows_out ? rs.sig.as<double>() : nullptr, rs.tq.as<float4>(), msp ? 1 : 0,
-                      tr.sigtab_m.t[0].nscale, rows_out ? rs.zfl.as<uint8_t>() : nullptr, ev_start, ev_stop);
+                      rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale,
+                      rs.zfl.as<uint8_t>(), ev_start, ev_stop);
   else
     launch_sigma_rows(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
                       tr.sig_fb.as<int32_t>(), tr.n_sig_fb, rs.sig.as<double>(), rs.tq.as<float4>(), msp ? 1 : 0,
@@ -2200,22 +2165,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // species merging (TransitDev::species_merge_ok) on the resampled fast path: downstream of the
   // column kernel there is one effective absorber
   const bool msp = pre_sigma && tr.species_merge_ok;
-  // fused Doppler path (opt-in, PROM_FUSED=1): no sigma rows in HBM; the planned tau kernel looks the cross
-  // sections up itself (per-lane gathers from the global tables) and k_order / k_windows take node-range Q
-  // bounds (k_qbounds).  Correct (test_fused_sigma) but slower on C3: 122 us for the fused tau kernel and
-  // 1 ms for the bounds' node scans against 48 + 28 us for k_sigma_rows + k_tau_p (DESIGN.md "Tried").
-  const char* fenv = std::getenv("PROM_FUSED");
-  const bool fused = pre_sigma && !tr.uniform_shift && tr.sig_seg_ok && tr.plan && tr.n_atoms <= 4 &&
-                     fenv && std::atoi(fenv) != 0;
   const int32_t nsig = tr.n_atoms;                 // species the column kernel resamples
   const int32_t na = msp ? 1 : tr.n_atoms;         // species the ordering and tau kernels see
-  // fused Doppler rows (default; PROM_SIG_TAU=0: off): the polynomial row kernel runs after k_order and
-  // integrates every light (row, half tile) window itself -- no Y rows / zero flags in HBM, no k_windows --
-  // leaving the heavy half tiles to k_tau_p's entry lists.  One effective absorber (merged species or one
-  // species), planned windows.
-  const char* stenv = std::getenv("PROM_SIG_TAU");
-  const bool sig_tau = pre_sigma && !fused && !tr.uniform_shift && tr.sig_seg_ok && tr.sig_deg > 0 && tr.plan &&
-                       na == 1 && !(stenv && std::atoi(stenv) == 0);
   const ColArgs& cargs = msp ? tr.colargs_m : tr.colargs;
   const int32_t n_terms = msp ? 1 : tr.n_terms;
   const double* smax = msp ? tr.sigma_max_m.as<double>() : tr.sigma_max_dev.as<double>();
@@ -2274,9 +2225,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
     // orbital Doppler shift with sigma segments: the rows come from their own kernel (k_sigma_rows)
     const bool rows_seg = pre_sigma && !tr.uniform_shift && tr.sig_seg_ok;   // (one row per phase, even one phase)
-    // fused with the polynomial rows: k_sigma_poly still gives the half-tile Q ranges (no rows stored)
-    const bool fused_poly = fused && tr.sig_deg > 0;
-    const bool sig_fork = rows_seg && !sig_tau && (!fused || fused_poly) && rs.aux && rs.ev_fork && rs.ev_join;
+    const bool sig_fork = rows_seg && rs.aux && rs.ev_fork && rs.ev_join;
     const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
     const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
     // the sigma rows do not depend on the columns or the ordering: with a second stream for the slot they
@@ -2284,26 +2233,17 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     // join before the tile windows.  The fork point is taken before the column kernel is queued (the rows
     // wait only for the slot's previous run); PROM_SIGMA_FIRST=1 queues them before the column kernel.
     const bool sig_first = !sig_fork || (std::getenv("PROM_SIGMA_FIRST") && std::atoi(std::getenv("PROM_SIGMA_FIRST")));
-    sig_after_order = rows_seg && !fused && !sig_fork && (rs.sig_late || sig_tau) && wpath;
+    sig_after_order = rows_seg && !sig_fork && rs.sig_late && wpath;
     if (sig_fork) {
       PROM_HIP(hipEventRecord(rs.ev_fork, s));
       PROM_HIP(hipStreamWaitEvent(rs.aux, rs.ev_fork, 0));
     }
     auto sigma_rows = [&]() {
-#ifdef PROM_PROFILE_PARTS
-      // (profiling builds: PROM_FUSED_ROWS=1 also stores the sigma rows of the fused path)
-      static const bool dbg_rows = std::getenv("PROM_FUSED_ROWS") && std::atoi(std::getenv("PROM_FUSED_ROWS"));
-#else
-      constexpr bool dbg_rows = false;
-#endif
-      launch_rows(sig_fork ? rs.aux : s, tr, rs, nsig, sig_rows, msp, sig_fork ? nullptr : ev0, !fused || dbg_rows);
+      launch_rows(sig_fork ? rs.aux : s, tr, rs, nsig, sig_rows, msp, sig_fork ? nullptr : ev0);
       if (sig_fork) PROM_HIP(hipEventRecord(rs.ev_join, rs.aux));
       else ev0 = nullptr;
     };
-    if (fused && !fused_poly) {
-      launch_qbounds(s, nsig, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows, tr.sig_seg.as<prom::SigSeg>(),
-                     rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale);
-    } else if (rows_seg && sig_first && !sig_after_order) {
+    if (rows_seg && sig_first && !sig_after_order) {
       sigma_rows();
     }
     if (!pre_sigma || rows_seg) { PROM_COLS_L(0) }
@@ -2312,7 +2252,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     else if (nsig == 3) { PROM_COLS_L(3) }
     else { PROM_COLS_L(4) }
     PROM_HIP(hipGetLastError());
-    if (rows_seg && (!fused || fused_poly) && !sig_first) sigma_rows();
+    if (rows_seg && !sig_first) sigma_rows();
     ev0 = nullptr;
   } else {
     if (ev0) PROM_HIP(hipEventRecord(ev0, s));
@@ -2332,7 +2272,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     if (tr.n_mol > 0) {
       hipLaunchKernelGGL(k_mol_prep, dim3(grid_for(nc * tr.n_mol, 64)), dim3(64), 0, s, tr.molslot.as<MolSlotDev>(),
                          tr.n_mol, tr.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
-                         tr.mol_ip.as<int32_t>(), tr.mol_wp.as<double>(), tr.mol_na.as<double>(),
+                         tr.mol_smp.as<double4>(), tr.mol_nin.as<int32_t>(),
                          tr.molcol.as<double>());
       PROM_HIP(hipGetLastError());
     }
@@ -2364,7 +2304,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   if (wpath) {
 #define PROM_CHW(NSV)                                                                                   \
   hipExtLaunchKernelGGL(k_order<NSV>, dim3(tr.n_orb), dim3(kWBlock), 0, s, kp_start(tr, PROM_K_ORDER, nullptr),    \
-                     kp_stop(tr, PROM_K_ORDER, (pre_sigma && !sig_tau) ? nullptr : ev_ord), 0,             \
+                     kp_stop(tr, PROM_K_ORDER, pre_sigma ? nullptr : ev_ord), 0,                           \
                      rs.flags.as<int32_t>(),                                                              \
                      tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb, tr.merge ? 1 : 0,   \
                      tr.window ? 1 : 0, tabs4, rs.recs.as<double>(),                                     \
@@ -2385,42 +2325,12 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       default: PROM_CHW(4); break;
     }
 #undef PROM_CHW
-    if (sig_tau) {
-      // 2b'. fused rows: sigma, Q ranges, windows and the light windows' integration in one kernel
-      TauArgs ta{};
-      ta.counts = rs.counts.as<int32_t>();
-      ta.wenv = rs.wenv.as<int32_t>();
-      ta.wmom = rs.wmom.as<double>();
-      ta.recs = rs.recs.as<double>();
-      ta.mrecs = rs.mrecs.as<double>();
-      ta.act_ip = rs.act_ip.as<int32_t>();
-      ta.fout = tr.cfout.as<double>();
-      ta.tfrac = rs.tsum.as<double>();
-      ta.fsum = rs.fsum.as<double>();
-      ta.R = rs.R.as<double>();
-      ta.sigh = rs.sig.as<double>();
-      ta.hlist = rs.hlist.as<int4>();
-      ta.hcnt = rs.hcnt.as<int32_t>();
-      ta.evals = tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr;
-      ta.hcap = hcap;
-      ta.n_pr = tr.n_pr;
-      ta.n_tiles = n_wtiles;
-      ta.nscale = tabs4.t[0].nscale;
-      hipEvent_t e0 = ev_tau0, e1 = nullptr;
-      if (tr.kprof) {
-        tr.kprof_mask |= 1u << PROM_K_SIGMA;
-        e0 = tr.kprof[2 * PROM_K_SIGMA];
-        e1 = tr.kprof[2 * PROM_K_SIGMA + 1];
-      }
-      launch_sigma_poly(s, nsig, tr.sig_deg, tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, sig_rows,
-                        tr.sig_seg.as<prom::SigSeg>(), tr.sig_fb.as<int32_t>(), tr.n_sig_fb, nullptr,
-                        rs.tq.as<float4>(), msp ? 1 : 0, tr.sigtab_m.t[0].nscale, nullptr, e0, e1, &ta);
-    } else if (sig_after_order) {
+    if (sig_after_order) {
       launch_rows(s, tr, rs, nsig, sig_rows, msp, nullptr);
     }
-    if (pre_sigma && !sig_tau) {
+    if (pre_sigma) {
       // 2b. every tile's window from the tables and the Q ranges (after the sigma rows: join)
-      if (!tr.uniform_shift && tr.sig_seg_ok && (!fused || tr.sig_deg > 0) && rs.aux && rs.ev_join)
+      if (!tr.uniform_shift && tr.sig_seg_ok && rs.aux && rs.ev_join)
         PROM_HIP(hipStreamWaitEvent(s, rs.ev_join, 0));
       const dim3 gw((unsigned)((n_wtiles + kBlock - 1) / kBlock), (unsigned)tr.n_orb);
 #define PROM_WIN(NSV)                                                                                    \
@@ -2505,66 +2415,40 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       // planned: big and small heavy entries from k_order's lists over the whole grid, then one static
       // wavefront per (tile, 4 phases)
       const bool ph = sig_rows > 1;
-      const int fsv = fused ? nsig : 0;   // table species the tau kernel looks up (0: reads sigma rows)
-      int& resident = fused ? tr.taup_resident_f : tr.taup_resident;
+      int& resident = tr.taup_resident;
       if (resident == 0) {
         int cus = 0, nb = 0;
         int dev = 0;
         PROM_HIP(hipGetDevice(&dev));
         PROM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-#define PROM_OCC(NSV, PHV, FSV) PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, PHV, FSV, kTauWpg>, kTauWpg * 64, 0))
-        if (fused) {
-          if (na == 1) {
-            switch (fsv) { case 1: PROM_OCC(1, true, 1); break; case 2: PROM_OCC(1, true, 2); break;
-                           case 3: PROM_OCC(1, true, 3); break; default: PROM_OCC(1, true, 4); break; }
-          } else {
-            switch (na) { case 2: PROM_OCC(2, true, 2); break; case 3: PROM_OCC(3, true, 3); break;
-                          default: PROM_OCC(4, true, 4); break; }
-          }
-        } else {
-          switch (na) {
-            case 1: if (ph) { PROM_OCC(1, true, 0); } else { PROM_OCC(1, false, 0); } break;
-            case 2: if (ph) { PROM_OCC(2, true, 0); } else { PROM_OCC(2, false, 0); } break;
-            case 3: if (ph) { PROM_OCC(3, true, 0); } else { PROM_OCC(3, false, 0); } break;
-            default: if (ph) { PROM_OCC(4, true, 0); } else { PROM_OCC(4, false, 0); } break;
-          }
+#define PROM_OCC(NSV, PHV) PROM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tau_p<NSV, PHV, kTauWpg>, kTauWpg * 64, 0))
+        switch (na) {
+          case 1: if (ph) { PROM_OCC(1, true); } else { PROM_OCC(1, false); } break;
+          case 2: if (ph) { PROM_OCC(2, true); } else { PROM_OCC(2, false); } break;
+          case 3: if (ph) { PROM_OCC(3, true); } else { PROM_OCC(3, false); } break;
+          default: if (ph) { PROM_OCC(4, true); } else { PROM_OCC(4, false); } break;
         }
 #undef PROM_OCC
         resident = std::max(1, cus) * std::max(1, nb);   // workgroups resident at once
       }
-      // fused rows: the static units are done; the grid takes the heavy entries only
-      const int64_t n_static = sig_tau ? 0 : (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
+      const int64_t n_static = (int64_t)n_wtiles * ((tr.n_orb + 3) / 4);
       const int64_t blocks = std::max<int64_t>((n_static + kTauWpg - 1) / kTauWpg, resident);
-      *variant = (sig_tau ? 70 : 30) + (na <= 4 ? na : 0);
-      unsigned long long* tsp = (tr.ts_out && blocks <= tr.ts_cap && !sig_tau) ? tr.ts_out : nullptr;
+      *variant = 30 + (na <= 4 ? na : 0);
+      unsigned long long* tsp = (tr.ts_out && blocks <= tr.ts_cap) ? tr.ts_out : nullptr;
       tr.ts_blocks = tsp ? (int32_t)blocks : 0;
-#define PROM_TAUP(NSV, PHV, FSV)                                                                        \
-  hipExtLaunchKernelGGL((k_tau_p<NSV, PHV, FSV, kTauWpg>), dim3((unsigned)blocks), dim3(kTauWpg * 64), 0, s, \
-                        kp_start(tr, PROM_K_TAU, sig_tau ? nullptr : ev_tau0), kp_stop(tr, PROM_K_TAU, ev ? ev[3] : nullptr), 0, \
+#define PROM_TAUP(NSV, PHV)                                                                             \
+  hipExtLaunchKernelGGL((k_tau_p<NSV, PHV, kTauWpg>), dim3((unsigned)blocks), dim3(kTauWpg * 64), 0, s,   \
+                        kp_start(tr, PROM_K_TAU, ev_tau0), kp_stop(tr, PROM_K_TAU, ev ? ev[3] : nullptr), 0, \
                         tabs4, rs.sig.as<double>(),                                                      \
                         recs, mrecs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, tr.n_wav,                \
                         rs.wmom.as<double>(), rs.trec.as<int4>(), n_wtiles, rs.hlist.as<int4>(),        \
-                        hcap, rs.hcnt.as<int32_t>(), (int32_t)n_static,                                 \
-                        (msp && !fused) ? rs.zfl.as<uint8_t>() : nullptr,                                \
-                        tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tsp, R,           \
-                        tr.sigtab_v, tr.sig_seg.as<prom::SigSeg>(), tr.wav.as<double>(), poly_coef(),   \
-                        fused ? tr.sig_deg : 0)
-      if (fused) {
-        if (na == 1) {
-          switch (fsv) { case 1: PROM_TAUP(1, true, 1); break; case 2: PROM_TAUP(1, true, 2); break;
-                         case 3: PROM_TAUP(1, true, 3); break; default: PROM_TAUP(1, true, 4); break; }
-        } else {
-          switch (na) { case 2: PROM_TAUP(2, true, 2); break; case 3: PROM_TAUP(3, true, 3); break;
-                        default: PROM_TAUP(4, true, 4); break; }
-        }
-        *variant = (tr.sig_deg > 0 ? 60 : 50) + (na <= 4 ? na : 0);   // 6x: polynomial lookups, k_sigma_poly's Q ranges
-      } else {
-        switch (na) {
-          case 1: if (ph) { PROM_TAUP(1, true, 0); } else { PROM_TAUP(1, false, 0); } break;
-          case 2: if (ph) { PROM_TAUP(2, true, 0); } else { PROM_TAUP(2, false, 0); } break;
-          case 3: if (ph) { PROM_TAUP(3, true, 0); } else { PROM_TAUP(3, false, 0); } break;
-          default: if (ph) { PROM_TAUP(4, true, 0); } else { PROM_TAUP(4, false, 0); } break;
-        }
+                        hcap, rs.hcnt.as<int32_t>(), (int32_t)n_static, msp ? rs.zfl.as<uint8_t>() : nullptr, \
+                        tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tsp, R)
+      switch (na) {
+        case 1: if (ph) { PROM_TAUP(1, true); } else { PROM_TAUP(1, false); } break;
+        case 2: if (ph) { PROM_TAUP(2, true); } else { PROM_TAUP(2, false); } break;
+        case 3: if (ph) { PROM_TAUP(3, true); } else { PROM_TAUP(3, false); } break;
+        default: if (ph) { PROM_TAUP(4, true); } else { PROM_TAUP(4, false); } break;
       }
 #undef PROM_TAUP
     } else if (pre_sigma) { PROM_TAUW_NS(8, true) } else { PROM_TAUW_NS(2, false) }

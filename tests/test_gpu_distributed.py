@@ -22,12 +22,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _bench(tmp, world, config):
-    out = os.path.join(tmp, "w%d" % world)
+def _bench(tmp, world, config, axis="wavelength"):
+    out = os.path.join(tmp, "w%d_%s" % (world, axis))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--steps", "3", "--warmup", "1", "--config", config, "--scaling", "strong",
-           "--no-cpu-baseline", "--no-projection", "--dump-R", out]
+           "--shard-axis", axis, "--no-cpu-baseline", "--no-projection", "--dump-R", out]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
@@ -36,7 +36,7 @@ def _bench(tmp, world, config):
     for r in range(world):
         with open(os.path.join(out, "range_rank%d.json" % r)) as fh:
             rg = json.load(fh)
-        shards.append((rg["w0"], rg["w1"], np.load(os.path.join(out, "R_rank%d.npy" % r))))
+        shards.append((rg["w0"], rg["w1"], np.load(os.path.join(out, "R_rank%d.npy" % r)), rg["o0"], rg["o1"]))
     return json.loads(line), shards
 
 
@@ -49,7 +49,7 @@ def test_two_rank_bench_gathers_bitwise(config, tmp_path):
     assert s1[0] == 0 and s1[1] == n_wav
     R = np.empty_like(s1[2])
     edge = 0
-    for w0, w1, part in sh:
+    for w0, w1, part, _, _ in sh:
         assert w0 == edge and part.shape == (R.shape[0], w1 - w0)
         R[:, w0:w1] = part
         edge = w1
@@ -65,7 +65,7 @@ def test_shard_mode_is_one_ranks_work(tmp_path):
     res1, (s1,) = _bench(str(tmp_path), 1, "C2")
     out = os.path.join(str(tmp_path), "shard")
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1", "--config", "C2",
-           "--shard", "1/2", "--no-cpu-baseline", "--no-projection", "--dump-R", out]
+           "--shard", "1/2", "--shard-axis", "wavelength", "--no-cpu-baseline", "--no-projection", "--dump-R", out]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     res = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
@@ -97,3 +97,19 @@ def test_phase_shard_is_full_runs_rows(config, tmp_path):
     n_orb = s1[2].shape[0]
     assert rg["w0"] == 0 and rg["w1"] == s1[2].shape[1] and 0 < rg["o0"] < rg["o1"] == n_orb
     assert np.array_equal(part, s1[2][rg["o0"]:rg["o1"]], equal_nan=True)
+
+
+def test_two_rank_bench_default_phase_axis(tmp_path):
+    """N > 1 defaults to strong scaling; --shard-axis auto splits the orbital phases when they divide evenly
+    (C4: 8 phases over 2 ranks): the gathered rows are the single-rank run's, bit for bit."""
+    res1, (s1,) = _bench(str(tmp_path), 1, "C4", axis="auto")
+    res2, sh = _bench(str(tmp_path), 2, "C4", axis="auto")
+    assert res2["scaling"] == "strong" and res2["config"]["parallelism"].startswith("phase shards")
+    R = np.full_like(s1[2], np.nan)
+    edge = 0
+    for w0, w1, part, o0, o1 in sorted(sh, key=lambda t: t[3]):
+        assert w0 == 0 and w1 == s1[2].shape[1] and o0 == edge and part.shape == (o1 - o0, w1)
+        R[o0:o1] = part
+        edge = o1
+    assert edge == s1[2].shape[0]
+    assert np.array_equal(R, s1[2], equal_nan=True)

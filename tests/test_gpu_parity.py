@@ -346,8 +346,6 @@ def test_planned_tau_within_window_bound(dev, name, monkeypatch):
     else:
         cfg = json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
-    monkeypatch.setenv("PROM_FUSED", "0")   # both read the same sigma rows (test_fused_sigma: the fused path)
-    monkeypatch.setenv("PROM_SIG_TAU", "0")  # k_tau_p's static units (the fused rows: test_sigma_tau_bitwise)
     monkeypatch.setenv("PROM_TAU_PLAN", "1")
     R_p = tr.sumOverChords(devices=[0])
     st_p = tr.last_stats[-1]
@@ -363,76 +361,6 @@ def test_planned_tau_within_window_bound(dev, name, monkeypatch):
     # on both kernels and are bitwise equal; only heavy halves (line cores) may differ
     diff = R_p != R_w
     assert np.count_nonzero(diff) <= diff.size // 2
-
-
-@pytest.mark.parametrize("name", ["C3r", "C4r", "exomoon", "C3"])
-def test_fused_sigma(dev, name, monkeypatch):
-    """The fused Doppler path (PROM_FUSED=1: the planned tau kernel looks sigma up itself, no sigma rows in
-    HBM) against the sigma-row path.  Polynomial rows (default): k_sigma_poly still gives the half-tile Q
-    ranges and the tau kernel's lookup is k_sigma_poly's arithmetic on the same record, so R is bitwise the
-    row path's.  exp10 rows (PROM_SIG_POLY=0): node-range Q bounds (k_qbounds), both within the windowed
-    integration's bound of the full evaluation, so within 1e-13 of each other.  And the reference's R."""
-    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
-    from prometheus_amd import configs
-    cfg = configs.get(name) if name == "C3" else json.loads(str(load("transit_" + name)["config"]))
-    tr = _product_transit(cfg)
-    monkeypatch.setenv("PROM_SIG_TAU", "0")   # the sigma-row path as the comparison
-    monkeypatch.setenv("PROM_FUSED", "1")
-    R_f = tr.sumOverChords(devices=[0])
-    st_f = tr.last_stats[-1]
-    monkeypatch.setenv("PROM_FUSED", "0")
-    R_r = tr.sumOverChords(devices=[0])
-    st_r = tr.last_stats[-1]
-    print(name, "variants", st_f["tau_kernel_variant"], st_r["tau_kernel_variant"], "exp evals", st_f["exp_evals"],
-          st_r["exp_evals"])
-    assert st_f["tau_kernel_variant"] // 10 in (5, 6) and st_r["tau_kernel_variant"] // 10 == 3
-    if st_f["tau_kernel_variant"] // 10 == 6:   # polynomial rows (a table with |a| too large keeps exp10)
-        assert np.array_equal(R_f, R_r, equal_nan=True)
-        assert st_f["exp_evals"] == st_r["exp_evals"]
-    else:
-        assert np.max(np.abs(R_f - R_r)) <= 1e-13
-    if name != "C3":
-        assert rel(R_f, load("transit_" + name)["R"]) < R_TOL
-    monkeypatch.setenv("PROM_SIG_POLY", "0")
-    monkeypatch.setenv("PROM_FUSED", "1")
-    R_fe = tr.sumOverChords(devices=[0])
-    monkeypatch.setenv("PROM_FUSED", "0")
-    R_re = tr.sumOverChords(devices=[0])
-    assert np.max(np.abs(R_fe - R_re)) <= 1e-13
-
-
-@pytest.mark.parametrize("name,merge", [("C3r", "1"), ("C3r", "0"), ("C4r", "1"), ("exomoon", "1"), ("C3", "1"),
-                                        ("C4", "1"), ("C4x10", "1")])
-def test_sigma_tau_bitwise(dev, name, merge, monkeypatch):
-    """The fused Doppler rows (default, variant 7x: k_sigma_poly integrates every light (row, half tile) window
-    itself after k_order and hands the heavy half tiles to k_tau_p's entry lists; no Y rows in HBM) against
-    the row path (PROM_SIG_TAU=0: Y rows, k_windows, k_tau_p's static units).  Same windows, records, order
-    and arithmetic: R is bitwise equal and the exponentials counted are the same.  Several unmerged species
-    (merge 0) and the exp10 rows keep the row path."""
-    monkeypatch.setenv("PROM_TCURVE", "0")   # the windowed path (k_order); transmission curves: test_gpu_tcurve.py
-    from prometheus_amd import configs
-    cfg = configs.get(name) if name in ("C3", "C4", "C4x10") else json.loads(str(load("transit_" + name)["config"]))
-    tr = _product_transit(cfg)
-    monkeypatch.setenv("PROM_SPECIES_MERGE", merge)
-    monkeypatch.setenv("PROM_FUSED", "0")
-    monkeypatch.setenv("PROM_SIG_TAU", "1")
-    R_f = tr.sumOverChords(devices=[0])
-    st_f = tr.last_stats[-1]
-    monkeypatch.setenv("PROM_SIG_TAU", "0")
-    R_r = tr.sumOverChords(devices=[0])
-    st_r = tr.last_stats[-1]
-    print(name, "merge", merge, "variants", st_f["tau_kernel_variant"], st_r["tau_kernel_variant"], "exp evals",
-          st_f["exp_evals"], st_r["exp_evals"])
-    assert st_r["tau_kernel_variant"] // 10 == 3
-    # (reduced tables whose |a| bound needs too high a degree keep the exp10 rows, and with them the row path)
-    if merge == "0":
-        assert st_f["tau_kernel_variant"] // 10 == 3
-    elif name in ("C3", "C4", "C4x10", "exomoon"):
-        assert st_f["tau_kernel_variant"] // 10 == 7
-    assert np.array_equal(R_f, R_r, equal_nan=True)
-    assert st_f["exp_evals"] == st_r["exp_evals"]
-    if name not in ("C3", "C4", "C4x10"):
-        assert rel(R_f, load("transit_" + name)["R"]) < R_TOL
 
 
 @pytest.mark.parametrize("name", ["C2r", "C2"])
@@ -463,7 +391,7 @@ def test_species_merge(dev, name, monkeypatch):
     assert rel(R_w, R_s) < 1e-13
 
 
-@pytest.mark.parametrize("plan", ["1", "0", "doppler", "doppler_rows", "tcurve", "tcurve_doppler"])
+@pytest.mark.parametrize("plan", ["1", "0", "doppler", "tcurve", "tcurve_doppler"])
 def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     """A user density plugin (host-tabulated n(c, x)) with one infinite sample: that chord's column is
     inf, its phase takes the exact chord-order path (ocml exp, no windows), e^{-inf sigma} = 0 and
@@ -478,7 +406,6 @@ def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     tcurve = plan.startswith("tcurve")
     monkeypatch.setenv("PROM_TCURVE", "1" if tcurve else "0")
     monkeypatch.setenv("PROM_TAU_PLAN", "1" if (plan.startswith("doppler") or tcurve) else plan)
-    monkeypatch.setenv("PROM_SIG_TAU", "0" if plan == "doppler_rows" else "1")
     cfg = configs.reduced(configs.get("C2"), orbphase_steps=3, lower_w=5886e-8, upper_w=5900e-8,
                           res_low=5e-9, res_high=1e-10)
     cfg["Fundamentals"]["DopplerOrbitalMotion"] = plan.startswith("doppler") or plan == "tcurve_doppler"
@@ -559,7 +486,6 @@ def test_sigma_rows_bitwise(dev, name, merge, monkeypatch):
     cfg = configs.get(name) if name in ("C3", "C4") else json.loads(str(load("transit_" + name)["config"]))
     tr = _product_transit(cfg)
     monkeypatch.setenv("PROM_SPECIES_MERGE", merge)
-    monkeypatch.setenv("PROM_FUSED", "0")   # the sigma-row kernel itself (the fused path: test_fused_sigma)
     monkeypatch.setenv("PROM_SIGMA_ROWS", "0")
     R_b = tr.sumOverChords(devices=[0])
     monkeypatch.setenv("PROM_SIGMA_ROWS", "1")

@@ -277,3 +277,29 @@ def test_failed_set_does_not_commit_sigma_segments(dev):
     R_c = tr2.sumOverChords(devices=[0])
     assert rel(R_c, _oracle_R(cfg2, tr2.wavelength)) < R_TOL
     assert rel(R_a, _oracle_R(cfg, tr.wavelength)) < R_TOL
+
+
+def test_molecular_zero_cross_sections(dev):
+    """A molecular table that is zero over half its wavenumbers (log10(0 + offset) = the floor): where every
+    in-table sample's cross-section is zero, the reference's tau is exactly 0 (R: the unblocked share of the disk
+    flux); the table-exp path subtracts the offset per sample (n_abs (10^v - offset)), so tau there is at most
+    ~1e-14 offset n_abs dx and e^-tau is 1.0: R within 1e-14 of the oracle there, and within R_TOL everywhere."""
+    from prometheus_amd import configs
+    from prometheus_amd import gasProperties as gp
+    from prometheus_amd import setupfile
+    tab = O.synthetic_molecular_table(n_nu=2001)
+    tab["xsecarr"][:, :, :1000] = 0.0          # nu < 7500 cm^-1: lambda > 1.333 um
+    gp.register_molecular_table("H2O", tab)
+    try:
+        cfg = configs.fixture_configs()["C5r"]
+        tr = setupfile.build_transit(cfg)
+        R = tr.sumOverChords(devices=[0])
+        scen, dop, grids = O.from_setup(cfg, {"H2O": tab})
+        Ro = O.transit_depth(scen, dop, grids, tr.wavelength, O.build_tables(scen, grids))
+        zero = tr.wavelength > 1.0 / 7490.0   # (the bins from 7497.5 cm^-1 up interpolate to nonzero values)
+        assert zero.any() and (~zero).any()
+        # tau = 0 there: the reference's R is the unblocked share of the disk flux, ours to rounding
+        assert float(np.max(np.abs(R[:, zero] - Ro[:, zero]))) < 1e-14
+        assert rel(R, Ro) < R_TOL
+    finally:
+        gp.register_molecular_table("H2O", O.synthetic_molecular_table(n_nu=2001))
