@@ -429,10 +429,48 @@ def molecular_sigma(rgi, P, T, wav, offset=1e-50):
     return (10 ** rgi(pts) - offset).reshape(nc, nx, nw)
 
 
+# --- C restatement of the molecular optical depth (oracle/mol_tau.c) -------------
+_MOL_C = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmol_tau.so")
+
+
+def build_c(force=False):
+    """gcc -O2 -fopenmp oracle/mol_tau.c -> oracle/libmol_tau.so (test infrastructure; no -ffast-math:
+    the restatement keeps IEEE order)."""
+    import subprocess
+    src = os.path.join(os.path.dirname(_MOL_C), "mol_tau.c")
+    if force or not os.path.exists(_MOL_C) or os.path.getmtime(_MOL_C) < os.path.getmtime(src):
+        subprocess.check_call(["gcc", "-O2", "-fno-fast-math", "-ffp-contract=off", "-fopenmp", "-shared",
+                               "-fPIC", src, "-o", _MOL_C, "-lm"])
+    return _MOL_C
+
+
+def molecular_tau_c(rgi, n_chi, P, T, shifts, wav, dx, tau, offset=1e-50):
+    """tau += dx * einsum("cx,cxw->cw", n_chi, molecular_sigma(rgi, P, T, shifts[:, None] * wav[None, :]))
+    through oracle/mol_tau.c (same interpolation semantics and order; OpenMP over chords)."""
+    import ctypes
+    lib = ctypes.CDLL(build_c())
+    f = lib.oracle_mol_tau
+    dp = ctypes.POINTER(ctypes.c_double)
+    i64, dbl = ctypes.c_int64, ctypes.c_double
+    f.argtypes = [i64, i64, i64, dp, dp, dp, dp, i64, dp, i64, dp, i64, dp, dp, dbl, dbl, dbl, dbl, dp]
+    f.restype = None
+    Pg, Tg, lg = (np.ascontiguousarray(g, dtype=np.float64) for g in rgi.grid)
+    vals = np.ascontiguousarray(rgi.values, dtype=np.float64)
+    n1 = np.ascontiguousarray(n_chi, dtype=np.float64)
+    P1 = np.ascontiguousarray(np.broadcast_to(P, n1.shape), dtype=np.float64)
+    sh = np.ascontiguousarray(shifts, dtype=np.float64)
+    w1 = np.ascontiguousarray(wav, dtype=np.float64)
+    assert tau.flags.c_contiguous and tau.dtype == np.float64 and tau.shape == (n1.shape[0], len(w1))
+    ptr = lambda a: a.ctypes.data_as(dp)  # noqa: E731
+    f(n1.shape[0], n1.shape[1], len(w1), ptr(n1), ptr(P1), ptr(sh), ptr(w1), len(Pg), ptr(Pg), len(Tg), ptr(Tg),
+      len(lg), ptr(lg), ptr(vals), float(T), float(offset), 1.0, float(dx), ptr(tau))
+
+
 # --- optical depth: gasProperties.py:885-956 -----------------------------------
-def optical_depth(scenarios, doppler, x, phi, rho, orb, wav, dx, tables):
+def optical_depth(scenarios, doppler, x, phi, rho, orb, wav, dx, tables, mol_c=False):
     """Atmosphere.getLOSopticalDepth_Batch restated.  ``tables[(si, ci)]`` holds
-    (x, y) refined log-sigma tables for atoms or an RGI for molecules."""
+    (x, y) refined log-sigma tables for atoms or an RGI for molecules (``mol_c``: molecular constituents
+    through oracle/mol_tau.c, the same interpolation restated in C)."""
     nc = len(phi)
     tau = np.zeros((nc, len(wav)))
     for si, sc in enumerate(scenarios):
@@ -445,6 +483,9 @@ def optical_depth(scenarios, doppler, x, phi, rho, orb, wav, dx, tables):
         for ci, con in enumerate(sc.constituents):
             if "molecule" in con:
                 P = n_tot * K_B * sc.T
+                if mol_c:
+                    molecular_tau_c(tables[(si, ci)], n_tot * con["chi"], P, sc.T, shifts, wav, dx, tau)
+                    continue
                 sig = molecular_sigma(tables[(si, ci)], P, sc.T, shifts[:, None] * wav[None, :])
                 tau += np.einsum("cx,cxw->cw", n_tot * con["chi"], sig) * dx
             else:
@@ -463,7 +504,7 @@ def chunk_size(n_chords, n_wav, n_x, max_memory_gb, molecular):
 
 
 def transit_depth(scenarios, doppler, grid, wav, tables, max_memory_gb=2.0,
-                  chord_limit=None):
+                  chord_limit=None, mol_c=False):
     """Transit.sumOverChords restated (gasProperties.py:1160-1258).
 
     ``chord_limit`` (bench CPU-baseline sample only) truncates the chord list
@@ -483,7 +524,7 @@ def transit_depth(scenarios, doppler, grid, wav, tables, max_memory_gb=2.0,
     star_shifts = doppler_shift(planet.vsini * rho / planet.star_R * np.cos(phi - planet.phi_rot))
     molecular = any("molecule" in c for s in scenarios for c in s.constituents)
     x = x_axis(grid)
-    B = chunk_size(len(cg), n_wav, len(x), max_memory_gb, molecular)
+    B = chunk_size(len(cg), n_wav, len(x), max_memory_gb, molecular and not mol_c)
     dx = delta_x(grid)
     Fin = np.zeros((n_orb, n_wav))
     Fout = np.zeros((n_orb, n_wav))
@@ -504,7 +545,7 @@ def transit_depth(scenarios, doppler, grid, wav, tables, max_memory_gb=2.0,
         act = ~blocked
         if np.any(act):
             tau = optical_depth(scenarios, doppler, x, phi[s][act], rho[s][act], orb[s][act],
-                                wav, dx, tables)
+                                wav, dx, tables, mol_c)
             fi[act] = fo[act] * np.exp(-tau)
         if B == len(cg) and chord_limit is None:
             npr = int(grid["phi_steps"]) * int(grid["rho_steps"])

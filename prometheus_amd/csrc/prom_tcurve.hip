@@ -627,12 +627,11 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
 #define PROM_TCK(NS, DG, MGV, RV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV>), dim3(nb), dim3(kBlock), 0, s, ev_sig0, ev_sig1, 0, tabv, \
                         pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, RF, ta)
-#define PROM_TCR(NS, DG, MGV)                          \
-  do {                                                 \
-    if (uni) PROM_TCK(NS, DG, MGV, 8, true);           \
-    else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false);  \
-    else if (R <= 4) PROM_TCK(NS, DG, MGV, 4, false);  \
-    else PROM_TCK(NS, DG, MGV, 8, false);              \
+#define PROM_TCR(NS, DG, MGV)                                       \
+  do {                                                              \
+    if (uni) PROM_TCK(NS, DG, MGV, 8, true);                        \
+    else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false);               \
+    else PROM_TCK(NS, DG, MGV, ((NS) == 1 ? 4 : 8), false);         \
   } while (0)
   // degree 8 covers every table with amax <= 0.07 (the high-resolution configs); 14 the rest (coarse tables)
 #define PROM_TCD(NS, MGV)                                                          \

@@ -8,6 +8,11 @@ heavy units) and the full grid.
 Sizes: C2 190,205 lambda x 8 phases; C3 351,222 x 16 (power law, Na I + Ca II + Mg I,
 Doppler); C4 186,604 x 8 (torus, Doppler); C5 1,000,000 x 32 (hydrostatic + H2O, synthetic ExoMol-layout
 table); 2,400 chords x 30 samples per phase.  Tolerance: 1e-10 relative (north star).
+
+C5 is checked on 1,000+ wavelengths through the C restatement of the molecular optical depth
+(oracle/mol_tau.c, pinned bitwise-close to the numpy oracle by tests/test_oracle_c.py): seeded interior
+wavelengths, both ends of the grid (the table's lambda edges coincide with the grid's, so the Doppler-shifted
+lookups leave the table there) and the grid wavelengths nearest the table's lambda nodes.
 """
 import numpy as np
 import pytest
@@ -39,8 +44,22 @@ CASES = {
     "C3": ((16, 351222), 400, 13),
     "C4": ((8, 186604), 600, 14),
     "C4x10": ((8, None), 300, 16),    # the 8-GPU strong-scaling workload (~1.9e6 wavelengths)
-    "C5": ((32, 1000000), 40, 15),
+    "C5": ((32, 1000000), 400, 15),
 }
+
+
+def _c5_sample(wav, table, seed):
+    """C5: 400 seeded wavelengths (_sample), 200 over each 1,000-point end of the grid (Doppler-shifted
+    lookups cross the table's lambda edges there) and 150 table lambda nodes with both grid neighbours."""
+    n = len(wav)
+    rng = np.random.default_rng(seed)
+    base = _sample(n, 400, seed)
+    ends = np.concatenate([np.linspace(0, 999, 200), np.linspace(n - 1000, n - 1, 200)]).astype(np.int64)
+    nodes = np.sort(1.0 / np.asarray(table["bin_edges"]))
+    nodes = nodes[(nodes > wav[0]) & (nodes < wav[-1])]
+    k = np.searchsorted(wav, rng.choice(nodes, 150, replace=False))
+    near = np.concatenate([k - 1, k])
+    return np.unique(np.concatenate([base, ends, near]))
 
 
 @pytest.mark.parametrize("name", ["C3", "C4", "C4x10", "C5"])
@@ -58,9 +77,13 @@ def test_full_size_config_sampled(name):
     if shape[1] is None:
         shape = (shape[0], len(tr.wavelength))
     assert R.shape == shape
-    idx = _sample(shape[1], k, seed)
+    if name == "C5":
+        idx = _c5_sample(tr.wavelength, mol["H2O"], seed)
+        assert len(idx) >= 1000
+    else:
+        idx = _sample(shape[1], k, seed)
     scen, dop, grids = O.from_setup(cfg, mol)
-    Ro = O.transit_depth(scen, dop, grids, tr.wavelength[idx], O.build_tables(scen, grids))
+    Ro = O.transit_depth(scen, dop, grids, tr.wavelength[idx], O.build_tables(scen, grids), mol_c=name == "C5")
     err = rel(R[:, idx], Ro)
     print("%s full size %s: sampled %d wavelengths, max rel err %.3e, stats %s" % (name, shape, len(idx), err, st))
     assert err < R_TOL
