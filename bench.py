@@ -10,12 +10,13 @@ with all inputs resident in HBM: density + column densities + culling, sigma res
 species at every phase's Doppler shift, chord ordering, and the fused tau -> exp(-tau) ->
 disk-sum -> ratio kernel (prom_transit_run).  --config C2 gives the configs[1] line.
 
-N>1 (launched by torch.distributed.run, one process per GPU), wavelength sharding, no collective on
-the data path (torch.distributed carries only the timing barrier and the max-over-ranks time):
-  --scaling weak (default): the global spectrum is the config's grid at N-times finer resolution
+N>1 (launched by torch.distributed.run, one process per GPU), sharding with no collective on the data
+path (torch.distributed carries only the timing barrier and the max-over-ranks time):
+  --scaling strong (default): the global spectrum is the config's grid as it stands (default config
+      C4x10, the 8-GPU workload BASELINE.json names; also C5), split into N shards along --shard-axis
+      (auto: orbital phases when they divide evenly, else contiguous wavelength ranges).
+  --scaling weak: the global spectrum is the config's grid at N-times finer resolution
       (resolutionLow/N, resolutionHigh/N: ~N x the wavelengths); rank r integrates shard r.
-  --scaling strong: the global spectrum is the config's grid as it stands (e.g. --config C4x10,
-      C5), split into N contiguous shards.
   --shard r/N (one process): only shard r of N of the config's grid, timed alone on one GPU -- one rank's
       work under an N-way strong split.
   --shard-axis phase: strong splits over orbital phases instead (every wavelength, phases [o0, o1)): the
@@ -464,11 +465,15 @@ def main():
         # measured table-exp rate (profiles/r02u_fp64_exp_peak.json: 2.8e12/s)
         # (the device counts them in stats runs: exp_evals = the 10^v of in-table samples + one e^-tau per
         # record and wavelength; out-of-table samples are skipped, k_mol_prep compacts them away)
+        # achieved / peak / frac in one unit (10^v per second); the byte figures move under "hbm"
         pow10 = max(0, int(st["exp_evals"]) - int(st["tau_records"]) * n_w)
-        kernels[tau_kernel].update(bound="fp64-exp", pow10_evals=pow10,
-                                   pow10_per_s=pow10 / (tau_ms_iso * 1e-3) if tau_ms_iso else None,
-                                   pow10_peak_per_s=2.815e12,
-                                   frac=(pow10 / (tau_ms_iso * 1e-3) / 2.815e12) if tau_ms_iso else None)
+        km = kernels[tau_kernel]
+        km.pop("valu_tflops", None)   # (flops_unit counts all n_x samples; only the in-table ones are evaluated)
+        km["hbm"] = {k: km.pop(k) for k in ("achieved", "peak", "unit", "frac", "frac_of_measured_read_peak",
+                                             "algorithmic_bytes") if k in km}
+        rate = pow10 / (tau_ms_iso * 1e-3) if tau_ms_iso else None
+        km.update(bound="fp64-exp", pow10_evals=pow10, achieved=rate, peak=2.815e12, unit="pow10/s",
+                  frac=(rate / 2.815e12) if rate else None, peak_source="profiles/r02u_fp64_exp_peak.json")
     if kms.get("sigma"):
         # Doppler sigma rows: one row per phase and wavelength (Y for merged species, else sigma per species)
         # and their zero flags written, the wavelengths and the refined tables' nodes (x, log10 sigma) read

@@ -165,6 +165,7 @@ struct MolSlotDev {
   const double* shift;   // [n_orb] Doppler factors of its scenario
   int32_t scenario;
   int32_t pad;
+  const double2* G;      // [n_p][n_w - 1] {g(i, w), g(i, w + 1)}: V lerped to the slot's T (k_mol_gt, per set)
 };
 
 // Terms and scenarios of small problems passed by value to the column kernel.
@@ -324,6 +325,7 @@ struct TransitDev {
   DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
   DevBuf mol_lst;                           // [n_orb][n_pr n_mol n_x] double4: each phase's records' in-table
                                             //     samples, one flat list (k_mol_list)
+  DevBuf mol_g;                             // every slot's MolSlotDev::G
   DevBuf mol_rend;                          // [n_orb][n_pr] int32: end of each record's samples in the list
   std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
@@ -428,6 +430,7 @@ void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const d
 void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,
                    hipEvent_t ev_sig1, hipEvent_t ev_tb0, hipEvent_t ev_tb1);
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
+void launch_mol_gt(hipStream_t s, const MolSlotDev& md);
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
 // prom_gridded_density (prom_fn.hip)

@@ -5,32 +5,55 @@ namespace prom {
 
 // ---- molecular fused kernel -------------------------------------------------------------------
 // tau(c, w) = sum_atomic N_s sigma_s(w) + sum_mol dx * sum_x n_abs(c,x) sigma_m(P(c,x), T, lambda'_w)
-// (gasProperties.py:924-954).  Per thread (phase o, wavelength w) and molecular slot, the (T, lambda)
-// part of the trilinear RegularGridInterpolator weights is fixed: u_i = sum_{T,lambda corners} w V[i][.][.]
-// is formed once for every P node i into LDS; each (chord, sample) then costs one P interpolation
-// (uniform bracket from k_mol_prep), 10^v and an FMA.  Out-of-table samples (P, T or lambda) take the
-// fill value, i.e. sigma = 0, as in the reference.
-constexpr double kLog2Ten256 = 0x1.a934f0979a371p+9;    // 256 log2(10)
-constexpr int kMolExpN = 256;                              // LDS exp table 2^(i/256) (2 KB: occupancy)
+// (gasProperties.py:924-954).  The slot's temperature is a constant, so the T part of the trilinear
+// RegularGridInterpolator weights is folded into G once per set (k_mol_gt: g(i, w) = (1 - t_T) V[i][iT][w] +
+// t_T V[i][iT + 1][w], stored as {g(i, w), g(i, w + 1)} pairs).  Per thread (phase o, wavelength w) and slot the
+// lambda' bracket is walked from the previous phase's; each in-table sample (P node i, weight t_P from k_mol_prep)
+// then reads two 16-byte pairs, u_i = (1 - t_w) g(i, iw) + t_w g(i, iw + 1), u_{i+1} likewise, v = u_i + t_P
+// (u_{i+1} - u_i), and costs 10^v and an FMA.  Out-of-table samples (P, T or lambda) take the fill value, i.e.
+// sigma = 0, as in the reference (k_mol_prep compacts them away; T and lambda' are checked here).
+constexpr double kLog2Ten1024 = 0x1.a934f0979a371p+11;   // 1024 log2(10)
+constexpr int kMolExpN = 1024;                             // LDS exp table 2^(i/1024) (8 KB)
 
-// 2^(y/256) = 2^(k >> 8) T[k & 255] exp(d ln2/256), k = rint(y), d in [-1/2, 1/2], degree-5 Taylor
-// polynomial (truncation 9e-21 relative; acc_exp256's arithmetic without the accumulation)
-__device__ __forceinline__ double exp2_256(double y, const double* __restrict__ tab) {
+// 2^(y/1024) = 2^(k >> 10) T[k & 1023] exp(d ln2/1024), k = rint(y), d in [-1/2, 1/2], cubic Taylor polynomial
+// (truncation 5.5e-16 relative; acc_exp1024's arithmetic without the accumulation)
+__device__ __forceinline__ double exp2_1024(double y, const double* __restrict__ tab) {
   const double k = __builtin_rint(y);
   const int ki = (int)k;
   const double d = y - k;
-  double p = __builtin_fma(d, kE256C5, kE256C4);
-  p = __builtin_fma(d, p, kE256C3);
-  p = __builtin_fma(d, p, kE256C2);
-  p = __builtin_fma(d, p, kE256C1);
+  double p = __builtin_fma(d, kE1024C3, kE1024C2);
+  p = __builtin_fma(d, p, kE1024C1);
   p = __builtin_fma(d, p, 1.0);
-  return __builtin_amdgcn_ldexp(tab[ki & (kMolExpN - 1)], ki >> 8) * p;
+  return __builtin_amdgcn_ldexp(tab[ki & (kMolExpN - 1)], ki >> 10) * p;
 }
 
-template <int NSA, int EXPK>
-__global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const SigTabDev* __restrict__ tabs,
-                                                    const MolSlotDev* __restrict__ ms, int32_t n_mol,
-                                                    int32_t max_np, int64_t lst_stride,
+// G of one slot: [n_p][n_w - 1] pairs {g(i, w), g(i, w + 1)} at the slot's T (unused when T is outside the table)
+__global__ void k_mol_gt(const double* __restrict__ Tg, int32_t n_t, double T, const double* __restrict__ V,
+                         int32_t n_p, int64_t n_w, double2* __restrict__ G) {
+  int64_t it = 0;
+  double tt = 0.0;
+  if (!rgi_bracket(Tg, n_t, T, &it, &tt)) return;
+  const int64_t nw1 = n_w - 1;
+  const int64_t tot = (int64_t)n_p * nw1;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < tot; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = k / nw1, w = k - i * nw1;
+    const double* v0 = V + (i * n_t + it) * n_w + w;
+    const double* v1 = v0 + n_w;
+    G[k] = make_double2((1.0 - tt) * v0[0] + tt * v1[0], (1.0 - tt) * v0[1] + tt * v1[1]);
+  }
+}
+
+void launch_mol_gt(hipStream_t s, const MolSlotDev& md) {
+  const int64_t tot = (int64_t)md.n_p * (md.n_w - 1);
+  const unsigned nb = (unsigned)std::min<int64_t>((tot + kBlock - 1) / kBlock, 8192);
+  hipLaunchKernelGGL(k_mol_gt, dim3(nb), dim3(kBlock), 0, s, md.T, md.n_t, md.temp, md.V, md.n_p, md.n_w,
+                     const_cast<double2*>(md.G));
+  PROM_HIP(hipGetLastError());
+}
+
+template <int NSA, int EXPK, bool M1>
+__global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const MolSlotDev* __restrict__ ms,
+                                                    int32_t n_mol, int64_t lst_stride,
                                                     const double* __restrict__ wav,
                                                     const double* __restrict__ recs,
                                                     const int32_t* __restrict__ act_ip,
@@ -39,13 +62,10 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
                                                     const double* __restrict__ tfrac,
                                                     const double* __restrict__ fsum, int32_t n_pr,
                                                     int32_t n_orb, int32_t phases_per_group, int64_t n_wav,
-                                                    int32_t n_x, double delta_x,
-                                                    const double4* __restrict__ lst,
+                                                    double delta_x, const double4* __restrict__ lst,
                                                     const int32_t* __restrict__ rend, double* __restrict__ R,
                                                     unsigned long long* __restrict__ evals) {
-  extern __shared__ double lds[];   // [256] exp table 2^(i/256) | [n_mol][max_np][kBlock] u
-  double* etab = lds;
-  double* ul = lds + kMolExpN;
+  __shared__ double etab[kMolExpN];   // exp table 2^(i/1024)
   if (EXPK)
     for (int i = threadIdx.x; i < kMolExpN; i += kBlock) etab[i] = kExp2TableDev[i * (PROM_EXP2_TABLE_N / kMolExpN)];
   __syncthreads();
@@ -59,13 +79,26 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
   double sg[NR], shv[NR];
 #pragma unroll
   for (int s = 0; s < NR; ++s) { shv[s] = __builtin_nan(""); sg[s] = 0.0; }
-  int64_t whint[4] = {-1, -1, -1, -1};
   unsigned long long npow = 0;   // stats runs: this lane's 10^v evaluations (in-table samples)
 
-  uint32_t inb = 0;              // bit m: molecular slot m has (T, lambda') inside its table
-  double lwprev[4];              // slot m's lambda' of the last u built in LDS (m < 4)
+  // per slot (at most 4): T inside its table (uniform), the lambda' bracket (iw, t_w) of the current phase, the
+  // in-table bit, and the walk's start
+  uint32_t tin = 0;
+  __amdgpu_buffer_rsrc_t rsv[M1 ? 1 : 4];   // each slot's G as one buffer (< 2^31 bytes: the launcher checks)
+  uint32_t rowbv[M1 ? 1 : 4];               // bytes per G row
 #pragma unroll
-  for (int m = 0; m < 4; ++m) lwprev[m] = __builtin_nan("");
+  for (int m = 0; m < (M1 ? 1 : 4); ++m) {
+    const bool valid = m < n_mol;   // (unused slots: empty buffers, never selected)
+    int64_t it;
+    double tt;
+    if (valid && rgi_bracket(ms[m].T, ms[m].n_t, ms[m].temp, &it, &tt)) tin |= 1u << m;
+    rowbv[m] = valid ? (uint32_t)(ms[m].n_w - 1) * (uint32_t)sizeof(double2) : 0u;
+    rsv[m] = __builtin_amdgcn_make_buffer_rsrc(valid ? const_cast<double2*>(ms[m].G) : nullptr, (short)0,
+                                               valid ? (int)((uint32_t)ms[m].n_p * rowbv[m]) : 0, 0x00020000);
+  }
+  int64_t iwv[4] = {-1, -1, -1, -1};
+  double twv[4] = {0.0, 0.0, 0.0, 0.0};
+  uint32_t inb = 0;
   for (int32_t o = o0; o < o1; ++o) {
     const bool exact = !EXPK || counts[o * kCnt + 3] != 0;
     const int32_t n_act = counts[o * kCnt + 0];
@@ -78,112 +111,127 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const S
         shv[s] = sh;
       }
     }
-    for (int32_t m = 0; m < n_mol; ++m) {
-      const MolSlotDev d = ms[m];
-      int64_t it, iw;
-      double tt, tw;
-      const double lw = d.shift[o] * lam;
-      // the same lambda' as this lane's previous phase (no orbital Doppler shift, or an equal factor): u and
-      // the in-table bit are unchanged (T is the slot's own constant)
-      if (m < 4) {
-        if (lw == lwprev[m]) continue;
-        lwprev[m] = lw;
-      }
-      inb &= ~(1u << m);
-      bool ok = rgi_bracket(d.T, d.n_t, d.temp, &it, &tt);
-      if (ok) {
-        // gallop the wavelength bracket from the previous phase's
-        ok = lw >= d.W[0] && lw <= d.W[d.n_w - 1];
-        if (ok) {
-          int64_t h = m < 4 ? whint[m] : -1;
-          int64_t lo = 0, hi = d.n_w - 1;
-          if (h >= 0 && h <= d.n_w - 2 && d.W[h] < lw && lw <= d.W[h + 1]) { lo = h; hi = h + 1; }
-          // scipy: i = searchsorted(g, v, 'left') - 1 clipped to [0, n-2]
-          while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (d.W[mid] < lw) lo = mid; else hi = mid;
-          }
-          iw = lo;
-          if (lw <= d.W[0]) iw = 0;
-          tw = (lw - d.W[iw]) / (d.W[iw + 1] - d.W[iw]);
-          if (m < 4) whint[m] = iw;
+#pragma unroll
+    for (int m = 0; m < (M1 ? 1 : 4); ++m) {
+      if (m >= n_mol) break;
+      const double* __restrict__ W = ms[m].W;
+      const int64_t nw = ms[m].n_w;
+      const double lw = ms[m].shift[o] * lam;
+      // scipy: i = searchsorted(W, lw, 'left') - 1 clipped to [0, n-2], fill outside [W[0], W[n-1]]
+      const bool ok = ((tin >> m) & 1u) && lw >= W[0] && lw <= W[nw - 1];
+      inb = ok ? (inb | (1u << m)) : (inb & ~(1u << m));
+      if (!ok) continue;
+      int64_t h = iwv[m];
+      if (h < 0) {
+        int64_t lo = 0, hi = nw - 1;
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (W[mid] < lw) lo = mid; else hi = mid;
         }
+        h = lo;
+      } else {
+        // walk from the previous phase's bracket (adjacent phases' Doppler factors differ by ~1e-6)
+        while (h < nw - 2 && W[h + 1] < lw) ++h;
+        while (h > 0 && !(W[h] < lw)) --h;
       }
-      if (ok) {
-        inb |= 1u << m;
-        const double w00 = (1.0 - tt) * (1.0 - tw), w01 = (1.0 - tt) * tw;
-        const double w10 = tt * (1.0 - tw), w11 = tt * tw;
-        for (int32_t i = 0; i < d.n_p; ++i) {
-          const double* v0 = d.V + ((int64_t)i * d.n_t + it) * d.n_w + iw;
-          const double* v1 = v0 + d.n_w;
-          double u = 0.0;
-          u = u + v0[0] * w00;
-          u = u + v0[1] * w01;
-          u = u + v1[0] * w10;
-          u = u + v1[1] * w11;
-          ul[((int64_t)m * max_np + i) * kBlock + threadIdx.x] = u;
-        }
-      }
+      iwv[m] = h;
+      twv[m] = (lw - W[h]) / (W[h + 1] - W[h]);
     }
     const int32_t* ipl = act_ip + (int64_t)o * n_pr;
     double acc = 0.0;
-    const double scale = exact ? 1.0 : kM256Ln2;
     // The phase's in-table samples are one flat list in record order (k_mol_list: {P weight, n_abs, slot << 16 |
     // P bracket, offset}, record r's samples ending at rend[r]), read with wave-uniform scalar loads four at a
-    // time: the four samples' u reads, 10^v and products are independent; then they are added into the current
+    // time: the four samples' G reads, 10^v and products are independent; then they are added into the current
     // record's sum, finishing records (e^-tau) at their ends.  Per sample n_abs (10^v - offset), the reference's
     // order of the subtraction (gasProperties.py:811-818, 10**interp - offset).
     const double4* __restrict__ lo = lst + (int64_t)o * lst_stride;
     const int32_t* __restrict__ ro = rend + (int64_t)o * n_pr;
     const int32_t K = n_act > 0 ? ro[n_act - 1] : 0;
-    int32_t r = 0;
-    int32_t end_r = n_act > 0 ? ro[0] : 0;
-    double sm = 0.0;
-    auto finish = [&](int32_t ri) {
-      const double* rr = rec + (int64_t)ri * ST;
-      double tau = 0.0;
+    // per slot: the lane's byte offset of its lambda' pair in a G row and the in-table mask (1 / 0: a product, no
+    // select; out-of-table lanes read the row's first pair, finite)
+    uint32_t boff[M1 ? 1 : 4];
+    double msk[M1 ? 1 : 4];
 #pragma unroll
-      for (int s = 0; s < NSA; ++s) tau = tau + rr[1 + s] * sg[s];
-      tau = tau + sm * delta_x;
-      sm = 0.0;
-      if (!exact) acc = acc_exp256(acc, rr[0], tau * scale, etab);
-      else acc = acc + fout[ipl[ri]] * exp(-tau);
-    };
-    for (int32_t k0 = 0; k0 < K; k0 += 4) {
-      double c[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int32_t k = k0 + j < K ? k0 + j : K - 1;
-        const double4 q = lo[k];
-        const int32_t code = (int32_t)q.z;
-        const int32_t m = code >> 16, pi = code & 0xffff;
-        const double* um = ul + ((int64_t)m * max_np + pi) * kBlock + threadIdx.x;
-        const double a = um[0], b = um[kBlock];
-        double e;
-        if (EXPK && !exact) {
-          // 10^v = 2^(y/256), y = v 256 log2(10), from the LDS table (relative error ~ |y| 2^-53 ln2/256 from the
-          // argument, ~1e-14 at the table's floor)
-          e = exp2_256(__builtin_fma(q.x, b - a, a) * kLog2Ten256, etab);
-        } else {
-          e = exp10((1.0 - q.x) * a + q.x * b);
-        }
-        const bool in = ((inb >> m) & 1u) != 0;
-        c[j] = in ? q.y * (e - q.w) : 0.0;
-        npow += (in && k0 + j < K) ? 1u : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int32_t k = k0 + j;
-        if (k >= K) break;
-        while (k >= end_r) {
-          finish(r);
-          ++r;
-          end_r = ro[r];
-        }
-        sm += c[j];
-      }
+    for (int m = 0; m < (M1 ? 1 : 4); ++m) {
+      const bool in = ((inb >> m) & 1u) != 0;
+      boff[m] = in ? (uint32_t)iwv[m] * (uint32_t)sizeof(double2) : 0u;
+      msk[m] = in ? 1.0 : 0.0;
     }
-    for (; r < n_act; ++r) finish(r);
+    int32_t nsl[4] = {0, 0, 0, 0};   // samples per slot (uniform; stats)
+    // one instance per exp mode (uniform per phase), so the four samples' loads issue together
+    auto samples = [&](auto ex) {
+      constexpr bool EX = decltype(ex)::value;
+      int32_t r = 0;
+      int32_t end_r = n_act > 0 ? ro[0] : 0;
+      double sm = 0.0;
+      auto finish = [&](int32_t ri) {
+        const double* rr = rec + (int64_t)ri * ST;
+        double tau = 0.0;
+#pragma unroll
+        for (int s = 0; s < NSA; ++s) tau = tau + rr[1 + s] * sg[s];
+        tau = tau + sm * delta_x;
+        sm = 0.0;
+        if constexpr (!EX) acc = acc_exp1024(acc, rr[0], tau * kM1024Ln2, etab);
+        else acc = acc + fout[ipl[ri]] * exp(-tau);
+      };
+      constexpr int NB = EX ? 1 : 4;   // (the ocml exp10 path: one sample at a time, few registers)
+      for (int32_t k0 = 0; k0 < K; k0 += NB) {
+        double c[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int32_t k = k0 + j < K ? k0 + j : K - 1;
+          const double4 q = lo[k];
+          const int32_t code = (int32_t)__double_as_longlong(q.z);   // (integer bits: scalar decode)
+          const int32_t m = M1 ? 0 : code >> 16, pi = code & 0xffff;
+          // the slot's bracket (m uniform: selects, no indexing of the register arrays)
+          uint32_t bo = boff[0];
+          double tw = twv[0], mk = msk[0];
+          __amdgpu_buffer_rsrc_t rs = rsv[0];
+          uint32_t rowb = rowbv[0];
+          if constexpr (!M1) {
+#pragma unroll
+            for (int mm = 1; mm < 4; ++mm)
+              if (m == mm) { bo = boff[mm]; tw = twv[mm]; mk = msk[mm]; rs = rsv[mm]; rowb = rowbv[mm]; }
+            if (k0 + j < K) nsl[m & 3] += 1;
+          }
+          // rows pi and pi + 1: buffer loads, the row at a uniform offset (soffset), the lane's pair at its own
+          const uint32_t so = (uint32_t)pi * rowb;
+          const double2 ga = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, bo, so, 0));
+          const double2 gb = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, bo, so + rowb, 0));
+          const double a = __builtin_fma(tw, ga.y - ga.x, ga.x);
+          const double b = __builtin_fma(tw, gb.y - gb.x, gb.x);
+          const double v = __builtin_fma(q.x, b - a, a);
+          double e;
+          if constexpr (!EX) {
+            // 10^v = 2^(y/1024), y = v 1024 log2(10), from the LDS table (relative error ~ |v| ln10 2^-53 from the
+            // argument, ~6e-15 at the table's floor)
+            e = exp2_1024(v * kLog2Ten1024, etab);
+          } else {
+            e = exp10(v);
+          }
+          c[j] = (q.y * (e - q.w)) * mk;
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int32_t k = k0 + j;
+          if (k >= K) break;
+          while (k >= end_r) {
+            finish(r);
+            ++r;
+            end_r = ro[r];
+          }
+          sm += c[j];
+        }
+      }
+      for (; r < n_act; ++r) finish(r);
+    };
+    if (!EXPK || exact) samples(std::true_type{});
+    else samples(std::false_type{});
+    if (evals) {
+      if constexpr (M1) nsl[0] = K;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) npow += ((inb >> m) & 1u) ? (unsigned long long)nsl[m] : 0ull;
+    }
     if (live) R[(int64_t)o * n_wav + w] = exact ? (acc + tfrac[o] * fsum[o]) / fsum[o] : acc + tfrac[o];
   }
   if (evals && live && npow) atomicAdd(&evals[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 63], npow);
@@ -228,7 +276,7 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
         const double off = ms[m].offset;
         for (int32_t k = 0; k < nin; ++k) {
           const double4 q = msmp[cidx * n_x + k];
-          lo[pos++] = make_double4(q.x, q.y, (double)((m << 16) | (int32_t)q.z), off);
+          lo[pos++] = make_double4(q.x, q.y, __longlong_as_double((long long)((m << 16) | (int32_t)q.z)), off);
         }
       }
       rend[(int64_t)o * n_pr + r] = pos;
@@ -237,8 +285,18 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
   }
 }
 
-void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg) {
-  const SigTabDev* tabs = tr.sigtab.as<SigTabDev>();
+void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3, int32_t) {
+  // phase groups: at least ~16 waves per SIMD over the whole grid (65,536 over 1,024 SIMDs), so the last round of
+  // the equally long waves is a small tail (one group of all 32 C5 phases left a 4th round ~5 % full: 1.58x on
+  // the step against 4-phase pieces, BENCH_r03 phase_shard); each group's first phase binary-searches the lambda'
+  // bracket, the others walk it.  PROM_MOL_PPG (profiling): phases per group.
+  const int64_t n_tiles = (tr.n_wav + kBlock - 1) / kBlock;
+  int32_t groups = (int32_t)std::max<int64_t>(1, std::min<int64_t>(tr.n_orb, (65536 + 4 * n_tiles - 1) / (4 * n_tiles)));
+  int32_t ppg = (tr.n_orb + groups - 1) / groups;
+  if (const char* e = std::getenv("PROM_MOL_PPG"))
+    if (std::atoi(e) > 0) ppg = std::min(tr.n_orb, std::atoi(e));
+  groups = (tr.n_orb + ppg - 1) / ppg;
+  const dim3 g((unsigned)n_tiles, (unsigned)groups);
   const double* wav = tr.wav.as<double>();
   const double* recs = rs.recs.as<double>();
   const int32_t* aip = rs.act_ip.as<int32_t>();
@@ -248,11 +306,10 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
   const double* fs = rs.fsum.as<double>();
   double* R = rs.R.as<double>();
     PROM_REQUIRE(na <= 4, "transit: at most 4 atomic constituents next to molecular ones");
-    int32_t max_np = 0;
-    for (const auto& m : tr.mslots) max_np = std::max(max_np, m.n_p);
-    const size_t lds = kMolExpN * sizeof(double) + (size_t)tr.n_mol * max_np * kBlock * sizeof(double);
-    PROM_REQUIRE(lds <= 160 * 1024, "transit: molecular tables too large for the LDS staging (n_mol * n_p)");
     PROM_REQUIRE(tr.n_mol <= 4, "transit: at most 4 molecular constituents");
+    for (const auto& md : tr.mslots)
+      PROM_REQUIRE(md.n_p < (1 << 15) && (double)md.n_p * (double)(md.n_w - 1) * 16.0 < 2147483648.0,
+                   "transit: molecular table too large (n_p < 2^15, n_p (n_w - 1) 16 bytes < 2^31)");
     // prom_transit_kernel_ms: the kernel's own dispatch-packet events
     hipEvent_t kps = nullptr, kpe = nullptr;
     if (tr.kprof) {
@@ -266,8 +323,10 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
                        lst_stride, tr.mol_lst.as<double4>(), tr.mol_rend.as<int32_t>());
     PROM_HIP(hipGetLastError());
 #define PROM_TAUM(NSV, EK)                                                                                  \
-  hipExtLaunchKernelGGL((k_tau_mol<NSV, EK>), g, dim3(kBlock), lds, s, kps, kpe, 0, tr.sigtab_v, tabs, tr.molslot.as<MolSlotDev>(), tr.n_mol, \
-                     max_np, lst_stride, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav, tr.n_x, \
+  if (tr.n_mol == 1) PROM_TAUM1(NSV, EK, true); else PROM_TAUM1(NSV, EK, false)
+#define PROM_TAUM1(NSV, EK, M1V)                                                                            \
+  hipExtLaunchKernelGGL((k_tau_mol<NSV, EK, M1V>), g, dim3(kBlock), 0, s, kps, kpe, 0, tr.sigtab_v, tr.molslot.as<MolSlotDev>(), \
+                     tr.n_mol, lst_stride, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav,     \
                      tr.delta_x, tr.mol_lst.as<double4>(), tr.mol_rend.as<int32_t>(), R,                     \
                      tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr)
 #define PROM_TAUM_NS(EK)                \
@@ -281,6 +340,7 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
     if (tr.exp_mode) { PROM_TAUM_NS(1) } else { PROM_TAUM_NS(0) }
 #undef PROM_TAUM_NS
 #undef PROM_TAUM
+#undef PROM_TAUM1
 }
 
 }  // namespace prom
