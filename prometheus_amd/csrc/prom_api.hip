@@ -1096,9 +1096,23 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       rs.fsum.ensure(sizeof(double) * n_orb);
       rs.R.ensure(sizeof(double) * n_orb * tr.n_wav);
       if (tr.tcurve) {
-        // k_tc_build: ~512 chords per part, at most 1024 (a part's LDS stage) unless that needs more than 8 parts
-        tr.tc_parts = (int32_t)std::max<int64_t>(1, std::min<int64_t>(prom::kTcPartMax,
-                                                                      std::max<int64_t>(tr.n_pr / 512, (tr.n_pr + 1023) / 1024)));
+        // k_tc_build: ~300 chords per part (C3: 8 parts; profiles/r04h_tc_build_parts.txt), at most kTcPartMax
+        // parts; one part needs no hand-off between workgroups; PROM_TC_PARTS (profiling) overrides
+        tr.tc_parts = (int32_t)std::max<int64_t>(1, std::min<int64_t>(prom::kTcPartMax, (tr.n_pr + 299) / 300));
+        if (const char* e = std::getenv("PROM_TC_PARTS"))
+          if (std::atoi(e) > 0) tr.tc_parts = std::min(prom::kTcPartMax, std::atoi(e));
+        if (!tr.tc_const.p) {
+          // c_k = sum_j f_j cm[k][j] at the nodes u_j = cos(pi (j + 1/2) / 16); node factors 2^((u_k + 1) / 2)
+          std::vector<double> cc(prom::kTcD * prom::kTcD + prom::kTcD);
+          for (int k = 0; k < prom::kTcD; ++k)
+            for (int j = 0; j < prom::kTcD; ++j)
+              cc[k * prom::kTcD + j] = std::cos(M_PI * (double)k * ((double)j + 0.5) / (double)prom::kTcD) *
+                                       ((k == 0 ? 1.0 : 2.0) / (double)prom::kTcD);
+          for (int k = 0; k < prom::kTcD; ++k)
+            cc[prom::kTcD * prom::kTcD + k] = std::exp2(0.5 * (std::cos(M_PI * ((double)k + 0.5) / (double)prom::kTcD) + 1.0));
+          tr.tc_const.ensure(sizeof(double) * cc.size());
+          PROM_HIP(hipMemcpy(tr.tc_const.p, cc.data(), sizeof(double) * cc.size(), hipMemcpyHostToDevice));
+        }
         const int64_t n_ch = (tr.tc_lg + prom::kTcChain - 1) / prom::kTcChain;
         rs.tc_hdr.ensure(sizeof(double) * n_orb * prom::kTcHdr);
         rs.tc_tab.ensure(sizeof(double) * n_orb * tr.tc_lg * prom::kTcD);
@@ -1112,6 +1126,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     }
     tr.last = 0;
     stg.flush(ctx, s);
+    if (tr.star) prom::launch_rm_fout(s, tr);   // per set: the unocculted flux of every wavelength
     if (seg_key_new) {
       // segments built by this call: mark those whose guess is numpy's bracket for every target
       const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;

@@ -187,7 +187,7 @@ enum : int { kTcHNmax = 0, kTcHTfrac = 1, kTcHFsum = 2, kTcHT0 = 3 /* .. 8: tail
              kTcHL = 9, kTcHFlags = 10 /* 1: opaque above the table, 2: non-finite columns */, kTcHNact = 11 };
 constexpr int kTcMaxOctaves = 64;
 constexpr int kTcChain = 4;                          // octaves per table exp (k_tc_build)
-constexpr int kTcPartMax = 8;                        // chord parts per (phase, chain)
+constexpr int kTcPartMax = 16;                       // chord parts per (phase, chain)
 constexpr int kTcPartVals = (kTcChain + 1) * kTcD;   // doubles per part: node sums per octave, then the moments
 
 struct TcArgs {
@@ -325,6 +325,7 @@ struct TransitDev {
   DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
   DevBuf mol_lst;                           // [n_orb][n_pr n_mol n_x] double4: each phase's records' in-table
                                             //     samples, one flat list (k_mol_list)
+  DevBuf rm_fout;                           // stellar spectrum: [n_wav] unocculted flux sum_c F(c, w) (k_rm_fout, per set)
   DevBuf mol_g;                             // every slot's MolSlotDev::G
   DevBuf mol_rend;                          // [n_orb][n_pr] int32: end of each record's samples in the list
   std::vector<MolSlotDev> mslots;           // host copy
@@ -355,6 +356,7 @@ struct TransitDev {
   // tables and the bound of Y (the effective absorber's sigma maximum) that sets each phase's table extent
   bool tcurve = true;
   int32_t tc_lg = 1;
+  DevBuf tc_const;                          // k_tc_build constants: Chebyshev matrix [kTcD][kTcD], node factors [kTcD]
   int32_t tc_parts = 1;                     // chord parts per (phase, chain) of k_tc_build
   double tc_ybound = 0.0;
   RunSlot slot[kMaxSlots];
@@ -431,6 +433,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
                    hipEvent_t ev_sig1, hipEvent_t ev_tb0, hipEvent_t ev_tb1);
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
 void launch_mol_gt(hipStream_t s, const MolSlotDev& md);
+void launch_rm_fout(hipStream_t s, TransitDev& tr);
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev);
 double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev);
 // prom_gridded_density (prom_fn.hip)

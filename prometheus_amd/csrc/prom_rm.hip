@@ -7,9 +7,9 @@ namespace prom {
 // F(c, w) = rho_c * (F_star(lambda_w / s_c) * clv_c) differs per chord AND wavelength (the Rossiter-
 // McLaughlin shift s_c moves the stellar lines across the disk), so neither the flat-star F_out
 // factorisation nor the windowed tail moments apply: every (chord, wavelength) flux is evaluated.
-// One thread per wavelength, kRmP phases per workgroup.  F is computed once per (chord, wavelength)
-// and shared by the workgroup's phases; chords transparent at every phase of the group add F to one
-// shared sum (exp(-tau) == 1 to the last ulp), the others are resolved per phase from a bit mask.
+// One thread per wavelength, kRmP phases per workgroup.  The unocculted flux Fout(w) = sum_c F(c, w) is a
+// per-set quantity (k_rm_fout); a run visits only the chords blocked or active at some phase of its group
+// (F once per such (chord, wavelength), shared by the group's phases) and subtracts their loss from Fout.
 // F_star(t) = 10^(f_k + slope_k (t - x_k)) is evaluated as 10^f_k * exp(ln10 slope_k (t - x_k)) on the
 // LDS copy of the star-table slice that the workgroup's targets t = lambda / s can reach (prom_api.hip
 // rm_slices), bracketed through a slice-local bucket directory; a tile whose slice exceeds kRmStarMax
@@ -36,6 +36,137 @@ __device__ __forceinline__ double exp_tab(double a, const double* __restrict__ t
   return __builtin_amdgcn_ldexp(tab[ki & 255], ki >> 8) * p;
 }
 
+// F_star(lambda_w / s_c) for kRmGroup chords of the LDS list at once (their LDS chains -- directory, bracket steps,
+// node, table exp -- are independent, so interleaving them hides the LDS latency)
+struct RmStar {
+  const double* sx;
+  const double* sF;
+  const double* sc;
+  const int16_t* sdir;
+  const double* sexp;
+  double sx0, inv_h;
+  int32_t m, nb;
+};
+
+template <bool UNISTAR>
+__device__ __forceinline__ void rm_fstar(double (&fsg)[kRmGroup], double lam, const double (&sh)[kRmGroup],
+                                         const RmStar& st, const SigTabDev& star, double fstar_uni) {
+  if constexpr (UNISTAR) {
+#pragma unroll
+    for (int u = 0; u < kRmGroup; ++u) fsg[u] = fstar_uni;
+  } else if (st.m > 0) {
+    const int32_t m = st.m, nb = st.nb;
+    double t[kRmGroup];
+    int k[kRmGroup];
+#pragma unroll
+    for (int u = 0; u < kRmGroup; ++u) {
+      t[u] = lam / sh[u];
+      const double fj = (t[u] - st.sx0) * st.inv_h;
+      const int j = !(fj >= 1.0) ? 1 : (fj >= (double)nb ? nb : (int)fj);
+      k[u] = st.sdir[j - 1];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int u = 0; u < kRmGroup; ++u) k[u] += (k[u] + 1 < m && st.sx[k[u] + 1] <= t[u]) ? 1 : 0;
+    const double xlast = st.sx[m - 1];
+#pragma unroll
+    for (int u = 0; u < kRmGroup; ++u) {
+      const double tu = t[u];
+      if (!(tu >= st.sx0) || tu >= xlast) {
+        // below the table (the slice starts at node 0) / at or beyond the table's last node
+        fsg[u] = tu != tu ? tu : (tu >= xlast ? st.sF[m - 1] : st.sF[0]);
+        continue;
+      }
+      int kk = k[u];
+      if (st.sx[kk + 1] <= tu) {                   // crowded bucket: bisect the rest of the slice
+        int a = kk + 1, b = m - 1;                 // sx[a] <= t < sx[b]
+        while (b - a > 1) {
+          const int mid = (a + b) >> 1;
+          if (st.sx[mid] <= tu) a = mid; else b = mid;
+        }
+        kk = a;
+      }
+      const double xk = st.sx[kk];
+      const double arg = st.sc[kk] * (tu - xk);
+      if (xk == tu) fsg[u] = st.sF[kk];
+      else if (__builtin_isfinite(arg)) fsg[u] = st.sF[kk] * exp_tab(arg, st.sexp);
+      else fsg[u] = sigma_of(tu, star);          // infinite slope (repeated node): np.interp's rules
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kRmGroup; ++u) fsg[u] = sigma_of(lam / sh[u], star);
+  }
+}
+
+// Stages the workgroup's star-table slice {lo, m, half} in LDS: nodes lo .. lo+m-1 as (x_k, 10^f_k, ln10 slope_k)
+// + a directory of nb = 4 half buckets over [x_0, x_m-1]: sdir[j] = last node <= x_0 + j h
+template <bool UNISTAR>
+__device__ __forceinline__ RmStar rm_stage(const SigTabDev& star, const int32_t* __restrict__ slices, double* sx,
+                                           double* sF, double* sc, int16_t* sdir, const double* sexp) {
+  RmStar st{sx, sF, sc, sdir, sexp, 0.0, 0.0, 0, 0};
+  const int32_t* sl = slices + 3 * (int64_t)blockIdx.x;
+  const int64_t lo = sl[0];
+  const int32_t m = UNISTAR ? 0 : sl[1], half = sl[2];
+  st.m = m;
+  st.nb = 4 * half < kRmDir ? 4 * half : kRmDir;
+  if (m > 0) {
+    for (int i = threadIdx.x; i < m; i += kBlock) {
+      const double x0 = star.x[lo + i], f0 = star.y[lo + i];
+      sx[i] = x0;
+      sF[i] = exp10(f0);                       // star tables have offset 0 (prom_transit_set)
+      sc[i] = i + 1 < m ? ((star.y[lo + i + 1] - f0) / (star.x[lo + i + 1] - x0)) * kLn10 : 0.0;
+    }
+    st.sx0 = star.x[lo];
+    const double span = star.x[lo + m - 1] - st.sx0;
+    st.inv_h = span > 0.0 ? (double)st.nb / span : 0.0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < st.nb; j += kBlock) {
+      const double b = st.sx0 + (double)j * (span / (double)st.nb);
+      int pos = 0;
+      for (int stp = half; stp > 0; stp >>= 1) pos += (pos + stp < m && sx[pos + stp] <= b) ? stp : 0;
+      sdir[j] = (int16_t)pos;
+    }
+  }
+  return st;
+}
+
+// Per set: the unocculted flux Fout(w) = sum_c F(c, w) over every chord in chord order (gasProperties.py:1221-1245,
+// the denominator of R), F(c, w) = rho_c (F_star(lambda_w / s_c) clv_c).  It depends only on the chord grid, the
+// star's spectrum and rotation and the wavelengths -- none of which a run changes -- so runs reuse it.
+template <bool UNISTAR>
+__global__ void __launch_bounds__(kBlock) k_rm_fout(const SigTabDev star, const int32_t* __restrict__ slices,
+                                                    const double* __restrict__ wav, int64_t n_wav,
+                                                    const double* __restrict__ crho, const double* __restrict__ cclv,
+                                                    const double* __restrict__ cshift, int32_t n_pr,
+                                                    double* __restrict__ fo) {
+  __shared__ double sexp[256];
+  __shared__ double sx[kRmStarMax], sF[kRmStarMax], sc[kRmStarMax];
+  __shared__ int16_t sdir[kRmDir];
+  sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
+  const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const double lam = wav[w < n_wav ? w : n_wav - 1];
+  const RmStar st = rm_stage<UNISTAR>(star, slices, sx, sF, sc, sdir, sexp);
+  __syncthreads();
+  double fstar_uni = 0.0;
+  if constexpr (UNISTAR) fstar_uni = sigma_of(lam / cshift[0], star);
+  double out = 0.0;
+  for (int32_t c0 = 0; c0 < n_pr; c0 += kRmGroup) {
+    double sh[kRmGroup], fsg[kRmGroup];
+#pragma unroll
+    for (int u = 0; u < kRmGroup; ++u) sh[u] = cshift[c0 + u < n_pr ? c0 + u : n_pr - 1];
+    rm_fstar<UNISTAR>(fsg, lam, sh, st, star, fstar_uni);
+#pragma unroll
+    for (int u = 0; u < kRmGroup; ++u)
+      if (c0 + u < n_pr) out += crho[c0 + u] * (fsg[u] * cclv[c0 + u]);
+  }
+  if (w < n_wav) fo[w] = out;
+}
+
+// Per run: R(o, w) = (Fout(w) - loss(o, w)) / Fout(w), loss = sum over the chords blocked at o of F + sum over the
+// chords active at o of F (1 - e^-tau) -- the reference's sum_unblocked F e^-tau with every transparent chord's
+// exact F (e^-tau == 1 to the last ulp) left inside Fout.  Only chords blocked or active at some phase of the
+// workgroup's group are visited (a 64-chord chunk is compacted by ballot), so F_star is looked up for those alone.
 template <int NSMAX, bool OCML, bool UNISTAR>
 __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__ tabs, int32_t na,
                                                    const SigTabDev star, const int32_t* __restrict__ slices,
@@ -43,6 +174,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
                                                    const double* __restrict__ crho,
                                                    const double* __restrict__ cclv,
                                                    const double* __restrict__ cshift,
+                                                   const double* __restrict__ fout_w,
                                                    const int32_t* __restrict__ flags,
                                                    const double* __restrict__ ncol, int32_t n_pr,
                                                    int32_t n_orb, int32_t* __restrict__ counts,
@@ -52,14 +184,16 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
   __shared__ int16_t sdir[kRmDir];
   __shared__ double sRho[kRmChunk], sClv[kRmChunk], sSh[kRmChunk];
   __shared__ double sN[kRmP * NSMAX * kRmChunk];
-  __shared__ int32_t sMask[kRmChunk];
+  __shared__ int32_t sMask[kRmChunk], sList[kRmChunk];
   __shared__ int32_t scnt[kRmP * 3];
+  __shared__ int32_t s_nl;
   sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
   const int32_t o0 = blockIdx.y * kRmP;
   const int32_t np = n_orb - o0 < kRmP ? n_orb - o0 : kRmP;
   const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
+  const double out = fout_w[live ? w : n_wav - 1];
   // chord counts per phase (stats), by the first workgroup of each phase group
   if (blockIdx.x == 0 && counts) {
     if (threadIdx.x < kRmP * 3) scnt[threadIdx.x] = 0;
@@ -78,31 +212,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       for (int k = 3; k < kCnt; ++k) cp[k] = 0;
     }
   }
-  // star-table slice {lo, m, half}: nodes lo .. lo+m-1 as (x_k, 10^f_k, ln10 slope_k) + a directory of
-  // nb = 4 half buckets over [x_0, x_m-1]: sdir[j] = last node <= x_0 + j h
-  const int32_t* sl = slices + 3 * (int64_t)blockIdx.x;
-  const int64_t lo = sl[0];
-  const int32_t m = UNISTAR ? 0 : sl[1], half = sl[2];
-  const int32_t nb = 4 * half < kRmDir ? 4 * half : kRmDir;
-  double sx0 = 0.0, inv_h = 0.0;
-  if (m > 0) {
-    for (int i = threadIdx.x; i < m; i += kBlock) {
-      const double x0 = star.x[lo + i], f0 = star.y[lo + i];
-      sx[i] = x0;
-      sF[i] = exp10(f0);                       // star tables have offset 0 (prom_transit_set)
-      sc[i] = i + 1 < m ? ((star.y[lo + i + 1] - f0) / (star.x[lo + i + 1] - x0)) * kLn10 : 0.0;
-    }
-    sx0 = star.x[lo];
-    const double span = star.x[lo + m - 1] - sx0;
-    inv_h = span > 0.0 ? (double)nb / span : 0.0;
-    __syncthreads();
-    for (int j = threadIdx.x; j < nb; j += kBlock) {
-      const double b = sx0 + (double)j * (span / (double)nb);
-      int pos = 0;
-      for (int st = half; st > 0; st >>= 1) pos += (pos + st < m && sx[pos + st] <= b) ? st : 0;
-      sdir[j] = (int16_t)pos;
-    }
-  }
+  const RmStar st = rm_stage<UNISTAR>(star, slices, sx, sF, sc, sdir, sexp);
   // sigma_s at each of this thread's phases (shift_o * lambda, as getLOSopticalDepth_Batch)
   double sg[kRmP][NSMAX];
 #pragma unroll
@@ -112,24 +222,34 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       sg[p][s] = (p < np && s < na) ? sigma_of(tabs[s].shift[o0 + p] * lam, tabs[s]) : 0.0;
   double fstar_uni = 0.0;
   if constexpr (UNISTAR) fstar_uni = sigma_of(lam / cshift[0], star);
-  double in[kRmP];
+  double loss[kRmP];
 #pragma unroll
-  for (int p = 0; p < kRmP; ++p) in[p] = 0.0;
-  double out = 0.0, tall = 0.0;
+  for (int p = 0; p < kRmP; ++p) loss[p] = 0.0;
   for (int32_t c0 = 0; c0 < n_pr; c0 += kRmChunk) {
     const int nch = n_pr - c0 < kRmChunk ? n_pr - c0 : kRmChunk;
     __syncthreads();
-    for (int i = threadIdx.x; i < nch; i += kBlock) {
-      sRho[i] = crho[c0 + i];
-      sClv[i] = cclv[c0 + i];
-      sSh[i] = cshift[c0 + i];
+    if (threadIdx.x < kRmChunk) {
+      // wave 0: the chunk's masks (active bits 0-7, blocked bits 8-15) and the list of chords with any bit, in
+      // chord order (ballot + popcount prefix)
+      const int i = threadIdx.x;
       int32_t am = 0, bm = 0;
-      for (int p = 0; p < np; ++p) {
-        const int32_t f = flags[(int64_t)(o0 + p) * n_pr + c0 + i];
-        am |= (f == 0) << p;
-        bm |= (f == 2) << p;
+      if (i < nch) {
+        for (int p = 0; p < np; ++p) {
+          const int32_t f = flags[(int64_t)(o0 + p) * n_pr + c0 + i];
+          am |= (f == 0) << p;
+          bm |= (f == 2) << p;
+        }
       }
-      sMask[i] = am | (bm << 8);
+      const int32_t mk = am | (bm << 8);
+      sMask[i] = mk;
+      const unsigned long long bal = __ballot(mk != 0);
+      if (mk != 0) sList[__popcll(bal & ((1ull << i) - 1ull))] = i;
+      if (i == 0) s_nl = __popcll(bal);
+      if (i < nch) {
+        sRho[i] = crho[c0 + i];
+        sClv[i] = cclv[c0 + i];
+        sSh[i] = cshift[c0 + i];
+      }
     }
     for (int i = threadIdx.x; i < na * np * nch; i += kBlock) {
       const int sp = i / nch, c = i - sp * nch;     // sp = s * np + p
@@ -137,67 +257,22 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       sN[(p * NSMAX + s) * kRmChunk + c] = ncol[((int64_t)s * n_orb + o0 + p) * n_pr + c0 + c];
     }
     __syncthreads();
-    for (int cg = 0; cg < nch; cg += kRmGroup) {
-      // F_star for kRmGroup chords at once: their LDS chains (directory -> bracket steps -> node ->
-      // table exp) are independent, so interleaving them hides the LDS latency
-      double fsg[kRmGroup];
-      if constexpr (UNISTAR) {
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) fsg[u] = fstar_uni;
-      } else if (m > 0) {
-        double t[kRmGroup];
-        int k[kRmGroup];
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) {
-          t[u] = lam / sSh[cg + u < nch ? cg + u : nch - 1];
-          const double fj = (t[u] - sx0) * inv_h;
-          const int j = !(fj >= 1.0) ? 1 : (fj >= (double)nb ? nb : (int)fj);
-          k[u] = sdir[j - 1];
-        }
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int u = 0; u < kRmGroup; ++u) k[u] += (k[u] + 1 < m && sx[k[u] + 1] <= t[u]) ? 1 : 0;
-        const double xlast = sx[m - 1];
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) {
-          const double tu = t[u];
-          if (!(tu >= sx0) || tu >= xlast) {
-            // below the table (the slice starts at node 0) / at or beyond the table's last node
-            fsg[u] = tu != tu ? tu : (tu >= xlast ? sF[m - 1] : sF[0]);
-            continue;
-          }
-          int kk = k[u];
-          if (sx[kk + 1] <= tu) {                      // crowded bucket: bisect the rest of the slice
-            int a = kk + 1, b = m - 1;                 // sx[a] <= t < sx[b]
-            while (b - a > 1) {
-              const int mid = (a + b) >> 1;
-              if (sx[mid] <= tu) a = mid; else b = mid;
-            }
-            kk = a;
-          }
-          const double xk = sx[kk];
-          const double arg = sc[kk] * (tu - xk);
-          if (xk == tu) fsg[u] = sF[kk];
-          else if (__builtin_isfinite(arg)) fsg[u] = sF[kk] * exp_tab(arg, sexp);
-          else fsg[u] = sigma_of(tu, star);          // infinite slope (repeated node): np.interp's rules
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < kRmGroup; ++u) fsg[u] = sigma_of(lam / sSh[cg + u < nch ? cg + u : nch - 1], star);
-      }
+    const int32_t nl = s_nl;
+    for (int cg = 0; cg < nl; cg += kRmGroup) {
+      double sh[kRmGroup], fsg[kRmGroup];
+      int cl[kRmGroup];
 #pragma unroll
       for (int u = 0; u < kRmGroup; ++u) {
-        const int c = cg + u;
-        if (c >= nch) break;
-        const double fs = fsg[u];
-        const double Fc = sRho[c] * (fs * sClv[c]);
-        out += Fc;
+        cl[u] = sList[cg + u < nl ? cg + u : nl - 1];
+        sh[u] = sSh[cl[u]];
+      }
+      rm_fstar<UNISTAR>(fsg, lam, sh, st, star, fstar_uni);
+#pragma unroll
+      for (int u = 0; u < kRmGroup; ++u) {
+        if (cg + u >= nl) break;
+        const int c = cl[u];
+        const double Fc = sRho[c] * (fsg[u] * sClv[c]);
         const int32_t mk = __builtin_amdgcn_readfirstlane(sMask[c]);
-        if (mk == 0) {
-          tall += Fc;                                  // transparent at every phase of the group
-          continue;
-        }
 #pragma unroll
         for (int p = 0; p < kRmP; ++p) {
           if (p >= np) break;
@@ -206,10 +281,12 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
 #pragma unroll
             for (int s = 0; s < NSMAX; ++s)
               if (s < na) tau += sN[(p * NSMAX + s) * kRmChunk + c] * sg[p][s];
-            if (OCML || !(tau < 700.0 && tau > -700.0)) in[p] += Fc * exp(-tau);
-            else in[p] = acc_exp256(in[p], Fc, tau * kM256Ln2, sexp);
-          } else if (!((mk >> (p + 8)) & 1)) {
-            in[p] += Fc;                               // transparent at this phase
+            // loss += F (1 - e^-tau)
+            loss[p] += Fc;
+            if (OCML || !(tau < 700.0 && tau > -700.0)) loss[p] -= Fc * exp(-tau);
+            else loss[p] = acc_exp256(loss[p], -Fc, tau * kM256Ln2, sexp);
+          } else if ((mk >> (p + 8)) & 1) {
+            loss[p] += Fc;                             // blocked at this phase
           }
         }
       }
@@ -218,8 +295,21 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
   if (live) {
 #pragma unroll
     for (int p = 0; p < kRmP; ++p)
-      if (p < np) R[(int64_t)(o0 + p) * n_wav + w] = (in[p] + tall) / out;
+      if (p < np) R[(int64_t)(o0 + p) * n_wav + w] = (out - loss[p]) / out;
   }
+}
+
+void launch_rm_fout(hipStream_t s, TransitDev& tr) {
+  const unsigned nb = (unsigned)((tr.n_wav + kBlock - 1) / kBlock);
+  tr.rm_fout.ensure(sizeof(double) * tr.n_wav);
+#define PROM_RMF(UV)                                                                                       \
+  hipLaunchKernelGGL((k_rm_fout<UV>), dim3(nb), dim3(kBlock), 0, s, tr.star_tab, tr.rm_slices.as<int32_t>(),  \
+                     tr.wav.as<double>(), tr.n_wav, tr.crho.as<double>(), tr.cclv.as<double>(),                  \
+                     tr.cshift.as<double>(), tr.n_pr, tr.rm_fout.as<double>())
+  if (tr.star_uniform) PROM_RMF(true);
+  else PROM_RMF(false);
+#undef PROM_RMF
+  PROM_HIP(hipGetLastError());
 }
 
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev) {
@@ -233,7 +323,7 @@ void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEv
   hipExtLaunchKernelGGL((k_tau_rm<NSV, OC, UV>), g, dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, \
                         tr.sigtab.as<SigTabDev>(), na, star, tr.rm_slices.as<int32_t>(), tr.wav.as<double>(), \
                         tr.n_wav, tr.crho.as<double>(), tr.cclv.as<double>(), tr.cshift.as<double>(),     \
-                        rs.flags.as<int32_t>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb,                  \
+                        tr.rm_fout.as<double>(), rs.flags.as<int32_t>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb,                  \
                         tr.count_evals ? rs.counts.as<int32_t>() : nullptr, rs.R.as<double>())
 #define PROM_RM_NS(OC)                       \
   if (na <= 1) PROM_RM(1, OC);               \

@@ -66,7 +66,7 @@ struct OpAddI { __device__ int32_t operator()(int32_t a, int32_t b) const { retu
 // error), so one table exp serves four octaves.  Chain 0 also sums the tail moments sum F n^e.  The parts'
 // node sums go to `part`; the last part to finish (atomic counter per (phase, chain), reset by it) adds them in
 // part order -- deterministic -- and writes the Chebyshev coefficients (and, chain 0, the header).
-constexpr int kTcB2 = 256;               // threads per workgroup
+constexpr int kTcB2 = 256;               // threads per workgroup (16 groups of 16 node threads)
 constexpr int kTcPartLds = 1024;         // a part's chords staged in LDS up to this many (16 KB)
 static_assert(kTcPartVals == (kTcChain + 1) * kTcD, "per part: 4 octaves' node sums, then the moments' row");
 
@@ -85,7 +85,8 @@ __device__ __forceinline__ double exp256(double y, const double* __restrict__ ta
 
 __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ flags, const double* __restrict__ fout,
                                                    const double* __restrict__ ncol, int32_t n_pr, int32_t n_parts,
-                                                   double ybound, int32_t lg, double* __restrict__ hdr,
+                                                   double ybound, int32_t lg, const double* __restrict__ tcc,
+                                                   double* __restrict__ hdr,
                                                    double* __restrict__ tab, double* __restrict__ part,
                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ counts,
                                                    unsigned long long* __restrict__ evals) {
@@ -93,8 +94,16 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   const int32_t ch = blockIdx.x, pt = blockIdx.y, o = blockIdx.z;
   const int32_t n_ch = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef PROM_TRACE
+  // per workgroup (tools/trace_tcb.py), at g_trace[2^19 + 8 id]: wall clock at start, after the phase sums, after
+  // the node sums, after the hand-off, at the end; then ch | part << 8 | phase << 16, L | last << 16
+  unsigned long long* tq = g_trace + (1u << 19) + 8ull * ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+  if (tid == 0) tq[0] = wall_clock64();
+  __shared__ unsigned long long s_tmax[2];   // the slowest wave's end of the sweep / of the node sums
+  if (tid == 0) s_tmax[0] = s_tmax[1] = 0;
+  __syncthreads();
+#endif
   __shared__ double etab[256];
-  __shared__ double cm[kTcD * kTcD];
   __shared__ double sd[4][NW];
   __shared__ int32_t si[4][NW];
   __shared__ double red[NW][kTcChain + 1][kTcD];
@@ -103,12 +112,8 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   __shared__ double2 spart[kTcPartLds];
   const int32_t* fl = flags + (int64_t)o * n_pr;
   const double* nc = ncol + (int64_t)o * n_pr;
-  // the exp table and the Chebyshev matrix c_k = sum_j f_j cm[k][j] (one cosine per thread)
-  etab[tid] = kExp2TableDev[8 * tid];
-  {
-    const int k = tid >> 4, jj = tid & 15;
-    cm[tid] = cos(M_PI * (double)k * ((double)jj + 0.5) / (double)kTcD) * ((k == 0 ? 1.0 : 2.0) / (double)kTcD);
-  }
+  // the exp table (the Chebyshev matrix and the node factors come precomputed: tcc)
+  if (tid < 256) etab[tid] = kExp2TableDev[8 * tid];
   // 1. the phase's sums (every workgroup of the phase, the same order).  Sweeps of kTcB2 x U chords, every load
   // of a sweep issued before any is used (one round trip per sweep, no load behind a flag test); this part's
   // chords [c_lo, c_hi) are kept in LDS on the way ({F_out, N}, zero for inactive chords) for step 2
@@ -116,37 +121,42 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   const bool in_lds = c_hi - c_lo <= kTcPartLds;
   double fs = 0.0, ts = 0.0, nmax = 0.0, nmin = __builtin_inf();
   int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0;
-  constexpr int U = 8;
+  constexpr int U = 12;   // (one sweep up to 3072 chords)
   for (int32_t c0 = 0; c0 < n_pr; c0 += kTcB2 * U) {
     int32_t f[U];
     double fo[U], N[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int32_t c = c0 + u * kTcB2 + tid;
-      const bool in = c < n_pr;
-      f[u] = in ? fl[c] : 3;
-      fo[u] = in ? fout[c] : 0.0;
-      N[u] = in ? nc[c] : 0.0;
+      const int32_t c = min(c0 + u * kTcB2 + tid, n_pr - 1);   // (clamped: no branch around the loads)
+      f[u] = fl[c];
+      fo[u] = fout[c];
+      N[u] = nc[c];
     }
+    // branch-free accumulation (selects; a chord past n_pr adds nothing)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int32_t c = c0 + u * kTcB2 + tid;
-      if (f[u] == 3) continue;
-      fs += fo[u];
-      if (f[u] == 1) { ts += fo[u]; ++ntr; }
-      else if (f[u] == 2) ++nbl;
-      else if (f[u] == 0) {
-        ++nact;
-        if (!__builtin_isfinite(N[u])) ++nnf;
-        else {
-          nmax = N[u] > nmax ? N[u] : nmax;
-          if (N[u] > 0.0) nmin = N[u] < nmin ? N[u] : nmin;
-        }
-      }
-      if (in_lds && c >= c_lo && c < c_hi)
-        spart[c - c_lo] = f[u] == 0 ? make_double2(fo[u], N[u]) : make_double2(0.0, 0.0);
+      const bool valid = c < n_pr;
+      const bool act = valid && f[u] == 0, tra = valid && f[u] == 1;
+      const bool fin_n = __builtin_isfinite(N[u]);
+      fs += valid ? fo[u] : 0.0;
+      ts += tra ? fo[u] : 0.0;
+      ntr += tra ? 1 : 0;
+      nbl += (valid && f[u] == 2) ? 1 : 0;
+      nact += act ? 1 : 0;
+      nnf += (act && !fin_n) ? 1 : 0;
+      nmax = (act && fin_n && N[u] > nmax) ? N[u] : nmax;
+      nmin = (act && fin_n && N[u] > 0.0 && N[u] < nmin) ? N[u] : nmin;
+      if (in_lds && c >= c_lo && c < c_hi) spart[c - c_lo] = act ? make_double2(fo[u], N[u]) : make_double2(0.0, 0.0);
     }
   }
+#ifdef PROM_TRACE
+  if (lane == 0) {   // (the slowest wave, after its sweep's loads are used)
+    double x = fs;
+    asm volatile("" : "+v"(x));
+    atomicMax(&s_tmax[0], wall_clock64());
+  }
+#endif
   fs = tc_wred<double>(fs, OpAdd());
   ts = tc_wred<double>(ts, OpAdd());
   nmax = tc_wred<double>(nmax, OpMax());
@@ -184,6 +194,14 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
     }
   }
   const int32_t j0 = ch * kTcChain;
+#ifdef PROM_TRACE
+  if (tid == 0) {
+    tq[1] = wall_clock64();
+    tq[5] = (unsigned long long)ch | ((unsigned long long)pt << 8) | ((unsigned long long)o << 16);
+    tq[6] = (unsigned long long)(uint32_t)L;
+    tq[2] = tq[3] = tq[4] = tq[1];
+  }
+#endif
   if (ch > 0 && j0 >= L) return;   // (chain 0 always runs: the moments and the header)
   // 2. this part's chords at this chain's nodes (and, chain 0, the moments); thread (k, g): node k, chords
   // c_lo + g + 16 m from LDS (the 16 threads of a group read the same entry: a broadcast)
@@ -195,32 +213,50 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   const double inv_nmax = fin ? 1.0 / nmax : 0.0;
   // node k of octave j0: q_k = 2^(j0 - 7 + v_k), v_k = (u_k + 1) / 2, u_k = cos(pi (k + 1/2) / 16);
   // y = N q_k / N_max (-256 / ln2)
-  const double uk = cos(M_PI * ((double)k + 0.5) / (double)kTcD);
-  const double sk = ldexp(exp2(0.5 * (uk + 1.0)), j0 + kTcExpEps) * inv_nmax * kM256Ln2;
-  __syncthreads();   // etab, cm
+  const double sk = ldexp(tcc[kTcD * kTcD + k], j0 + kTcExpEps) * inv_nmax * kM256Ln2;
+  __syncthreads();   // etab
   if (fin) {
-    for (int32_t c = c_lo + g; c < c_hi; c += kTcB2 / 16) {
-      double2 fn;
-      if (in_lds) fn = spart[c - c_lo];
-      else fn = fl[c] == 0 ? make_double2(fout[c], nc[c]) : make_double2(0.0, 0.0);
-      const double F = fn.x * inv_fs, N = fn.y;
-      if (do_tab) {
-        double e = exp256(N * sk, etab);
-        acc[0] = __builtin_fma(F, e, acc[0]);
+    auto chord = [&](int32_t c) -> double2 {
+      if (in_lds) return spart[c - c_lo];
+      return fl[c] == 0 ? make_double2(fout[c], nc[c]) : make_double2(0.0, 0.0);
+    };
+    if (do_tab) {
+      // two chords per iteration (independent exps; the second is the part's zero entry past c_hi)
+      for (int32_t c = c_lo + g; c < c_hi; c += 2 * (kTcB2 / 16)) {
+        const int32_t c2 = c + kTcB2 / 16;
+        const double2 f1 = chord(c);
+        const double2 f2 = c2 < c_hi ? chord(c2) : make_double2(0.0, 0.0);
+        double e1 = exp256(f1.y * sk, etab), e2 = exp256(f2.y * sk, etab);
+        const double F1 = f1.x * inv_fs, F2 = f2.x * inv_fs;
+        acc[0] = __builtin_fma(F1, e1, acc[0]);
+        acc[0] = __builtin_fma(F2, e2, acc[0]);
 #pragma unroll
         for (int m = 1; m < kTcChain; ++m) {
-          e = e * e;
-          acc[m] = __builtin_fma(F, e, acc[m]);
+          e1 = e1 * e1;
+          e2 = e2 * e2;
+          acc[m] = __builtin_fma(F1, e1, acc[m]);
+          acc[m] = __builtin_fma(F2, e2, acc[m]);
         }
       }
-      if (ch == 0 && k < 6) {
-        const double n = N * inv_nmax;
-        double pw = F;
+    }
+    if (ch == 0 && k < 6) {
+      // tail moments sum F n^e (e = k)
+      for (int32_t c = c_lo + g; c < c_hi; c += kTcB2 / 16) {
+        const double2 fn = chord(c);
+        const double n = fn.y * inv_nmax;
+        double pw = fn.x * inv_fs;
         for (int e2 = 0; e2 < k; ++e2) pw *= n;
         mom += pw;
       }
     }
   }
+#ifdef PROM_TRACE
+  if (lane == 0) {
+    double x = acc[0] + mom;
+    asm volatile("" : "+v"(x));
+    atomicMax(&s_tmax[1], wall_clock64());
+  }
+#endif
   // fold the 16 groups: across the 4 rows of a wave (butterfly: every row the same sum), then the waves in LDS
 #pragma unroll
   for (int m = 0; m < kTcChain; ++m) {
@@ -235,41 +271,69 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
     red[wid][kTcChain][lane] = mom;
   }
   __syncthreads();
+#ifdef PROM_TRACE
+  if (tid == 0) { tq[7] = s_tmax[0]; tq[2] = s_tmax[1]; }
+#endif
   const int32_t item = o * n_ch + ch;
   double* pp = part + (int64_t)item * kTcPartMax * kTcPartVals;
-  // hand-off to the last part of this (phase, chain) (MI355X_MICROARCH.md, inter-workgroup visibility, first
-  // row of the sc1 table): write-through (sc1) stores, every storing wave's vmcnt(0), a barrier, one agent-scope
-  // atomic add per workgroup; the workgroup whose add comes last reads with sc1 loads after a barrier
+  // the workgroup's sums, waves in order
+  double v = 0.0;
   if (tid < (kTcChain + 1) * kTcD) {
     const int m = tid >> 4, kk = tid & 15;
-    double v = red[0][m][kk];
+    v = red[0][m][kk];
 #pragma unroll
     for (int w = 1; w < NW; ++w) v += red[w][m][kk];
-    __hip_atomic_store(&pp[pt * kTcPartVals + tid], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const int32_t prev = __hip_atomic_fetch_add(&cnt[item], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == n_parts - 1 ? 1 : 0;
-    // ready for the next run of this slot (a later launch: the kernel boundary orders it)
-    if (s_last) __hip_atomic_store(&cnt[item], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (tid < (kTcChain + 1) * kTcD) {
-    double v = 0.0;
-    for (int q = 0; q < n_parts; ++q)
-      v += __hip_atomic_load(&pp[q * kTcPartVals + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sf[tid >> 4][tid & 15] = v;
-  }
-  __syncthreads();
+  if (n_parts == 1) {
+    // every chord in this workgroup: no hand-off
+    if (tid < (kTcChain + 1) * kTcD) sf[tid >> 4][tid & 15] = v;
+#ifdef PROM_TRACE
+    if (tid == 0) {
+      tq[3] = tq[4] = wall_clock64();
+      tq[6] |= 1ull << 16;
+    }
+#endif
+  } else {
+    // hand-off to the last part of this (phase, chain) (MI355X_MICROARCH.md, inter-workgroup visibility, first
+    // row of the sc1 table): write-through (sc1) stores, every storing wave's vmcnt(0), a barrier, one agent-scope
+    // atomic add per workgroup; the workgroup whose add comes last reads with sc1 loads after a barrier
+    if (tid < (kTcChain + 1) * kTcD)
+      __hip_atomic_store(&pp[pt * kTcPartVals + tid], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int32_t prev = __hip_atomic_fetch_add(&cnt[item], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = prev == n_parts - 1 ? 1 : 0;
+      // ready for the next run of this slot (a later launch: the kernel boundary orders it)
+      if (s_last) __hip_atomic_store(&cnt[item], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#ifdef PROM_TRACE
+    if (tid == 0) {
+      tq[3] = tq[4] = wall_clock64();
+      tq[6] |= (unsigned long long)s_last << 16;
+    }
+#endif
+    if (!s_last) return;
+    if (tid < (kTcChain + 1) * kTcD) {
+      // every part's value loaded first (independent loads in flight together), then added in part order
+      double pv[kTcPartMax];
+#pragma unroll
+      for (int q = 0; q < kTcPartMax; ++q)
+        pv[q] = q < n_parts ? __hip_atomic_load(&pp[q * kTcPartVals + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+      double sv = 0.0;
+#pragma unroll
+      for (int q = 0; q < kTcPartMax; ++q)
+        if (q < n_parts) sv += pv[q];
+      sf[tid >> 4][tid & 15] = sv;
+    }
+  }  __syncthreads();
   if (tid < kTcChain * kTcD) {
     const int m = tid >> 4, kk = tid & 15;
     if (do_tab && j0 + m < L) {
       double c = 0.0;
 #pragma unroll
-      for (int jj = 0; jj < kTcD; ++jj) c = __builtin_fma(sf[m][jj], cm[kk * kTcD + jj], c);
+      for (int jj = 0; jj < kTcD; ++jj) c = __builtin_fma(sf[m][jj], tcc[kk * kTcD + jj], c);
       tab[((int64_t)o * lg + j0 + m) * kTcD + kk] = c;
     }
   }
@@ -300,6 +364,9 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   }
   if (evals && tid == 0 && do_tab)
     atomicAdd(&evals[item & 63], (unsigned long long)nact * kTcD * (L - j0 < kTcChain ? L - j0 : kTcChain));
+#ifdef PROM_TRACE
+  if (tid == 0) tq[4] = wall_clock64();
+#endif
 }
 
 // T_o(Y) for a phase whose columns are finite (header h, its table rows tabo)
@@ -356,9 +423,11 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
                                                      int32_t n_rc, int32_t rf, const TcArgs ta) {
   static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per workgroup");
   constexpr int NT = UNI ? 1 : R;
-  __shared__ double2 slds[2 * kSigSeg];
-  double2* sxr = slds;
-  double2* sel = slds + kSigSeg;
+  // every species' slice staged at once (one load round, one barrier): per species the nodes x_k (m + 1 of them)
+  // and the records' {(chi) E_k, slope_k} (24 bytes a record: four 3-species workgroups per CU)
+  constexpr int SXN = kSigSeg + 2;   // (x_0 .. x_m, padded to 16 bytes)
+  __shared__ double2 ssel[(D > 0 && NT > 1) ? NSIG * kSigSeg : 1];
+  __shared__ double ssx[(D > 0 && NT > 1) ? NSIG * SXN : 1];
   const int tid = threadIdx.x;
   const int32_t RF = rf;
   const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * ((n_rows + RF - 1) / RF);
@@ -378,7 +447,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
     wb = grp * 8 + rem % 8;
     r0 = (int32_t)(rem / 8) * R;
     if (wb >= n_blk) return;
-    if constexpr (NT == 1) {
+    if constexpr (NT == 1 || D == 0) {
       // one target row (one phase, or phases sharing one Doppler factor): no LDS slices -- each lane reads its
       // own 32-byte record from the global table, adjacent wavelengths' records adjacent (coalesced), no
       // barriers; every block here (the launcher passes no front)
@@ -388,6 +457,16 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
       for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
       if (!lds_ok) return;   // (a front workgroup's)
     }
+  }
+  // the block's segments, every species at once
+  SigSeg sgs[NSIG];
+#pragma unroll
+  for (int s = 0; s < NSIG; ++s) sgs[s] = seg[wb * NSIG + s];
+  // the rows' curve headers, staged with the slices (read after the lookups: no load round at the end)
+  __shared__ double shdr[R * kTcHdr];
+  if (tid < R * kTcHdr) {
+    const int32_t rr = r0 + tid / kTcHdr;
+    shdr[tid] = ta.hdr[(int64_t)(rr < n_rows ? rr : n_rows - 1) * kTcHdr + tid % kTcHdr];
   }
   const int32_t rlim = r0 + rcap < n_rows ? r0 + rcap : n_rows;
   rcap = rlim - r0;
@@ -408,10 +487,42 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
 #pragma unroll
   for (int r = 0; r < NT; ++r) acc[r] = 0.0;
   double choff = 0.0;
+  if constexpr (D > 0 && NT > 1) {
+    if (lds_ok) {
+      // each thread: records tid and tid + 256 of every species' slice (m <= kSigSeg = 512), all loads in flight
+      // before the first LDS write
+      double4 qa[NSIG], qb[NSIG];
+#pragma unroll
+      for (int s = 0; s < NSIG; ++s) {
+        const double4* __restrict__ rr = tabv.t[s].rec + sgs[s].lo;
+        qa[s] = rr[tid < sgs[s].m ? tid : 0];
+        qb[s] = rr[tid + kBlock < sgs[s].m ? tid + kBlock : 0];
+      }
+#pragma unroll
+      for (int s = 0; s < NSIG; ++s) {
+        const double chi = tabv.t[s].chi;
+        double* sx = ssx + s * SXN;
+        double2* sel = ssel + s * kSigSeg;
+        const int32_t m = sgs[s].m;
+        if (tid < m) {
+          sx[tid] = qa[s].x;
+          sel[tid] = make_double2(MG ? chi * qa[s].y : qa[s].y, qa[s].z);
+          if (tid == m - 1) sx[m] = qa[s].w;   // the last record's upper node
+        }
+        if (tid + kBlock < m) {
+          sx[tid + kBlock] = qb[s].x;
+          sel[tid + kBlock] = make_double2(MG ? chi * qb[s].y : qb[s].y, qb[s].z);
+          if (tid + kBlock == m - 1) sx[m] = qb[s].w;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (!lds_ok) __syncthreads();   // (shdr)
 #pragma unroll
   for (int s = 0; s < NSIG; ++s) {
     const SigTabDev& tb = tabv.t[s];
-    const SigSeg sg = seg[wb * NSIG + s];
+    const SigSeg& sg = sgs[s];
     if constexpr (D == 0) {
       // tables too coarse for a degree-14 e^a polynomial: numpy.interp + exp10 per target (sigma_seg: the
       // block's verified guess into the global x / f arrays), bit for bit the per-target lookups
@@ -425,15 +536,6 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
     }
     const double off = tb.offset, chi = tb.chi;
     if constexpr (MG) choff += chi * off;
-    if (lds_ok) {
-      if (s > 0) __syncthreads();   // the previous species' slice is no longer read
-      for (int32_t i = tid; i < sg.m; i += kBlock) {
-        const double4 q = tb.rec[sg.lo + i];
-        sxr[i] = make_double2(q.x, q.w);
-        sel[i] = make_double2(MG ? chi * q.y : q.y, q.z);
-      }
-      __syncthreads();
-    }
     const bool exact = (sg.kind & 4) != 0;
     // v = (chi) E_k e^a: merged, accumulated; one species, sigma = E_k e^a - offset
     auto emit = [&](int r, double ce, double p) {
@@ -473,7 +575,9 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
           else acc[r] = v;
         }
       }
-    } else {
+    } else if constexpr (D > 0 && NT > 1) {
+      const double* sx = ssx + s * SXN;
+      const double2* sel = ssel + s * kSigSeg;
       auto lds_rows = [&](auto guard) {
         constexpr bool GD = decltype(guard)::value;
         double xk[NT];
@@ -483,12 +587,12 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
           if (GD && r >= ncap) break;
           const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
           if (exact) {
-            xk[r] = sxr[g].x;
+            xk[r] = sx[g];
             el[r] = sel[g];
           } else {
-            const double2 xx = sxr[g];
+            const double2 xx = make_double2(sx[g], sx[g + 1]);
             const int32_t k = tt[r] < xx.x ? g - 1 : (tt[r] >= xx.y ? g + 1 : g);
-            xk[r] = sxr[k].x;
+            xk[r] = sx[k];
             el[r] = sel[k];
           }
         }
@@ -512,7 +616,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
     if (r >= rcap) break;
     const int32_t o = r0 + r;
     const double Y = acc[UNI ? 0 : r];
-    const double* h = ta.hdr + (int64_t)o * kTcHdr;
+    const double* h = shdr + r * kTcHdr;
     double v;
     if (!((int32_t)h[kTcHFlags] & 2)) {
       v = tc_eval(Y, h, ta.tab + (int64_t)o * ta.lg * kTcD, ta.flags + (int64_t)o * ta.n_pr,
@@ -583,7 +687,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   const int32_t n_parts = tr.tc_parts;
   hipExtLaunchKernelGGL(k_tc_build, dim3((unsigned)n_ch, (unsigned)n_parts, (unsigned)tr.n_orb), dim3(kTcB2), 0, s,
                         ev_tb0, ev_tb1, 0, rs.flags.as<int32_t>(), tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr,
-                        n_parts, tr.tc_ybound, lg, rs.tc_hdr.as<double>(), rs.tc_tab.as<double>(), rs.tc_part.as<double>(),
+                        n_parts, tr.tc_ybound, lg, tr.tc_const.as<double>(), rs.tc_hdr.as<double>(), rs.tc_tab.as<double>(), rs.tc_part.as<double>(),
                         rs.tc_cnt.as<int32_t>(), rs.counts.as<int32_t>(), evals);
   PROM_HIP(hipGetLastError());
   TcArgs ta{};
