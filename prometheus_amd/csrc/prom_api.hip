@@ -842,9 +842,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         key_gen.push_back(ctx->tables[t.table].gen);
         key_sh.insert(key_sh.end(), sh.begin() + t.scenario * n_orb, sh.begin() + (t.scenario + 1) * n_orb);
       }
-      // (without orbital Doppler shift only the transmission-curve path reads them)
-      const bool want_seg = !tr.uniform_shift || tr.tcurve;
-      const bool seg_reuse = want_seg && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
+      // (every path with resampled rows reads them, with or without orbital Doppler shift).  PROM_SIGMA_ROWS=0
+      // (validation): every block without a guess -- per-target directory lookups (sigma_of) everywhere
+      const char* srows = std::getenv("PROM_SIGMA_ROWS");
+      const bool no_guess = srows && std::atoi(srows) == 0;
+      const bool want_seg = true;
+      const bool seg_reuse = !no_guess && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
                              key_sh == tr.seg_key_sh && (int64_t)tr.seg_key_wav.size() == tr.n_wav &&
                              std::memcmp(tr.seg_key_wav.data(), pb->wavelength, sizeof(double) * tr.n_wav) == 0;
       // reused segments stay valid only if this set completes; a throw below must not leave the key
@@ -852,11 +855,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       tr.seg_key_valid = false;
       seg_key_keep = seg_reuse;   // the stored key stays as it is (re-validated at the end)
       if (seg_reuse) {
-        tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
+        tr.sig_seg_ok = true;
       } else if (want_seg && n_atoms >= 1 && n_atoms <= 4) {
         tr.seg_key_valid = false;
         const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
         std::vector<prom::SigSeg> seg(nb * n_atoms, prom::SigSeg{0, 0, 0, 0, 0.0, 0.0});
+        std::vector<prom::SigSeg> seg4(nb * n_atoms * 4, prom::SigSeg{0, 0, 0, 0, 0.0, 0.0});   // per wavefront
         int32_t ia = 0;
         for (const auto& t : tr.terms) {
           if (t.is_molecule) continue;
@@ -875,29 +879,16 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
             int64_t j = (int64_t)(std::upper_bound(X.begin(), X.end(), v) - X.begin()) - 1;
             return j < 0 ? 0 : (j > n - 2 ? n - 2 : j);
           };
-          auto blocks = [&](int64_t b0, int64_t b1) {
-          for (int64_t b = b0; ok && b < b1; ++b) {
-            double lmin = INFINITY, lmax = -INFINITY;
-            bool fin = true;
-            for (int64_t w = b * prom::kSigBlockW; w < std::min<int64_t>(tr.n_wav, (b + 1) * prom::kSigBlockW); ++w) {
-              const double l = pb->wavelength[w];
-              if (!(l > 0.0) || !std::isfinite(l)) fin = false;
-              lmin = std::min(lmin, l);
-              lmax = std::max(lmax, l);
-            }
-            if (!fin) continue;
-            const double tlo = smin * lmin, thi = smax * lmax;
-            // every target inside [x_0, x_{n-1}): no clamp or end rule
-            if (!(tlo >= X[0] && thi < X[n - 1])) continue;
+          // the slice [lo, hi] of targets in [tlo, thi] and its linear bracket guess, verified at both ends of
+          // every node interval (g and numpy's bracket are monotone step functions, and the bracket is constant
+          // inside an interval): kind 1 (LDS-sized) or 2 with a guess, 0 without; false: no slice
+          auto make_seg = [&](double tlo, double thi, prom::SigSeg& e) -> bool {
             const int64_t lo = bracket(tlo);
             const int64_t hi = bracket(thi) + 1;
             const int64_t m = hi - lo + 1;
-            if (m < 2 || m > INT32_MAX / 2) continue;
-            prom::SigSeg& e = seg[b * n_atoms + ia];
+            if (m < 2 || m > INT32_MAX / 2) return false;
             e.lo = (int32_t)lo;
             e.m = (int32_t)m;
-            // linear guess over the slice, verified at both ends of every node interval (g and numpy's
-            // bracket are monotone step functions, and the bracket is constant inside an interval)
             const double xs = X[lo], span = X[hi] - X[lo];
             const double inv = span > 0.0 ? (double)(m - 1) / span : 0.0;
             const double b0 = -(xs * inv);
@@ -915,10 +906,50 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
               const int64_t ga = guess(a), gz = guess(z);
               if (ga < k - 1 || ga > k + 1 || gz < k - 1 || gz > k + 1) lin = false;
             }
+            e.kind = 0;
             if (lin) {
               e.kind = m <= prom::kSigSeg ? 1 : 2;
               e.xs = b0;
               e.inv = inv;
+            }
+            return true;
+          };
+          auto blocks = [&](int64_t b0, int64_t b1) {
+          for (int64_t b = b0; ok && b < b1; ++b) {
+            double lmin = INFINITY, lmax = -INFINITY;
+            bool fin = true;
+            for (int64_t w = b * prom::kSigBlockW; w < std::min<int64_t>(tr.n_wav, (b + 1) * prom::kSigBlockW); ++w) {
+              const double l = pb->wavelength[w];
+              if (!(l > 0.0) || !std::isfinite(l)) fin = false;
+              lmin = std::min(lmin, l);
+              lmax = std::max(lmax, l);
+            }
+            if (!fin) continue;
+            const double tlo = smin * lmin, thi = smax * lmax;
+            // every target inside [x_0, x_{n-1}): no clamp or end rule
+            if (!(tlo >= X[0] && thi < X[n - 1])) continue;
+            prom::SigSeg& e = seg[b * n_atoms + ia];
+            if (!make_seg(tlo, thi, e)) continue;
+            if ((e.kind & 3) == 0) {
+              // no guess over the block: one per wavefront of 64 wavelengths (oversize blocks read global
+              // records per wavefront, so each wave may take its own slice and guess); m = 0: none for that wave
+              bool any = false;
+              for (int q = 0; q < prom::kSigBlockW / 64; ++q) {
+                double wl = INFINITY, wh = -INFINITY;
+                const int64_t w0 = b * prom::kSigBlockW + 64 * q;
+                for (int64_t w = w0; w < std::min<int64_t>(tr.n_wav, w0 + 64); ++w) {
+                  wl = std::min(wl, pb->wavelength[w]);
+                  wh = std::max(wh, pb->wavelength[w]);
+                }
+                prom::SigSeg& ew = seg4[(b * n_atoms + ia) * 4 + q];
+                if (wl <= wh && make_seg(smin * wl, smax * wh, ew) && (ew.kind & 3) != 0) {
+                  ew.kind = 2;   // (read from the global records; never k_seg_exact's exact mark)
+                  any = true;
+                } else {
+                  ew = prom::SigSeg{0, 0, 0, 0, 0.0, 0.0};
+                }
+              }
+              if (any) e.kind |= 8;
             }
           }
           };
@@ -930,7 +961,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
           for (auto& th : pool) th.join();
           ++ia;
         }
+        if (no_guess)
+          for (auto& e : seg) e.kind = 0;
         stg.add(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
+        stg.add(tr.sig_seg4, seg4.data(), (int64_t)seg4.size(), s);
         std::vector<int32_t> fbl;
         for (int64_t b = 0; b < nb; ++b) {
           bool lds = true;
@@ -940,10 +974,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         tr.n_sig_fb = (int32_t)fbl.size();
         if (fbl.empty()) fbl.push_back(0);
         stg.add(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
-        tr.sig_seg_ok = std::getenv("PROM_SIGMA_ROWS") == nullptr || std::atoi(std::getenv("PROM_SIGMA_ROWS")) != 0;
+        tr.sig_seg_ok = true;
         // the key is committed only after the segments have reached the device (end of this call):
-        // a set that throws later must not leave a key that a retry would reuse
-        seg_key_new = true;
+        // a set that throws later must not leave a key that a retry would reuse (validation segments never)
+        seg_key_new = !no_guess;
         new_key_sh = std::move(key_sh);
         new_key_gen = std::move(key_gen);
       }
@@ -953,8 +987,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     // has non-finite values or |a| is too large for D <= 14
     tr.sig_deg = 0;
     {
+      // PROM_SIG_POLY=0, and PROM_SIGMA_ROWS=0 (per-target directory lookups: numpy.interp + exp10 everywhere)
       const char* e = std::getenv("PROM_SIG_POLY");
-      bool fin = !(e && std::atoi(e) == 0);
+      const char* er = std::getenv("PROM_SIGMA_ROWS");
+      bool fin = !(e && std::atoi(e) == 0) && !(er && std::atoi(er) == 0);
       double am = 0.0;
       for (const auto& t : tr.terms) {
         if (t.is_molecule) continue;

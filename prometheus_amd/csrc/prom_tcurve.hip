@@ -419,6 +419,7 @@ __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h
 template <int NSIG, int D, bool MG, int R, bool UNI>
 __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
                                                      int64_t n_wav, int32_t n_rows, const SigSeg* __restrict__ seg,
+                                                     const SigSeg* __restrict__ seg4,
                                                      const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
                                                      int32_t n_rc, int32_t rf, const TcArgs ta) {
   static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per workgroup");
@@ -544,20 +545,27 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const 
     };
     const int32_t ncap = UNI ? 1 : rcap;
     if (!lds_ok) {
-      if ((sg.kind & 3) > 0) {
+      // a block without a guess may have one per wavefront (kind & 8: the wave's own slice, global records)
+      SigSeg sgw = sg;
+      if ((sg.kind & 3) == 0 && (sg.kind & 8)) {
+        const SigSeg sub = seg4[((int64_t)wb * NSIG + s) * 4 + (tid >> 6)];
+        if (sub.m > 0) sgw = sub;
+      }
+      if ((sgw.kind & 3) > 0) {
+        const bool exact = (sgw.kind & 4) != 0;
         constexpr int G = NT < 4 ? NT : 4;
-        const double4* __restrict__ rr = tb.rec + sg.lo;
+        const double4* __restrict__ rr = tb.rec + sgw.lo;
 #pragma unroll
         for (int r0g = 0; r0g < NT; r0g += G) {
           if (r0g >= ncap) break;
           double4 q[G];
 #pragma unroll
-          for (int jj = 0; jj < G; ++jj) q[jj] = rr[seg_guess(tt[r0g + jj], sg.xs, sg.inv, sg.m)];
+          for (int jj = 0; jj < G; ++jj) q[jj] = rr[seg_guess(tt[r0g + jj], sgw.xs, sgw.inv, sgw.m)];
           if (!exact) {
 #pragma unroll
             for (int jj = 0; jj < G; ++jj) {
               const double t = tt[r0g + jj];
-              const int32_t g = seg_guess(t, sg.xs, sg.inv, sg.m);
+              const int32_t g = seg_guess(t, sgw.xs, sgw.inv, sgw.m);
               const int32_t k = t < q[jj].x ? g - 1 : (t >= q[jj].w ? g + 1 : g);
               if (k != g) q[jj] = rr[k];
             }
@@ -726,11 +734,12 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   const SigTabs4& tabv = tr.sigtab_v;
   const double* wav = tr.wav.as<double>();
   const SigSeg* seg = tr.sig_seg.as<SigSeg>();
+  const SigSeg* seg4 = tr.sig_seg4.as<SigSeg>();
   const int32_t* fb = tr.sig_fb.as<int32_t>();
   PROM_REQUIRE(msp || nsig == 1, "transmission curves: one effective absorber only");
 #define PROM_TCK(NS, DG, MGV, RV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV>), dim3(nb), dim3(kBlock), 0, s, ev_sig0, ev_sig1, 0, tabv, \
-                        pc, wav, n_wav, n_rows, seg, fb, n_fb, n_blk, n_rc, RF, ta)
+                        pc, wav, n_wav, n_rows, seg, seg4, fb, n_fb, n_blk, n_rc, RF, ta)
 #define PROM_TCR(NS, DG, MGV)                                       \
   do {                                                              \
     if (uni) PROM_TCK(NS, DG, MGV, 8, true);                        \

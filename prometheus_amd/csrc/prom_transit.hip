@@ -2224,7 +2224,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     const unsigned chord_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
     // resampling workgroups: 256 wavelengths x one row each, rounded up to a multiple of 8 (XCD order)
     // orbital Doppler shift with sigma segments: the rows come from their own kernel (k_sigma_rows)
-    const bool rows_seg = pre_sigma && !tr.uniform_shift && tr.sig_seg_ok;   // (one row per phase, even one phase)
+    const bool rows_seg = pre_sigma && tr.sig_seg_ok;   // (one row per phase, or one shared row without Doppler shift)
     const bool sig_fork = rows_seg && rs.aux && rs.ev_fork && rs.ev_join;
     const unsigned sig_blocks = (pre_sigma && !rows_seg) ? (((unsigned)sig_rows * grid_for(tr.n_wav) + 7u) & ~7u) : 0u;
     const unsigned col_blocks = (pre_sigma && !rows_seg) ? ((chord_blocks + 7u) & ~7u) + sig_blocks : chord_blocks;
@@ -2246,11 +2246,10 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     if (rows_seg && sig_first && !sig_after_order) {
       sigma_rows();
     }
-    if (!pre_sigma || rows_seg) { PROM_COLS_L(0) }
-    else if (nsig == 1) { PROM_COLS_L(1) }
-    else if (nsig == 2) { PROM_COLS_L(2) }
-    else if (nsig == 3) { PROM_COLS_L(3) }
-    else { PROM_COLS_L(4) }
+    // (the resampled rows always come from the row kernels: sigma segments are built for 1 to 4 species, and
+    // pre_sigma implies at most kWinMaxSpecies = 4)
+    PROM_REQUIRE(!pre_sigma || rows_seg, "transit: resampled rows need sigma segments");
+    PROM_COLS_L(0)
     PROM_HIP(hipGetLastError());
     if (rows_seg && !sig_first) sigma_rows();
     ev0 = nullptr;

@@ -34,7 +34,8 @@ for it in range(3):
     dev.transit_run()
     dev.synchronize()
 rd(buf, N, 0)
-a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(-1, 4)
+# (k_sigma_tc's records: the first 2^19 entries; k_tc_build's stage stamps follow, tools/trace_tcb.py)
+a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)[:1 << 19].reshape(-1, 4)
 a = a[a[:, 1] > 0]
 t0 = a[:, 0].min()
 st, en = (a[:, 0] - t0) * 0.01, (a[:, 1] - t0) * 0.01
