@@ -14,7 +14,10 @@ from prometheus_amd import _native, configs, setupfile  # noqa: E402
 tr = setupfile.build_transit(configs.get(sys.argv[1] if len(sys.argv) > 1 else "C2"))
 dev = _native.get_device(0)
 host = tr._host_inputs()
-dev.transit_set(tr._problem(dev, host, 0, len(tr.wavelength), 0.0))
+# optional second argument k: only the first 1/k of the wavelengths (one rank's shard of a k-way split)
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+n_w = (len(tr.wavelength) // k + 255) // 256 * 256 if k > 1 else len(tr.wavelength)
+dev.transit_set(tr._problem(dev, host, 0, n_w, 0.0))
 for _ in range(5):
     dev.transit_run()
 dev.synchronize()
