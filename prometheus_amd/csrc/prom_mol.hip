@@ -7,7 +7,8 @@ namespace prom {
 // tau(c, w) = sum_atomic N_s sigma_s(w) + sum_mol dx * sum_x n_abs(c,x) sigma_m(P(c,x), T, lambda'_w)
 // (gasProperties.py:924-954).  The slot's temperature is a constant, so the T part of the trilinear
 // RegularGridInterpolator weights is folded into G once per set (k_mol_gt: g(i, w) = (1 - t_T) V[i][iT][w] +
-// t_T V[i][iT + 1][w], stored as {g(i, w), g(i, w + 1)} pairs).  Per thread (phase o, wavelength w) and slot the
+// t_T V[i][iT + 1][w], stored times 1024 log2(10) as {g(i, w), g(i, w + 1)} pairs: 10^v = 2^(y/1024) without a
+// multiply per sample).  Per thread (phase o, wavelength w) and slot the
 // lambda' bracket is walked from the previous phase's; each in-table sample (P node i, weight t_P from k_mol_prep)
 // then reads two 16-byte pairs, u_i = (1 - t_w) g(i, iw) + t_w g(i, iw + 1), u_{i+1} likewise, v = u_i + t_P
 // (u_{i+1} - u_i), and costs 10^v and an FMA.  Out-of-table samples (P, T or lambda) take the fill value, i.e.
@@ -39,7 +40,8 @@ __global__ void k_mol_gt(const double* __restrict__ Tg, int32_t n_t, double T, c
     const int64_t i = k / nw1, w = k - i * nw1;
     const double* v0 = V + (i * n_t + it) * n_w + w;
     const double* v1 = v0 + n_w;
-    G[k] = make_double2((1.0 - tt) * v0[0] + tt * v1[0], (1.0 - tt) * v0[1] + tt * v1[1]);
+    // stored as y = 1024 log2(10) v (the lookups' exponent scale: 10^v = 2^(y/1024), no multiply per sample)
+    G[k] = make_double2(((1.0 - tt) * v0[0] + tt * v1[0]) * kLog2Ten1024, ((1.0 - tt) * v0[1] + tt * v1[1]) * kLog2Ten1024);
   }
 }
 
@@ -205,9 +207,9 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
           if constexpr (!EX) {
             // 10^v = 2^(y/1024), y = v 1024 log2(10), from the LDS table (relative error ~ |v| ln10 2^-53 from the
             // argument, ~6e-15 at the table's floor)
-            e = exp2_1024(v * kLog2Ten1024, etab);
+            e = exp2_1024(v, etab);
           } else {
-            e = exp10(v);
+            e = exp2(v * 0x1p-10);   // (v is 1024 log2(10) times the table value: 2^(v/1024) = 10^value)
           }
           c[j] = (q.y * (e - q.w)) * mk;
         }

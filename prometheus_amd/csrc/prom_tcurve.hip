@@ -416,8 +416,14 @@ __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h
 // slice's linear guess is numpy's bracket (kind & 4), the degree-D Taylor e^a; oversize blocks first, reading
 // 32-byte records from the global table.  NT = R target rows with orbital Doppler shift, NT = 1 without (UNI:
 // the R phases of the workgroup share one Y per wavelength).  Then each (phase, wavelength): R = T_o(Y).
+// (build macro PROM_TC_WPE: pin the lookup kernel's waves per SIMD, for occupancy sweeps)
+#ifdef PROM_TC_WPE
+#define PROM_TC_ATTR __attribute__((amdgpu_waves_per_eu(PROM_TC_WPE, PROM_TC_WPE)))
+#else
+#define PROM_TC_ATTR
+#endif
 template <int NSIG, int D, bool MG, int R, bool UNI>
-__global__ void __launch_bounds__(kBlock) k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
+__global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
                                                      int64_t n_wav, int32_t n_rows, const SigSeg* __restrict__ seg,
                                                      const SigSeg* __restrict__ seg4,
                                                      const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
