@@ -79,7 +79,7 @@ inline int n_tail_moments(int S) { return S == 1 ? 8 : (S + 1) * (S + 2) * (S + 
 // Doppler cross-section rows: table nodes a resampling workgroup stages in LDS per species (prom_api.hip
 // sigma segments; larger slices gather from the global table).
 #ifndef PROM_SIG_SEG
-#define PROM_SIG_SEG 512
+#define PROM_SIG_SEG 416   // (LDS slice cap: 416 nodes keep a 3-species k_sigma_tc workgroup at 31 KB; r04o sweep)
 #endif
 constexpr int kSigSeg = PROM_SIG_SEG;
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)

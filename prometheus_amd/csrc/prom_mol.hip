@@ -295,6 +295,9 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
   const int64_t n_tiles = (tr.n_wav + kBlock - 1) / kBlock;
   int32_t groups = (int32_t)std::max<int64_t>(1, std::min<int64_t>(tr.n_orb, (65536 + 4 * n_tiles - 1) / (4 * n_tiles)));
   int32_t ppg = (tr.n_orb + groups - 1) / groups;
+  // equal groups: the next phase count that divides the phases (C5: 7 -> 8, four groups of 8; a short last group
+  // ends early and leaves its CUs idle: profiles/r04o_C5_ppg_sweep.txt)
+  while (ppg < tr.n_orb && tr.n_orb % ppg != 0 && ppg < 2 * ((tr.n_orb + groups - 1) / groups)) ++ppg;
   if (const char* e = std::getenv("PROM_MOL_PPG"))
     if (std::atoi(e) > 0) ppg = std::min(tr.n_orb, std::atoi(e));
   groups = (tr.n_orb + ppg - 1) / ppg;
