@@ -42,11 +42,12 @@ L = a[:, 6] & 0xffff
 ch = a[:, 5] & 0xff
 print("%s k_tc_build: %d workgroups, span %.2f us, last arrivers %d, chains with work %d" %
       (name, len(a), t[:, 4].max(), last.sum(), int((ch * 4 < np.maximum(L, 1)).sum())))
-sw = (a[:, 7] - t0) * 0.01
+sw = np.where(a[:, 7] > 0, (a[:, 7] - t0) * 0.01, np.nan)   # (early-exit chains stamp no sweep end)
 for nm, d in (("start", t[:, 0]), ("sweep (loads)", sw - t[:, 0]), ("reductions", t[:, 1] - sw),
               ("phase sums", t[:, 1] - t[:, 0]), ("node sums", t[:, 2] - t[:, 1]),
               ("hand-off", t[:, 3] - t[:, 2]), ("coefficients (last)", (t[:, 4] - t[:, 3])[last == 1]),
               ("end", t[:, 4])):
+    d = d[np.isfinite(d)]
     if len(d):
         print("  %-22s p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f" % (nm, *np.percentile(d, [10, 50, 90, 100])))
 print("  L per phase:", " ".join(str(int(x)) for x in np.unique(L)))
