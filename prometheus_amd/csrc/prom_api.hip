@@ -1137,6 +1137,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         tr.tc_parts = (int32_t)std::max<int64_t>(1, std::min<int64_t>(prom::kTcPartMax, (tr.n_pr + 299) / 300));
         if (const char* e = std::getenv("PROM_TC_PARTS"))
           if (std::atoi(e) > 0) tr.tc_parts = std::min(prom::kTcPartMax, std::atoi(e));
+        {
+          // the chords' F_out total (the disk sum's denominator, the same for every phase), in chord order
+          double fsum = 0.0;
+          for (int32_t i = 0; i < tr.n_pr; ++i) fsum += pb->chord_fout[i];
+          tr.tc_fsum = fsum;
+        }
         if (!tr.tc_const.p) {
           // c_k = sum_j f_j cm[k][j] at the nodes u_j = cos(pi (j + 1/2) / 16); node factors 2^((u_k + 1) / 2)
           std::vector<double> cc(prom::kTcD * prom::kTcD + prom::kTcD);
@@ -1158,6 +1164,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
           rs.tc_cnt.ensure(cb);
           PROM_HIP(hipMemsetAsync(rs.tc_cnt.p, 0, rs.tc_cnt.cap, s));
         }
+        rs.tc_pp.ensure(sizeof(prom::TcPart) * (size_t)std::max<int64_t>(1, n_orb * (tr.n_pr / 32)));
       }
     }
     tr.last = 0;

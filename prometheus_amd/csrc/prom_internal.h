@@ -150,6 +150,13 @@ struct SigSeg {
 };
 
 // Per molecular slot of a transit problem.
+// Per 32-chord group of one phase (k_columns8, transmission-curve path): the order-independent phase sums
+// k_tc_build needs before its node sums (max / min of the active finite columns, chord counts by class)
+struct TcPart {
+  double nmax, nmin;
+  int32_t nact, ntr, nbl, nnf;
+};
+
 struct MolSlotDev {
   const double* P;       // [n_p] dyn cm^-2
   const double* T;       // [n_t]
@@ -258,6 +265,7 @@ struct RunSlot {
   DevBuf tc_tab;                            // ... [n_orb][tc_lg][kTcD] Chebyshev coefficients (k_tc_build)
   DevBuf tc_part;                           // ... per (phase, chain, part) node sums and moments
   DevBuf tc_cnt;                            // ... per (phase, chain) arrival counters (zero between runs)
+  DevBuf tc_pp;                             // ... [n_orb][n_pr / 32] TcPart from k_columns8 (n_pr % 32 == 0)
   // second stream of the slot and its fork / join events (the Doppler sigma rows run beside the column
   // and ordering kernels); set per run by prom_transit_run, null: one stream
   hipStream_t aux = nullptr;
@@ -358,7 +366,9 @@ struct TransitDev {
   bool tcurve = true;
   int32_t tc_lg = 1;
   DevBuf tc_const;                          // k_tc_build constants: Chebyshev matrix [kTcD][kTcD], node factors [kTcD]
-  int32_t tc_parts = 1;                     // chord parts per (phase, chain) of k_tc_build
+  int32_t tc_parts = 1;
+  double tc_fsum = 0.0;                     // sum of the chords' F_out (every phase's disk sum; per set)
+  bool tc_pp_ok = false;                    // this run's k_columns8 wrote the curves' phase partials (launch_transit)                     // chord parts per (phase, chain) of k_tc_build
   double tc_ybound = 0.0;
   RunSlot slot[kMaxSlots];
   // PROM_GRAPH=1: a fast-path run is one hipGraph per slot, captured at the slot's first untimed run

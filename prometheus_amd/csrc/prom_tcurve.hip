@@ -89,7 +89,8 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
                                                    double* __restrict__ hdr,
                                                    double* __restrict__ tab, double* __restrict__ part,
                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ counts,
-                                                   unsigned long long* __restrict__ evals) {
+                                                   unsigned long long* __restrict__ evals,
+                                                   const TcPart* __restrict__ tcp, double fsum_set) {
   constexpr int NW = kTcB2 / 64;
   const int32_t ch = blockIdx.x, pt = blockIdx.y, o = blockIdx.z;
   const int32_t n_ch = gridDim.x;
@@ -122,7 +123,25 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   double fs = 0.0, ts = 0.0, nmax = 0.0, nmin = __builtin_inf();
   int32_t nact = 0, ntr = 0, nbl = 0, nnf = 0;
   constexpr int U = 12;   // (one sweep up to 3072 chords)
-  for (int32_t c0 = 0; c0 < n_pr; c0 += kTcB2 * U) {
+  if (tcp) {
+    // k_columns8's partials (32 chords each: max / min / counts, order-independent) instead of a sweep over every
+    // chord; only this part's chords are loaded (to LDS, with their transparent F_out sum: the phase's comes from the
+    // parts in part order); the F_out total is the set's
+    const int32_t n_g = n_pr / 32;
+    for (int32_t g = tid; g < n_g; g += kTcB2) {
+      const TcPart v = tcp[(int64_t)o * n_g + g];
+      nmax = v.nmax > nmax ? v.nmax : nmax;
+      nmin = v.nmin < nmin ? v.nmin : nmin;
+      nact += v.nact; ntr += v.ntr; nbl += v.nbl; nnf += v.nnf;
+    }
+    for (int32_t c = c_lo + tid; c < c_hi; c += kTcB2) {
+      const int32_t f = fl[c];
+      const double fo = fout[c], N = nc[c];
+      if (in_lds) spart[c - c_lo] = f == 0 ? make_double2(fo, N) : make_double2(0.0, 0.0);
+      ts += f == 1 ? fo : 0.0;
+    }
+  }
+  for (int32_t c0 = 0; !tcp && c0 < n_pr; c0 += kTcB2 * U) {
     int32_t f[U];
     double fo[U], N[U];
 #pragma unroll
@@ -170,7 +189,7 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
     si[0][wid] = nact; si[1][wid] = ntr; si[2][wid] = nbl; si[3][wid] = nnf;
   }
   __syncthreads();
-  fs = sd[0][0]; ts = sd[1][0]; nmax = sd[2][0]; nmin = sd[3][0];
+  fs = sd[0][0]; ts = sd[1][0]; nmax = sd[2][0]; nmin = sd[3][0];   // (tcp: ts is this part's)
   nact = si[0][0]; ntr = si[1][0]; nbl = si[2][0]; nnf = si[3][0];
 #pragma unroll
   for (int w = 1; w < NW; ++w) {
@@ -179,6 +198,7 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
     nmin = sd[3][w] < nmin ? sd[3][w] : nmin;
     nact += si[0][w]; ntr += si[1][w]; nbl += si[2][w]; nnf += si[3][w];
   }
+  if (tcp) fs = fsum_set;
   // table extent: octaves up to the host's bound of q = Y N_max, or up to q = 40 N_max / N_min (every chord
   // opaque beyond it), whichever comes first; lg caps it
   const bool fin = nnf == 0 && nmax > 0.0 && nact > 0;
@@ -250,6 +270,8 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
       }
     }
   }
+  // (tcp: the part's transparent F_out sum rides in the moments row, slot 6 -- summed over the parts in order)
+  if (tcp && ch == 0 && k == 6 && g == 0) mom = ts;
 #ifdef PROM_TRACE
   if (lane == 0) {
     double x = acc[0] + mom;
@@ -349,7 +371,7 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
     t[5] = -t[5] / 120.0;
     double* h = hdr + (int64_t)o * kTcHdr;
     h[kTcHNmax] = nmax;
-    h[kTcHTfrac] = ts / fs;
+    h[kTcHTfrac] = (tcp ? sf[kTcChain][6] : ts) / fs;
     h[kTcHFsum] = fs;
 #pragma unroll
     for (int e = 0; e < 6; ++e) h[kTcHT0 + e] = t[e];
@@ -699,10 +721,12 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   unsigned long long* evals = tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr;
   const int32_t n_ch = (lg + kTcChain - 1) / kTcChain;
   const int32_t n_parts = tr.tc_parts;
+  // (k_columns8 wrote the phase partials when n_pr % 32 == 0: launch_transit's col_tcp rule)
+  const TcPart* pp = tr.tc_pp_ok ? rs.tc_pp.as<TcPart>() : nullptr;
   hipExtLaunchKernelGGL(k_tc_build, dim3((unsigned)n_ch, (unsigned)n_parts, (unsigned)tr.n_orb), dim3(kTcB2), 0, s,
                         ev_tb0, ev_tb1, 0, rs.flags.as<int32_t>(), tr.cfout.as<double>(), rs.ncol.as<double>(), tr.n_pr,
                         n_parts, tr.tc_ybound, lg, tr.tc_const.as<double>(), rs.tc_hdr.as<double>(), rs.tc_tab.as<double>(), rs.tc_part.as<double>(),
-                        rs.tc_cnt.as<int32_t>(), rs.counts.as<int32_t>(), evals);
+                        rs.tc_cnt.as<int32_t>(), rs.counts.as<int32_t>(), evals, pp, tr.tc_fsum);
   PROM_HIP(hipGetLastError());
   TcArgs ta{};
   ta.hdr = rs.tc_hdr.as<double>();

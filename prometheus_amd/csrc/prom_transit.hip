@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
                                  const SigTabs4 tabv, const double* __restrict__ wav, int64_t n_wav,
                                  double* __restrict__ sig, float4* __restrict__ tq, int32_t merge_sp,
                                  double nscale_m, int32_t* __restrict__ hcnt, uint8_t* __restrict__ zfl,
-                                 int32_t sig_rows) {
+                                 int32_t sig_rows, TcPart* __restrict__ tcp) {
   if (hcnt && blockIdx.x == 0 && threadIdx.x < 2) hcnt[threadIdx.x] = 0;   // k_order's heavy-entry counters
   // Eight lanes per chord; lane j holds samples j, j + 8, ..., j + 8 (SPL - 1).  That is numpy's
   // pairwise_sum layout (loops_utils.h.src) for 8 <= n_x < 128: lane j accumulates r[j] = a[j] +
@@ -252,6 +252,7 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
     xs[k] = i < n_x ? x[i] : 0.0;
   }
   double bound = 0.0;
+  double n_last = 0.0;   // (the last term's column: the transmission-curve path has one term)
   double nv[SPL];
   int32_t cur_sc = -1;
 #pragma unroll
@@ -306,8 +307,45 @@ __global__ void __launch_bounds__(kBlock) k_columns8(const ColArgs ca, int32_t n
     const double N = blocked ? 0.0 : (0.0 + res) * delta_x;
     if (gl == 0 && valid) ncol[((int64_t)td.slot * n_orb + o) * n_pr + ip] = N;
     bound += N * sig_max[td.slot];
+    n_last = N;
   }
-  if (gl == 0 && valid) flags[c] = blocked ? 2 : ((bound <= cull) ? 1 : 0);
+  const int32_t fcls = blocked ? 2 : ((bound <= cull) ? 1 : 0);
+  if (gl == 0 && valid) flags[c] = fcls;
+  if (tcp) {
+    // transmission curves (one term, n_pr % 32 == 0: the workgroup's 32 chords belong to one phase): the group's
+    // max / min over its active finite columns and counts, folded by wave 0 (order-independent)
+    __shared__ double s_n[G];
+    __shared__ int32_t s_f[G];
+    if (gl == 0) {
+      s_n[threadIdx.x / 8] = n_last;
+      s_f[threadIdx.x / 8] = valid ? fcls : 3;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int li = threadIdx.x & (G - 1);
+      const bool own = threadIdx.x < G;
+      const int32_t f = own ? s_f[li] : 3;
+      const double n = s_n[li];
+      const bool act = f == 0, fin = __builtin_isfinite(n);
+      double mx = (act && fin) ? n : 0.0;
+      double mn = (act && fin && n > 0.0) ? n : __builtin_inf();
+      int32_t ca = act ? 1 : 0, ct = f == 1 ? 1 : 0, cb = f == 2 ? 1 : 0, cn = (act && !fin) ? 1 : 0;
+      for (int off = 32; off > 0; off >>= 1) {
+        mx = fmax(mx, __shfl_xor(mx, off, 64));
+        mn = fmin(mn, __shfl_xor(mn, off, 64));
+        ca += __shfl_xor(ca, off, 64);
+        ct += __shfl_xor(ct, off, 64);
+        cb += __shfl_xor(cb, off, 64);
+        cn += __shfl_xor(cn, off, 64);
+      }
+      const int32_t c0 = (int32_t)blockIdx.x * G;
+      if (threadIdx.x == 0 && c0 < nc) {
+        TcPart pv;
+        pv.nmax = mx; pv.nmin = mn; pv.nact = ca; pv.ntr = ct; pv.nbl = cb; pv.nnf = cn;
+        tcp[c0 / G] = pv;   // (phase c0 / n_pr, group (c0 % n_pr) / 32: consecutive)
+      }
+    }
+  }
 #ifdef PROM_TRACE
   {
     const int64_t wv = 600000 + 2 * ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
@@ -2196,7 +2234,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
                      tr.moon_R.as<double>(), smax, tr.cull_tau, rs.ncol.as<double>(),                       \
                      rs.flags.as<int32_t>(), tr.sigtab_v, tr.wav.as<double>(), tr.n_wav, rs.sig.as<double>(), \
                      pre_sigma ? rs.tq.as<float4>() : nullptr, msp ? 1 : 0, tr.sigtab_m.t[0].nscale,    \
-                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, rs.zfl.as<uint8_t>(), sig_rows)
+                     (pre_sigma && tr.plan) ? rs.hcnt.as<int32_t>() : nullptr, rs.zfl.as<uint8_t>(), sig_rows, col_tcp)
 #define PROM_COLS_L(NSV)                       \
   if (tr.n_x <= 8) PROM_COLS(1, NSV);          \
   else if (tr.n_x <= 16) PROM_COLS(2, NSV);    \
@@ -2205,7 +2243,10 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
   // transmission-curve path (prom_tcurve.hip, the default for one effective absorber): k_columns8, then
   // k_tc_build -> k_sigma_tc; no ordering, windows or heavy entries
   const bool tcp = tr.tcurve && cols8 && wpath && tr.window && !tr.star && na == 1 && tr.sig_seg_ok;
+  TcPart* col_tcp = nullptr;   // the curves' phase partials (k_columns8 -> k_tc_build)
   if (tcp) {
+    if (tr.n_pr % 32 == 0 && n_terms == 1) col_tcp = rs.tc_pp.as<TcPart>();
+    tr.tc_pp_ok = col_tcp != nullptr;
     const unsigned col_blocks = (unsigned)((nc + kBlock / 8 - 1) / (kBlock / 8));
     PROM_COLS_L(0)
     PROM_HIP(hipGetLastError());
