@@ -68,6 +68,9 @@ struct OpAddI { __device__ int32_t operator()(int32_t a, int32_t b) const { retu
 // part order -- deterministic -- and writes the Chebyshev coefficients (and, chain 0, the header).
 constexpr int kTcB2 = 256;               // threads per workgroup (16 groups of 16 node threads)
 constexpr int kTcPartLds = 1024;         // a part's chords staged in LDS up to this many (16 KB)
+#ifndef PROM_TC_ILP
+#define PROM_TC_ILP 4                    // node sums: chords per iteration (build macro, for sweeps)
+#endif
 static_assert(kTcPartVals == (kTcChain + 1) * kTcD, "per part: 4 octaves' node sums, then the moments' row");
 
 __device__ __forceinline__ double exp256(double y, const double* __restrict__ tab) {
@@ -241,32 +244,49 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
       return fl[c] == 0 ? make_double2(fout[c], nc[c]) : make_double2(0.0, 0.0);
     };
     if (do_tab) {
-      // two chords per iteration (independent exps; the second is the part's zero entry past c_hi)
-      for (int32_t c = c_lo + g; c < c_hi; c += 2 * (kTcB2 / 16)) {
-        const int32_t c2 = c + kTcB2 / 16;
-        const double2 f1 = chord(c);
-        const double2 f2 = c2 < c_hi ? chord(c2) : make_double2(0.0, 0.0);
-        double e1 = exp256(f1.y * sk, etab), e2 = exp256(f2.y * sk, etab);
-        const double F1 = f1.x * inv_fs, F2 = f2.x * inv_fs;
-        acc[0] = __builtin_fma(F1, e1, acc[0]);
-        acc[0] = __builtin_fma(F2, e2, acc[0]);
+      // kTcIlp chords per iteration (independent LDS reads and exps: one wave per SIMD here, so the chains'
+      // latency is hidden only by the thread's own overlap; a chord past c_hi is the zero entry).  The adds keep
+      // the chord order c, c + 16, c + 32, ... of a one-chord loop
+      constexpr int kTcIlp = PROM_TC_ILP;
+      for (int32_t c = c_lo + g; c < c_hi; c += kTcIlp * (kTcB2 / 16)) {
+        double F[kTcIlp], e[kTcIlp];
+#pragma unroll
+        for (int u = 0; u < kTcIlp; ++u) {
+          const int32_t cu = c + u * (kTcB2 / 16);
+          const double2 f = cu < c_hi ? chord(cu) : make_double2(0.0, 0.0);
+          e[u] = exp256(f.y * sk, etab);
+          F[u] = f.x * inv_fs;
+        }
+#pragma unroll
+        for (int u = 0; u < kTcIlp; ++u) acc[0] = __builtin_fma(F[u], e[u], acc[0]);
 #pragma unroll
         for (int m = 1; m < kTcChain; ++m) {
-          e1 = e1 * e1;
-          e2 = e2 * e2;
-          acc[m] = __builtin_fma(F1, e1, acc[m]);
-          acc[m] = __builtin_fma(F2, e2, acc[m]);
+#pragma unroll
+          for (int u = 0; u < kTcIlp; ++u) {
+            e[u] = e[u] * e[u];
+            acc[m] = __builtin_fma(F[u], e[u], acc[m]);
+          }
         }
       }
     }
     if (ch == 0 && k < 6) {
       // tail moments sum F n^e (e = k)
-      for (int32_t c = c_lo + g; c < c_hi; c += kTcB2 / 16) {
-        const double2 fn = chord(c);
-        const double n = fn.y * inv_nmax;
-        double pw = fn.x * inv_fs;
-        for (int e2 = 0; e2 < k; ++e2) pw *= n;
-        mom += pw;
+      // (four chords per iteration, added in chord order)
+      for (int32_t c = c_lo + g; c < c_hi; c += 4 * (kTcB2 / 16)) {
+        double n[4], pw[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t cu = c + u * (kTcB2 / 16);
+          const double2 fn = cu < c_hi ? chord(cu) : make_double2(0.0, 0.0);
+          n[u] = fn.y * inv_nmax;
+          pw[u] = fn.x * inv_fs;
+        }
+        for (int e2 = 0; e2 < k; ++e2) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) pw[u] *= n[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mom += pw[u];
       }
     }
   }
