@@ -585,7 +585,9 @@ def main():
                      "kernels": kernels, "path": dict(path or {}, ms_per_step=ms_step),
                      "tau_ms_pipelined_loop": tau_ms_loop, "tau_ms_hip_events": tau_ms_events,
                      "chord_lambda_evals": cle, "fused_sigma": fused},
-        "stage_ms_single_run": {"columns_order": st["ms_density"], "tau": st["ms_tau"], "total": st["ms_total"]},
+        "stage_ms_single_run": {"columns_order": st["ms_density"], "tau": st["ms_tau"], "total": st["ms_total"],
+                                "note": "the first run, instrumented (evaluation counters on: C5's per-sample "
+                                        "counters dominate); single_run_ms is the uninstrumented latency"},
         "single_run_ms": single_run_ms,
         "chords": {"active": st["active_chords"], "transparent": st["transparent_chords"],
                    "blocked": st["blocked_chords"], "integrated_records": st["tau_records"]},
