@@ -861,6 +861,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
         std::vector<prom::SigSeg> seg(nb * n_atoms, prom::SigSeg{0, 0, 0, 0, 0.0, 0.0});
         std::vector<prom::SigSeg> seg4(nb * n_atoms * 4, prom::SigSeg{0, 0, 0, 0, 0.0, 0.0});   // per wavefront
+        // bucket directories of blocks without a linear guess (their SigSeg appended to seg4 at the end, the
+        // buckets in sig_dir); PROM_SEG_DIR=0 turns them off, for comparisons
+        std::vector<prom::SigSeg> segr;
+        std::vector<int32_t> sdir;
+        std::mutex segr_mu;
+        const char* e_sd = std::getenv("PROM_SEG_DIR");
+        const bool use_dir = !(e_sd && std::atoi(e_sd) == 0);
         int32_t ia = 0;
         for (const auto& t : tr.terms) {
           if (t.is_molecule) continue;
@@ -950,6 +957,59 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
                 }
               }
               if (any) e.kind |= 8;
+              // a slice whose node spacing varies too much for one linear guess: a bucket directory over the
+              // slice (B uniform buckets, bucket j -> numpy's bracket at its start), verified like the linear
+              // guess (a monotone step function within one node of the bracket at both ends of every node
+              // interval); B = 4, 16, ..., 1024 times the slice's nodes (kind & 32; pad = its SigSeg in seg4 past the
+              // per-wavefront entries, whose pad is the directory's offset in sig_dir)
+              if (!use_dir) continue;
+              const int64_t lo = e.lo, m = e.m, hi = lo + m - 1;
+              const double x0 = X[lo], span = X[hi] - X[lo];
+              if (!(span > 0.0)) continue;
+              std::vector<int32_t> dv;
+              prom::SigSeg de{(int32_t)lo, 0, 32, 0, 0.0, 0.0};
+              bool okd = false;
+              for (int64_t mult = 4; !okd && mult <= 1024 && m * mult <= (1 << 22); mult *= 4) {
+                const int64_t B = m * mult;
+                const double inv = (double)B / span, b0 = -(x0 * inv);
+                if (!std::isfinite(inv) || !std::isfinite(b0)) break;
+                dv.assign(B, 0);
+                // bucket j starts at x0 + j span / B: the bracket there, by one sweep over the slice's nodes
+                int64_t k = 0;
+                for (int64_t j = 0; j < B; ++j) {
+                  const double v = x0 + span * ((double)j / (double)B);
+                  while (k < m - 2 && X[lo + k + 1] <= v) ++k;
+                  dv[j] = (int32_t)k;
+                }
+                auto gd = [&](double v) -> int64_t {
+                  const double f = std::fma(v, inv, b0);   // the device's seg_guess with m = B + 1
+                  const int64_t j = f < 0.0 ? 0 : (f >= (double)(B - 1) ? B - 1 : (int64_t)f);
+                  return dv[j];
+                };
+                okd = true;
+                for (int64_t i = lo; okd && i < hi; ++i) {
+                  if (X[i] == X[i + 1]) continue;
+                  const double a = std::max(X[i], tlo), z = std::nextafter(X[i + 1], -INFINITY);
+                  if (a > z) continue;
+                  const int64_t kk = i - lo;
+                  const int64_t ga = gd(a), gz = gd(z);
+                  if (ga < kk - 1 || ga > kk + 1 || gz < kk - 1 || gz > kk + 1) okd = false;
+                }
+                if (okd) {
+                  de.m = (int32_t)(B + 1);
+                  de.xs = b0;
+                  de.inv = inv;
+                }
+              }
+              if (okd) {
+                std::lock_guard<std::mutex> lk(segr_mu);
+                if (sdir.size() + dv.size() > ((size_t)1 << 26)) continue;   // (256 MB of directories at most)
+                de.pad = (int32_t)sdir.size();
+                e.pad = (int32_t)(seg4.size() + segr.size());
+                segr.push_back(de);
+                sdir.insert(sdir.end(), dv.begin(), dv.end());
+                e.kind |= 32;
+              }
             }
           }
           };
@@ -964,7 +1024,11 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         if (no_guess)
           for (auto& e : seg) e.kind = 0;
         stg.add(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
+        seg4.insert(seg4.end(), segr.begin(), segr.end());
         stg.add(tr.sig_seg4, seg4.data(), (int64_t)seg4.size(), s);
+        stg.add(tr.sig_dir, sdir.data(), (int64_t)sdir.size(), s);
+        if (std::getenv("PROM_DEBUG"))
+          std::fprintf(stderr, "[prom] bucket directories: %zu, %zu buckets\n", segr.size(), sdir.size());
         std::vector<int32_t> fbl;
         for (int64_t b = 0; b < nb; ++b) {
           bool lds = true;

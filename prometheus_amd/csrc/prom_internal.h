@@ -333,7 +333,9 @@ struct TransitDev {
   DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
   DevBuf mol_lst;                           // [n_orb][n_pr n_mol n_x] double4: each phase's records' in-table
                                             //     samples, one flat list (k_mol_list)
-  DevBuf sig_seg4;                          // [n_blk][n_atoms][4] per-wavefront SigSeg of blocks without a guess (kind & 8)
+  DevBuf sig_seg4;                          // [n_blk][n_atoms][4] per-wavefront SigSeg of blocks without a guess (kind & 8),
+                                            // then the bucket directories' SigSeg (kind & 32)
+  DevBuf sig_dir;                           // the bucket directories (bracket at each bucket's start, slice-relative)
   DevBuf rm_fout;                           // stellar spectrum: [n_wav] unocculted flux sum_c F(c, w) (k_rm_fout, per set)
   DevBuf mol_g;                             // every slot's MolSlotDev::G
   DevBuf mol_rend;                          // [n_orb][n_pr] int32: end of each record's samples in the list

@@ -467,7 +467,7 @@ __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h
 template <int NSIG, int D, bool MG, int R, bool UNI>
 __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
                                                      int64_t n_wav, int32_t n_rows, const SigSeg* __restrict__ seg,
-                                                     const SigSeg* __restrict__ seg4,
+                                                     const SigSeg* __restrict__ seg4, const int32_t* __restrict__ sdir,
                                                      const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
                                                      int32_t n_rc, int32_t rf, const TcArgs ta) {
   static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per workgroup");
@@ -595,6 +595,34 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
     if (!lds_ok) {
       // a block without a guess may have one per wavefront (kind & 8: the wave's own slice, global records)
       SigSeg sgw = sg;
+      if ((sg.kind & 3) == 0 && (sg.kind & 32)) {
+        // a bucket directory over the slice (kind & 32: seg4[pad] = {slice lo, buckets + 1, its offset in sdir,
+        // the linear map to buckets}): the bucket's bracket, verified on the host within one node of numpy's
+        constexpr int G = NT < 4 ? NT : 4;
+        const SigSeg dg = seg4[sg.pad];
+        const int32_t* __restrict__ dv = sdir + dg.pad;
+        const double4* __restrict__ rr = tb.rec + dg.lo;
+#pragma unroll
+        for (int r0g = 0; r0g < NT; r0g += G) {
+          if (r0g >= ncap) break;
+          int32_t gg[G];
+          double4 q[G];
+#pragma unroll
+          for (int jj = 0; jj < G; ++jj) gg[jj] = dv[seg_guess(tt[r0g + jj], dg.xs, dg.inv, dg.m)];
+#pragma unroll
+          for (int jj = 0; jj < G; ++jj) q[jj] = rr[gg[jj]];
+#pragma unroll
+          for (int jj = 0; jj < G; ++jj) {
+            const double t = tt[r0g + jj];
+            const int32_t k = t < q[jj].x ? gg[jj] - 1 : (t >= q[jj].w ? gg[jj] + 1 : gg[jj]);
+            if (k != gg[jj]) q[jj] = rr[k];
+          }
+#pragma unroll
+          for (int jj = 0; jj < G; ++jj)
+            emit(r0g + jj, MG ? chi * q[jj].y : q[jj].y, exp_taylor<D>(q[jj].z * (tt[r0g + jj] - q[jj].x), pc));
+        }
+        continue;
+      }
       if ((sg.kind & 3) == 0 && (sg.kind & 8)) {
         const SigSeg sub = seg4[((int64_t)wb * NSIG + s) * 4 + (tid >> 6)];
         if (sub.m > 0) sgw = sub;
@@ -716,7 +744,8 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
     unsigned long long kinds = 0;
     int32_t mmax = 0;
     for (int s = 0; s < NSIG; ++s) {
-      kinds |= (unsigned long long)(seg[wb * NSIG + s].kind & 7) << (3 * s);
+      const int32_t kd = seg[wb * NSIG + s].kind;   // (3: no linear guess, a bucket directory)
+      kinds |= (unsigned long long)((kd & 3) == 0 && (kd & 32) ? 3 : (kd & 7)) << (3 * s);
       mmax = seg[wb * NSIG + s].m > mmax ? seg[wb * NSIG + s].m : mmax;
     }
     tp[3] = (unsigned long long)(uint32_t)r0 | (kinds << 32) | ((unsigned long long)(mmax > 65535 ? 65535 : mmax) << 44);
@@ -785,11 +814,12 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   const double* wav = tr.wav.as<double>();
   const SigSeg* seg = tr.sig_seg.as<SigSeg>();
   const SigSeg* seg4 = tr.sig_seg4.as<SigSeg>();
+  const int32_t* sdir = tr.sig_dir.as<int32_t>();
   const int32_t* fb = tr.sig_fb.as<int32_t>();
   PROM_REQUIRE(msp || nsig == 1, "transmission curves: one effective absorber only");
 #define PROM_TCK(NS, DG, MGV, RV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV>), dim3(nb), dim3(kBlock), 0, s, ev_sig0, ev_sig1, 0, tabv, \
-                        pc, wav, n_wav, n_rows, seg, seg4, fb, n_fb, n_blk, n_rc, RF, ta)
+                        pc, wav, n_wav, n_rows, seg, seg4, sdir, fb, n_fb, n_blk, n_rc, RF, ta)
 #define PROM_TCR(NS, DG, MGV)                                       \
   do {                                                              \
     if (uni) PROM_TCK(NS, DG, MGV, 8, true);                        \

@@ -61,7 +61,10 @@ if (front == 1).any():
                                                  oct((a[i, 3] >> 32) & 0xfff), (a[i, 3] >> 44) & 0xffff) for i in idx))
     kz = np.array([any(((v >> (32 + 3 * s)) & 3) == 0 for s in range(4) if ((v >> 32) & 0xfff) >> (3 * s))
                    for v in a[:, 3]])
-    for nm, m in (("front, a species without guess", (front == 1) & kz), ("front, all guessed", (front == 1) & ~kz)):
+    kr = np.array([any(((v >> (32 + 3 * s)) & 3) == 3 for s in range(4) if ((v >> 32) & 0xfff) >> (3 * s))
+                   for v in a[:, 3]])
+    for nm, m in (("front, a species without guess", (front == 1) & kz), ("front, bucket directories", (front == 1) & kr & ~kz),
+                  ("front, all guessed per block", (front == 1) & ~kz & ~kr)):
         if m.any():
             d = en[m] - st[m]
             print("  %-34s n %5d  dur p50 %5.2f p90 %5.2f max %5.2f" % (nm, m.sum(), *np.percentile(d, [50, 90, 100])))
