@@ -958,9 +958,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
               }
               if (any) e.kind |= 8;
               // a slice whose node spacing varies too much for one linear guess: a bucket directory over the
-              // slice (B uniform buckets, bucket j -> numpy's bracket at its start), verified like the linear
-              // guess (a monotone step function within one node of the bracket at both ends of every node
-              // interval); B = 4, 16, ..., 1024 times the slice's nodes (kind & 32; pad = its SigSeg in seg4 past the
+              // slice (B uniform buckets, bucket j -> numpy's bracket at its start), verified within one node
+              // of numpy's bracket at every target of the block; B = 4, 16, ..., 1024 times the slice's nodes (kind & 32; pad = its SigSeg in seg4 past the
               // per-wavefront entries, whose pad is the directory's offset in sig_dir)
               if (!use_dir) continue;
               const int64_t lo = e.lo, m = e.m, hi = lo + m - 1;
@@ -986,14 +985,17 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
                   const int64_t j = f < 0.0 ? 0 : (f >= (double)(B - 1) ? B - 1 : (int64_t)f);
                   return dv[j];
                 };
+                // verified at the block's actual targets (every row's factor times every wavelength, the
+                // kernel's clamped rows and lanes among them; the same products as the kernel's tt[]), so
+                // node intervals no target falls in (near-coincident nodes) do not matter
                 okd = true;
-                for (int64_t i = lo; okd && i < hi; ++i) {
-                  if (X[i] == X[i + 1]) continue;
-                  const double a = std::max(X[i], tlo), z = std::nextafter(X[i + 1], -INFINITY);
-                  if (a > z) continue;
-                  const int64_t kk = i - lo;
-                  const int64_t ga = gd(a), gz = gd(z);
-                  if (ga < kk - 1 || ga > kk + 1 || gz < kk - 1 || gz > kk + 1) okd = false;
+                for (int64_t o = 0; okd && o < n_orb; ++o) {
+                  const double v = sh[t.scenario * n_orb + o];
+                  for (int64_t w = b * prom::kSigBlockW; okd && w < (b + 1) * prom::kSigBlockW; ++w) {
+                    const double tt = v * pb->wavelength[std::min<int64_t>(w, tr.n_wav - 1)];
+                    const int64_t kk = bracket(tt) - lo, g = gd(tt);
+                    if (kk < 0 || kk > m - 2 || g < kk - 1 || g > kk + 1) okd = false;
+                  }
                 }
                 if (okd) {
                   de.m = (int32_t)(B + 1);
