@@ -129,3 +129,22 @@ def test_tcurve_exp10_lookups(dev, name, monkeypatch):
     assert tr.last_stats[-1]["tau_kernel_variant"] == 81
     assert rel(R0, R) < 1e-13
     assert rel(R0, d["R"]) < R_TOL
+
+
+def test_bucket_directories(dev, monkeypatch, capfd):
+    """Oversize sigma blocks without a linear guess look their brackets up in per-block bucket directories
+    (SigSeg kind & 32, verified on the host at every target): exomoon has some (PROM_DEBUG's count) and its R
+    agrees with the directory-free lookups (PROM_SEG_DIR=0) within the path's bound and with the golden R."""
+    d = load("transit_exomoon")
+    cfg = json.loads(str(d["config"]))
+    monkeypatch.setenv("PROM_DEBUG", "1")
+    R = _transit(cfg).sumOverChords(devices=[0])
+    err = capfd.readouterr().err
+    n_dir = [int(l.split(":")[1].split(",")[0]) for l in err.splitlines() if "bucket directories" in l]
+    assert n_dir and n_dir[-1] > 0
+    monkeypatch.setenv("PROM_SEG_DIR", "0")
+    R0 = _transit(cfg).sumOverChords(devices=[0])
+    err = capfd.readouterr().err
+    assert any("bucket directories: 0," in l for l in err.splitlines())
+    assert float(np.max(np.abs(R - R0))) < TC_TOL
+    assert rel(R, d["R"]) < R_TOL
