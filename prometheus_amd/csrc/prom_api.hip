@@ -1025,6 +1025,9 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         }
         if (no_guess)
           for (auto& e : seg) e.kind = 0;
+        // (block, species) pairs left with neither a linear guess nor a directory (k_sigma_tc's front row split)
+        tr.sig_noguess = 0;
+        for (const auto& e : seg) tr.sig_noguess += (e.kind & 3) == 0 && !(e.kind & 32);
         stg.add(tr.sig_seg, seg.data(), (int64_t)seg.size(), s);
         seg4.insert(seg4.end(), segr.begin(), segr.end());
         stg.add(tr.sig_seg4, seg4.data(), (int64_t)seg4.size(), s);

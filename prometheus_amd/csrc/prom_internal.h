@@ -335,6 +335,7 @@ struct TransitDev {
                                             //     samples, one flat list (k_mol_list)
   DevBuf sig_seg4;                          // [n_blk][n_atoms][4] per-wavefront SigSeg of blocks without a guess (kind & 8),
                                             // then the bucket directories' SigSeg (kind & 32)
+  int64_t sig_noguess = 0;                  // (block, species) pairs without a guess or a directory (host count)
   DevBuf sig_dir;                           // the bucket directories (bracket at each bucket's start, slice-relative)
   DevBuf rm_fout;                           // stellar spectrum: [n_wav] unocculted flux sum_c F(c, w) (k_rm_fout, per set)
   DevBuf mol_g;                             // every slot's MolSlotDev::G

@@ -799,10 +799,16 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   const int Rmax = (nsig >= 2 || uni) ? 8 : 4;
   const int R = (uni || deg == 0) ? 8 : (n_rows == 1 ? 1 : Rmax);
   const int32_t n_rc = (n_rows + R - 1) / R;
-  // front workgroups (oversize blocks): R / 2 rows for several species, or for one species with fewer than
-  // 16384 (block, row) pairs of them (profiles/r03_sigma_rf_sweep.txt); one shared target: all R
+  // front workgroups (oversize blocks): R / 2 rows for one species with fewer than 16384 (block, row) pairs of
+  // them (profiles/r03_sigma_rf_sweep.txt), or for several species when some block has neither a linear guess
+  // nor a directory (its slow lookups spread over more workgroups); else all R (C3 with every block guessed:
+  // 34.5 -> 32.6 us, profiles/r04t_front_rows_sweep.txt); one shared target: all R
   int RF = R;
-  if (!uni && R >= 2 && (nsig >= 2 || (int64_t)tr.n_sig_fb * n_rows < 16384)) RF = R / 2;
+  if (!uni && R >= 2 && ((nsig >= 2 && tr.sig_noguess > 0) || (nsig == 1 && (int64_t)tr.n_sig_fb * n_rows < 16384)))
+    RF = R / 2;
+  // PROM_TC_RF (profiling): rows per front workgroup, 1 .. R (read once)
+  static const int rf_env = [] { const char* e = std::getenv("PROM_TC_RF"); return e ? std::atoi(e) : 0; }();
+  if (rf_env >= 1 && rf_env <= R) RF = rf_env;
   // one target row (NT == 1: no Doppler shift between the phases, or one phase): every block reads the global
   // records directly, no front of oversize blocks
   const bool direct = uni || R == 1;
