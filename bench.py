@@ -6,9 +6,11 @@
 N=1: the largest single-GPU configuration of BASELINE.json, configs[2] (C3: power-law atmosphere
 with Na I + Ca II + Mg I, orbital Doppler shift on, 351,222 wavelengths x 16 orbital phases x
 2,400 chords x 30 samples, WASP-49b).  One step = one pass of the hot path over the whole spectrum
-with all inputs resident in HBM: density + column densities + culling, sigma resample of every
-species at every phase's Doppler shift, chord ordering, and the fused tau -> exp(-tau) ->
-disk-sum -> ratio kernel (prom_transit_run).  --config C2 gives the configs[1] line.
+with all inputs resident in HBM (prom_transit_run): on the default transmission-curve path
+k_columns8 (densities, column densities, culling), k_tc_build (every phase's transmission curve
+T_o) and k_sigma_tc (sigma of the merged absorber at every phase's Doppler shift, R = T_o(Y));
+several unmerged species take the windowed path (k_order, k_tau_w / k_tau_p), molecules k_tau_mol.
+--config C2 gives the configs[1] line.
 
 N>1 (launched by torch.distributed.run, one process per GPU), sharding with no collective on the data
 path (torch.distributed carries only the timing barrier and the max-over-ranks time):
@@ -419,7 +421,7 @@ def main():
     sig_tau = tv == 7
     tcurve = tv == 8
     mol = bool(getattr(prob, "n_molecules", 0))
-    tau_kernel = "k_tau_mol" if mol else ("k_tau_p" if tv in (3, 5, 6, 7) else "k_tau_w")
+    tau_kernel = "k_tau_mol" if mol else {2: "k_tau_w", 3: "k_tau_p", 4: "k_tau_rm"}.get(tv, "k_tau")
     # k_tau_p in the pipelined loop: its span on the device clock (first workgroup start -> last workgroup end)
     tau_ms_events = float(np.mean(ms_runs[:, 2])) if len(ms_runs) else st["ms_tau"]
     dev_ms = ms_runs[:, 3][np.isfinite(ms_runs[:, 3])] if len(ms_runs) else np.zeros(0)
@@ -474,6 +476,10 @@ def main():
         rate = pow10 / (tau_ms_iso * 1e-3) if tau_ms_iso else None
         km.update(bound="fp64-exp", pow10_evals=pow10, achieved=rate, peak=2.815e12, unit="pow10/s",
                   frac=(rate / 2.815e12) if rate else None, peak_source="profiles/r02u_fp64_exp_peak.json")
+    if kms.get("sigma_tc"):
+        kms["sigma"] = kms["sigma_tc"]   # (k_sigma_tc reads the tables as the row kernels do)
+    if kms.get("tc_build"):
+        kms["order"] = kms["tc_build"]
     if kms.get("sigma"):
         # Doppler sigma rows: one row per phase and wavelength (Y for merged species, else sigma per species)
         # and their zero flags written, the wavelengths and the refined tables' nodes (x, log10 sigma) read
@@ -502,7 +508,8 @@ def main():
         col_bytes = 8 * n_orb * n_pr * prob.n_atoms + 4 * n_orb * n_pr + 8 * (3 * n_pr + n_x)
         kernels["k_columns"] = dict(hbm(col_bytes, kms["columns"]), bound="latency", ms=kms["columns"],
                                     density_evals=dens, density_evals_per_s=dens / (kms["columns"] * 1e-3))
-    for k, name in (("order", "k_tc_build" if tcurve else "k_order"), ("windows", "k_windows")):
+    order_name = "k_tc_build" if tcurve else ("k_order" if tv in (2, 3) else "k_chords")
+    for k, name in (("order", order_name), ("windows", "k_windows")):
         if kms.get(k):
             kernels[name] = {"bound": "latency", "ms": kms[k],
                              "workgroups": n_orb if (k == "order" and not tcurve) else None}

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PROM_ABI_VERSION 5
+#define PROM_ABI_VERSION 6
 
 typedef struct prom_ctx prom_ctx;
 
@@ -213,10 +213,18 @@ typedef struct prom_transit_stats {
                                   the windowed kernel evaluates only the records of each
                                   wavefront's tau window; tau_records * n_wav without windows;
                                   molecular problems add the 10^v of every in-table sample)   */
-  int32_t tau_kernel_variant;  /* tens: 1 k_tau (table exp), 2 k_tau_w, 3 k_tau_p on sigma rows, 4 k_tau_rm
-                                  (stellar spectrum), 5 / 6 k_tau_p with the Doppler sigma looked up in the
-                                  kernel (exp10 / polynomial), 7 fused Doppler rows (k_sigma_poly integrates
-                                  the light windows, k_tau_p the heavy ones); units: effective species       */
+  int32_t tau_kernel_variant;  /* which integration path the run took: tens = path, units = effective atomic
+                                  species the path's kernels see (1 when species are merged into one absorber,
+                                  0 when more than 4).  Tens (prom_transit.hip launch_transit):
+                                    0  exact chord-order validation kernel k_tau with the ocml exp
+                                       (PROM_OPT_OCML_EXP, and phases with a non-finite column);
+                                    1  k_tau with the table exp (generic path; with molecular constituents:
+                                       k_mol_list + k_tau_mol);
+                                    2  windowed integration k_tau_w (k_order windows, per-tile records);
+                                    3  planned windowed integration k_tau_p (k_order + k_windows heavy lists);
+                                    4  stellar spectrum / CLV / RM rotation k_tau_rm;
+                                    8  transmission curves, the default for one effective absorber:
+                                       k_columns8 -> k_tc_build -> k_sigma_tc (prom_tcurve.hip)          */
   int32_t tau_kernel_variant_exact_phases;  /* phases integrated on the exact (ocml) path because a
                                                column density was not finite                      */
 } prom_transit_stats;
@@ -224,10 +232,11 @@ typedef struct prom_transit_stats {
 /* Copy a problem to the device (all host arrays are read during the call). */
 int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* problem);
 /* Run the integrator on the device; R stays in device memory.  stats may be NULL (with stats the
- * call waits for the run).  Runs are asynchronous: consecutive runs of a problem on the fast path
- * (1-4 atomic species, windows on) rotate over PROM_PIPELINE (default 4) internal streams and
- * work-buffer slots, so one run's column / ordering kernels overlap earlier runs' tau kernels;
- * prom_transit_result, prom_synchronize and prom_transit_set wait for all of them. */
+ * call waits for the run).  Runs are asynchronous: consecutive runs of a problem on the atomic paths
+ * rotate over PROM_PIPELINE (default 4) internal streams and work-buffer slots, so the kernels of one run
+ * (on the default path k_columns8 -> k_tc_build -> k_sigma_tc) overlap those of the runs before it; each
+ * run is complete and independent.  prom_transit_result, prom_synchronize and prom_transit_set wait for
+ * all of them. */
 int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats);
 /* Copy R[n_orb][n_wav] (row-major) of the last run to a host buffer.  A buffer from prom_host_alloc
  * takes one DMA at the link rate; any other buffer is filled through the context's pinned staging. */
@@ -253,18 +262,24 @@ int32_t prom_transit_columns(prom_ctx* ctx, double* N_out);
 int32_t prom_transit_band_stats(prom_ctx* ctx, int32_t n_bands, const double* bounds, double* sum_out,
                                 int64_t* count_out, double* max_out);
 
-/* Per-kernel device durations of the transit path (ABI 5): n_runs runs of the current problem, one at a
+/* Per-kernel device durations of the transit path (ABI 5; ids 5 and 6 since ABI 6): n_runs runs of the current problem, one at a
  * time (one slot, no second stream; the stream waits after every run), each kernel timed by start/stop
  * events on its own dispatch packet (groups of kernels: the first start to the last stop).  ms_out[k] is
  * the mean duration in milliseconds of kernel k (prom_kernel_id), NaN when the path does not launch it.
  * What rocprofv3 --kernel-trace reports for one slot in flight; measurement aid for bench.py. */
 enum prom_kernel_id {
-  PROM_K_COLUMNS = 0,   /* column densities + culling: k_columns8 (k_ntot + k_mol_prep + k_columns)   */
-  PROM_K_SIGMA = 1,     /* Doppler cross-section rows: k_sigma_poly / k_sigma_rows                     */
-  PROM_K_ORDER = 2,     /* per-phase ordering and windows: k_order (k_chords)                          */
-  PROM_K_WINDOWS = 3,   /* tile windows and heavy-entry lists: k_windows                               */
-  PROM_K_TAU = 4,       /* the fused tau kernel: k_tau_p / k_tau_w / k_tau / k_tau_mol / k_tau_rm      */
-  PROM_K_COUNT = 5
+  PROM_K_COLUMNS = 0,   /* densities, column densities and culling: k_columns8 (atomic paths); k_ntot +
+                           k_mol_prep + k_columns (molecular and generic paths)                        */
+  PROM_K_SIGMA = 1,     /* Doppler cross-section rows of the windowed paths: k_sigma_poly / k_sigma_rows */
+  PROM_K_ORDER = 2,     /* per-phase chord ordering: k_order (windowed paths), k_chords (generic and
+                           molecular paths)                                                            */
+  PROM_K_WINDOWS = 3,   /* tile windows and heavy-entry lists: k_windows (planned windowed path)        */
+  PROM_K_TAU = 4,       /* the integration kernel: k_tau / k_tau_w / k_tau_p / k_tau_rm / k_mol_list +
+                           k_tau_mol                                                                   */
+  PROM_K_TC_BUILD = 5,  /* transmission-curve path: every phase's curve T_o, k_tc_build                 */
+  PROM_K_SIGMA_TC = 6,  /* transmission-curve path: sigma at each phase's Doppler shift and R = T_o(Y),
+                           k_sigma_tc                                                                  */
+  PROM_K_COUNT = 7      /* length of prom_transit_kernel_ms's ms_out                                   */
 };
 int32_t prom_transit_kernel_ms(prom_ctx* ctx, int32_t n_runs, double* ms_out);
 

@@ -157,6 +157,19 @@ def gen_transits():
               orbphase=sgrid.constructOrbphaseAxis(), config=np.array(json.dumps(cfg)), **tables)
 
 
+def gen_multi():
+    """Several density scenarios in one atmosphere, and atoms with a molecule in one scenario
+    (configs.multi_fixture_configs; gasProperties.py:906-954, prometheus.py:74-129)."""
+    _MOLECULAR[configs.VIS_MOLECULE] = configs.visible_molecular_table()
+    for name, cfg in configs.multi_fixture_configs().items():
+        tr, lst, sgrid = reference_transit(cfg)
+        R = tr.sumOverChords(max_memory_gb=2.0)
+        # chords are batched so that every batch holds every phase's chords only partly (np.add.at branch)
+        R_small = tr.sumOverChords(max_memory_gb=2e-3)
+        _save("multi_" + name, R=R, R_small_batches=R_small, wavelength=tr.wavelength,
+              orbphase=sgrid.constructOrbphaseAxis(), config=np.array(json.dumps(cfg)))
+
+
 def gen_stars():
     """Stellar-spectrum fixtures (gasProperties.py:1180-1219): CLV + RM rotation + a synthetic
     spectrum installed as the reference's interp1d Fstar_function (celestialBodies.py:223-235)."""
@@ -495,7 +508,9 @@ def gen_lightcurve():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["interp", "tables", "density", "grids", "molecular", "transits", "stars",
-                             "star_methods", "serpens", "tidal", "harness", "lightcurve"]
+                             "star_methods", "serpens", "tidal", "harness", "lightcurve", "multi"]
+    if "multi" in which:
+        gen_multi()
     if "interp" in which:
         gen_interp_kats()
     if "tables" in which:

@@ -63,7 +63,13 @@ class TransitProblem(C.Structure):
                 ("chord_rho", _dp), ("chord_clv", _dp), ("chord_star_shift", _dp)]
 
 
-ABI_VERSION = 5
+ABI_VERSION = 6
+# prom_kernel_id order (prom_hip.h): the keys of Device.transit_kernel_ms
+KERNEL_IDS = ("columns", "sigma", "order", "windows", "tau", "tc_build", "sigma_tc")
+# prom_transit_stats.tau_kernel_variant // 10 -> the integration path the run took (prom_hip.h)
+VARIANT_PATHS = {0: "k_tau (ocml exp, validation)", 1: "k_tau / k_tau_mol (table exp)", 2: "k_tau_w (windowed)",
+                 3: "k_tau_p (planned windows)", 4: "k_tau_rm (stellar spectrum)",
+                 8: "k_tc_build + k_sigma_tc (transmission curves)"}
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
 OPT_NO_WINDOW = 4
@@ -384,7 +390,7 @@ class Device:
         self._check(self.lib.prom_timing_end(self.h, max_runs, _d(ms), C.byref(n)), "prom_timing_end")
         return ms[:min(int(n.value), max_runs)]
 
-    KERNEL_IDS = ("columns", "sigma", "order", "windows", "tau")   # prom_kernel_id order
+    KERNEL_IDS = KERNEL_IDS
 
     def transit_kernel_ms(self, n_runs: int = 20) -> dict:
         """prom_transit_kernel_ms: mean device duration [ms] of each kernel of the current problem over

@@ -198,6 +198,60 @@ def fixture_configs():
     }
 
 
+# A seeded molecular table over the Na D region (16,900-17,050 cm^-1 = 5,866-5,917 A), so one collisional
+# scenario can carry atoms and a molecule whose opacities overlap (prometheus.py:109-119 allows any mix).
+VIS_MOLECULE = "TiO"
+
+
+def visible_molecular_table():
+    return synthetic_molecular_table(n_nu=601, nu_lo=16900., nu_hi=17050., seed=1)
+
+
+def multi_fixture_configs():
+    """Atmospheres with several density scenarios, or atoms and a molecule in one scenario, pinned by golden
+    R vectors (tests/golden/multi_*.npz).  The reference builds one scenario per ``Scenarios`` key
+    (prometheus.py:74-105) and sums their optical depths, each with its own Doppler factor (planet or moon),
+    in getLOSopticalDepth_Batch (gasProperties.py:906-954)."""
+    _, Rp, _ = _system()
+    moon_arch = {"planetName": "WASP-49b", "R_moon": 1.822e8, "a_moon": 1.44 * Rp,
+                 "starting_orbphase_moon": 0.65 * 2. * 3.141592653589793}
+    baro = {"T": 3000., "P_0": 1e4, "mu": 2.3 * _AMU}
+    # (i) barometric Na I + K I and a moon exosphere of Na I, orbital Doppler shift on: two scenarios with
+    # the planet's and the moon's Doppler factors, and chords blocked by the moon
+    baro_moon = {"Fundamentals": dict(_fund(True), ExomoonSource=True),
+                 "Scenarios": {"barometric": dict(baro), "exomoon": {"q_moon": 3.34}},
+                 "Architecture": dict(moon_arch),
+                 "Species": {"barometric": {"NaI": {"chi": 1e-6}, "KI": {"chi": 1e-6}},
+                             "exomoon": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 1e32}}},
+                 "Grids": _grids(5880e-8, 7710e-8, 5e-9, 1e-10, orbphase_steps=4, phi_steps=12, rho_steps=20)}
+    # (ii) hydrostatic Na I + a molecule in one scenario, Doppler on: atoms and a molecule in one tau
+    mixed = {"Fundamentals": _fund(True),
+             "Scenarios": {"hydrostatic": {"T": 1500., "P_0": 1e5, "mu": 2.3 * _AMU}},
+             "Architecture": {"planetName": "WASP-49b"},
+             "Species": {"hydrostatic": {"NaI": {"chi": 1e-6}, VIS_MOLECULE: {"chi": 1e-4}}},
+             "Grids": _grids(5880e-8, 5910e-8, 1e-9, 5e-11, orbphase_steps=3, phi_steps=12, rho_steps=20)}
+    # (iii) power-law atmosphere (pressure-normalised) + a Na torus, Doppler on: one Doppler factor, two
+    # absorbers with different columns per chord (thermal and torus sigma_v tables); Mg I has no line in the
+    # range (its table is the offset floor everywhere, gasProperties.py:1003-1006)
+    plaw_torus = {"Fundamentals": _fund(True),
+                  "Scenarios": {"powerLaw": {"q_esc": 6., "P_0": 1e-3, "T": 3000.},
+                                "torus": {"a_torus": 2. * Rp, "v_ej": 5. * _KMS}},
+                  "Architecture": {"planetName": "WASP-49b"},
+                  "Species": {"powerLaw": {"NaI": {"chi": 1e-6}, "CaII": {"chi": 1e-6}, "MgI": {"chi": 1e-6}},
+                              "torus": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 1e33}}},
+                  "Grids": _grids(5000e-8, 5900e-8, 5e-9, 1e-10, orbphase_steps=4, phi_steps=12, rho_steps=20)}
+    # (iv) all of it, Doppler off: barometric Na I + molecule, moon exosphere, torus (three scenarios)
+    three = {"Fundamentals": dict(_fund(False), ExomoonSource=True),
+             "Scenarios": {"barometric": dict(baro), "exomoon": {"q_moon": 3.34},
+                           "torus": {"a_torus": 2. * Rp, "v_ej": 5. * _KMS}},
+             "Architecture": dict(moon_arch),
+             "Species": {"barometric": {"NaI": {"chi": 1e-6}, VIS_MOLECULE: {"chi": 1e-5}},
+                         "exomoon": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 1e32}},
+                         "torus": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 1e33}}},
+             "Grids": _grids(5884e-8, 5902e-8, 1e-9, 5e-11, orbphase_steps=3, phi_steps=12, rho_steps=20)}
+    return {"baro_moon": baro_moon, "mixed_mol": mixed, "plaw_torus": plaw_torus, "three": three}
+
+
 def synthetic_molecular_table(n_p=22, n_t=27, n_nu=50001, nu_lo=5000., nu_hi=10000., seed=0):
     """Seeded stand-in for an ExoMol/TauREx H2O table (no network, no ExoMol data in this image):
     p [Pa] = logspace(-1, 8), t [K] = linspace(100, 3400), bin_edges [cm^-1] = linspace(nu_lo, nu_hi),

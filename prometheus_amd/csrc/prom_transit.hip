@@ -2255,8 +2255,8 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     hipEvent_t e_tb1 = ev ? (stage_events ? ev1 : ev[2]) : nullptr;
     hipEvent_t e_sg0 = (ev && stage_events) ? ev[2] : nullptr;
     hipEvent_t e_sg1 = ev ? ev[3] : nullptr;
-    launch_tcurve(s, tr, rs, nsig, msp, kp_start(tr, PROM_K_SIGMA, e_sg0), kp_stop(tr, PROM_K_SIGMA, e_sg1),
-                  kp_start(tr, PROM_K_ORDER, nullptr), kp_stop(tr, PROM_K_ORDER, e_tb1));
+    launch_tcurve(s, tr, rs, nsig, msp, kp_start(tr, PROM_K_SIGMA_TC, e_sg0), kp_stop(tr, PROM_K_SIGMA_TC, e_sg1),
+                  kp_start(tr, PROM_K_TC_BUILD, nullptr), kp_stop(tr, PROM_K_TC_BUILD, e_tb1));
     *variant = 80 + na;
     return;
   }

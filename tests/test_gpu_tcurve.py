@@ -148,3 +148,29 @@ def test_bucket_directories(dev, monkeypatch, capfd):
     assert any("bucket directories: 0," in l for l in err.splitlines())
     assert float(np.max(np.abs(R - R0))) < TC_TOL
     assert rel(R, d["R"]) < R_TOL
+
+
+def test_kernel_ms_ids_match_the_path(dev):
+    """prom_transit_kernel_ms times each kernel under the id prom_hip.h documents for it: on the transmission-
+    curve path k_columns8 (columns), k_tc_build (tc_build) and k_sigma_tc (sigma_tc) and nothing else; on the
+    molecular path k_chords (order) and k_tau_mol (tau)."""
+    from prometheus_amd import _native, gasProperties as gp
+    d = load("transit_C3r")
+    tr = _transit(json.loads(str(d["config"])))
+    host = tr._host_inputs()
+    dv = _native.get_device(0)
+    with dv.lock:
+        dv.transit_set(tr._problem(dv, host, 0, len(tr.wavelength), 0.0))
+        kms = dv.transit_kernel_ms(3)
+    assert set(kms) == set(_native.KERNEL_IDS)
+    timed = {k for k, v in kms.items() if v is not None}
+    assert timed == {"columns", "tc_build", "sigma_tc"}, kms
+    gp.register_molecular_table("H2O", O.synthetic_molecular_table(n_nu=2001))
+    d = load("transit_C5r")
+    tr = _transit(json.loads(str(d["config"])))
+    host = tr._host_inputs()
+    with dv.lock:
+        dv.transit_set(tr._problem(dv, host, 0, len(tr.wavelength), 0.0))
+        kms = dv.transit_kernel_ms(2)
+    timed = {k for k, v in kms.items() if v is not None}
+    assert timed == {"columns", "order", "tau"}, kms

@@ -31,7 +31,7 @@ def test_library_exports_header():
 def test_abi_version_and_no_device_here():
     from prometheus_amd import _native
     lib = _native.load_library()
-    assert lib.prom_abi_version() == _native.ABI_VERSION == 5
+    assert lib.prom_abi_version() == _native.ABI_VERSION == 6
     if _native.device_count() == 0:
         with pytest.raises(_native.NativeUnavailable):
             _native.Device(0)
@@ -65,3 +65,29 @@ def test_pinned_pool_argument_errors():
     assert lib.prom_host_free(None) == E_ARG
     buf = np.zeros(4)
     assert lib.prom_host_free(C.c_void_p(buf.ctypes.data)) == E_ARG   # not a pool buffer
+
+
+def test_header_documents_kernel_ids_and_variants():
+    """prom_hip.h's prom_kernel_id enum is the binding's KERNEL_IDS (in order), every tens code of
+    tau_kernel_variant the launcher can return is documented in the header, and the transmission-curve
+    launcher times k_tc_build / k_sigma_tc under their own ids."""
+    from prometheus_amd import _native
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "prom_hip.h")).read()
+    enum = hdr[hdr.index("enum prom_kernel_id {"):]
+    enum = enum[:enum.index("};")]
+    ids = re.findall(r"PROM_K_(\w+) = (\d+)", enum)
+    names = [n.lower() for n, v in ids if n != "COUNT"]
+    assert [int(v) for n, v in ids] == list(range(len(ids)))
+    assert tuple(names) == _native.KERNEL_IDS
+    doc = hdr[hdr.index("int32_t tau_kernel_variant;"):hdr.index("tau_kernel_variant_exact_phases")]
+    documented = {int(t) for t in re.findall(r"^\s+(\d)  \w", doc, re.M)}
+    assert documented == set(_native.VARIANT_PATHS)
+    src = "".join(open(os.path.join(root, "prometheus_amd", "csrc", f)).read()
+                  for f in ("prom_transit.hip", "prom_mol.hip", "prom_tcurve.hip"))
+    launched = {int(v) // 10 for v in re.findall(r"\*variant = (\d+)", src)}
+    launched |= {1, 2}   # *variant = na + (exp_mode ? (windowed ? 20 : 10) : 0)
+    assert launched <= documented, launched - documented
+    call = src[src.index("launch_tcurve(s, tr, rs"):]
+    call = call[:call.index(";")]
+    assert "PROM_K_SIGMA_TC" in call and "PROM_K_TC_BUILD" in call

@@ -130,3 +130,18 @@ def test_synthetic_star_matches_product_copy():
     a = O.synthetic_star_spectrum(5886e-8, 5890e-8)
     b = configs.synthetic_star_spectrum(5886e-8, 5890e-8)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("name", ["baro_moon", "mixed_mol", "plaw_torus", "three"])
+def test_multi_scenario_transit_depth(name):
+    """Several density scenarios (planet and moon Doppler factors) and atoms with a molecule in one
+    scenario (gasProperties.py:906-954): the oracle reproduces the reference bitwise."""
+    from prometheus_amd import configs
+    d = load("multi_" + name)
+    cfg = json.loads(str(d["config"]))
+    mol = {configs.VIS_MOLECULE: O.synthetic_molecular_table(n_nu=601, nu_lo=16900., nu_hi=17050., seed=1)}
+    wav, orb, R = O.run_setup(cfg, mol)
+    assert np.array_equal(wav, d["wavelength"])
+    assert np.array_equal(orb, d["orbphase"])
+    assert np.array_equal(d["R"], d["R_small_batches"])
+    assert np.array_equal(R, d["R"]), np.max(np.abs(R / d["R"] - 1))
