@@ -846,8 +846,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       // (validation): every block without a guess -- per-target directory lookups (sigma_of) everywhere
       const char* srows = std::getenv("PROM_SIGMA_ROWS");
       const bool no_guess = srows && std::atoi(srows) == 0;
+      // PROM_SEG_DIR=0 (comparisons): no bucket directories.  Like no_guess, such segments are neither reused nor
+      // committed as the key, so toggling the switch between sets with the same tables never measures the other
+      const char* e_sd = std::getenv("PROM_SEG_DIR");
+      const bool use_dir = !(e_sd && std::atoi(e_sd) == 0);
       const bool want_seg = true;
-      const bool seg_reuse = !no_guess && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
+      const bool seg_reuse = !no_guess && use_dir && tr.seg_key_valid && key_gen == tr.seg_key_gen &&
                              key_sh == tr.seg_key_sh && (int64_t)tr.seg_key_wav.size() == tr.n_wav &&
                              std::memcmp(tr.seg_key_wav.data(), pb->wavelength, sizeof(double) * tr.n_wav) == 0;
       // reused segments stay valid only if this set completes; a throw below must not leave the key
@@ -866,8 +870,6 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         std::vector<prom::SigSeg> segr;
         std::vector<int32_t> sdir;
         std::mutex segr_mu;
-        const char* e_sd = std::getenv("PROM_SEG_DIR");
-        const bool use_dir = !(e_sd && std::atoi(e_sd) == 0);
         int32_t ia = 0;
         for (const auto& t : tr.terms) {
           if (t.is_molecule) continue;
@@ -1046,7 +1048,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         tr.sig_seg_ok = true;
         // the key is committed only after the segments have reached the device (end of this call):
         // a set that throws later must not leave a key that a retry would reuse (validation segments never)
-        seg_key_new = !no_guess;
+        seg_key_new = !no_guess && use_dir;
         new_key_sh = std::move(key_sh);
         new_key_gen = std::move(key_gen);
       }

@@ -209,7 +209,10 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
             // argument, ~6e-15 at the table's floor)
             e = exp2_1024(v, etab);
           } else {
-            e = exp2(v * 0x1p-10);   // (v is 1024 log2(10) times the table value: 2^(v/1024) = 10^value)
+            // (v is 1024 log2(10) times the table value: 2^(v/1024) = 10^value.  The scaling of G, k_mol_gt, adds
+            // |value| ln10 2^-53 relative per sample (8e-15 at -30) next to ocml's exp2; the validation test
+            // test_transit_ocml_exp_mode checks this path against the reference's golden R at 1e-12)
+            e = exp2(v * 0x1p-10);
           }
           c[j] = (q.y * (e - q.w)) * mk;
         }

@@ -338,7 +338,10 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   } else {
     // hand-off to the last part of this (phase, chain) (MI355X_MICROARCH.md, inter-workgroup visibility, first
     // row of the sc1 table): write-through (sc1) stores, every storing wave's vmcnt(0), a barrier, one agent-scope
-    // atomic add per workgroup; the workgroup whose add comes last reads with sc1 loads after a barrier
+    // atomic add per workgroup; the workgroup whose add comes last reads with sc1 loads after a barrier.  This is
+    // the guide's measured sc1 form (global_store_dwordx2 sc1 / global_atomic_add / global_load_dwordx2 sc1 in the
+    // ISA), used in place of an agent-scope release/acquire pair: the release fence is a buffer_wbl2 sc1 of the
+    // whole XCD L2 (1.7 us clean, ~6.5 us with other runs' R rows dirty in it), per workgroup and run
     if (tid < (kTcChain + 1) * kTcD)
       __hip_atomic_store(&pp[pt * kTcPartVals + tid], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -811,7 +814,9 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   if (rf_env >= 1 && rf_env <= R) RF = rf_env;
   // one target row (NT == 1: no Doppler shift between the phases, or one phase): every block reads the global
   // records directly, no front of oversize blocks
-  const bool direct = uni || R == 1;
+  // (deg == 0: the exp10 lookups read the global arrays in every block -- k_sigma_tc's main grid takes the oversize
+  // blocks too, so no front: a front would look them up and write their R rows a second time)
+  const bool direct = uni || R == 1 || deg == 0;
   const int32_t n_fb = direct ? 0 : tr.n_sig_fb;
   const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
   const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));

@@ -610,17 +610,18 @@ def _star_lookup_table(fn) -> "LookupTable":
 
 
 def _content_fingerprint(*arrays) -> tuple:
-    """(shape, 64-bit content hash) per array: xxhash when importable, else zlib's crc32."""
+    """(shape, 64-bit content hash) per array: xxhash's xxh3_64 when importable, else blake2b with an 8-byte
+    digest."""
     try:
         import xxhash
 
         def h(b):
             return xxhash.xxh3_64_intdigest(b)
     except ImportError:   # pragma: no cover
-        import zlib
+        import hashlib
 
         def h(b):
-            return zlib.crc32(b)
+            return hashlib.blake2b(b, digest_size=8).digest()
     return tuple((a.shape, h(memoryview(a).cast("B"))) for a in arrays)
 
 
