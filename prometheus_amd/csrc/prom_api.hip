@@ -917,7 +917,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
             }
             e.kind = 0;
             if (lin) {
-              e.kind = m <= prom::kSigSeg ? 1 : 2;
+              e.kind = (m <= prom::kSigSeg ? 1 : 2) | (m <= prom::tc_slice_cap(n_atoms) ? 64 : 0);
               e.xs = b0;
               e.inv = inv;
             }
@@ -952,7 +952,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
                 }
                 prom::SigSeg& ew = seg4[(b * n_atoms + ia) * 4 + q];
                 if (wl <= wh && make_seg(smin * wl, smax * wh, ew) && (ew.kind & 3) != 0) {
-                  ew.kind = 2;   // (read from the global records; never k_seg_exact's exact mark)
+                  ew.kind = 2;   // (read from the global records; never k_seg_exact's exact mark, never LDS)
                   any = true;
                 } else {
                   ew = prom::SigSeg{0, 0, 0, 0, 0.0, 0.0};
@@ -1036,15 +1036,22 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         stg.add(tr.sig_dir, sdir.data(), (int64_t)sdir.size(), s);
         if (std::getenv("PROM_DEBUG"))
           std::fprintf(stderr, "[prom] bucket directories: %zu, %zu buckets\n", segr.size(), sdir.size());
-        std::vector<int32_t> fbl;
+        std::vector<int32_t> fbl, fbt;
         for (int64_t b = 0; b < nb; ++b) {
-          bool lds = true;
-          for (int32_t a = 0; a < n_atoms; ++a) lds = lds && seg[b * n_atoms + a].kind == 1;
+          bool lds = true, ldt = true;
+          for (int32_t a = 0; a < n_atoms; ++a) {
+            lds = lds && (seg[b * n_atoms + a].kind & ~64) == 1;
+            ldt = ldt && (seg[b * n_atoms + a].kind & 64) != 0;
+          }
           if (!lds) fbl.push_back((int32_t)b);
+          if (!ldt) fbt.push_back((int32_t)b);
         }
         tr.n_sig_fb = (int32_t)fbl.size();
+        tr.n_sig_fb_tc = (int32_t)fbt.size();
         if (fbl.empty()) fbl.push_back(0);
+        if (fbt.empty()) fbt.push_back(0);
         stg.add(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
+        stg.add(tr.sig_fb_tc, fbt.data(), (int64_t)fbt.size(), s);
         tr.sig_seg_ok = true;
         // the key is committed only after the segments have reached the device (end of this call):
         // a set that throws later must not leave a key that a retry would reuse (validation segments never)
@@ -1253,10 +1260,10 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         PROM_HIP(hipStreamSynchronize(s));
         int64_t cnt[8] = {};
         for (const auto& e : hs) ++cnt[e.kind & 7];
-        std::fprintf(stderr, "[prom] sigma segments: %lld blocks x %d species, %d oversize blocks, kinds: none %lld, lds %lld, "
-                     "global %lld, lds exact %lld, global exact %lld; poly degree %d\n", (long long)nb, n_atoms,
-                     tr.n_sig_fb, (long long)cnt[0], (long long)cnt[1], (long long)cnt[2], (long long)cnt[5],
-                     (long long)cnt[6], tr.sig_deg);
+        std::fprintf(stderr, "[prom] sigma segments: %lld blocks x %d species, %d oversize blocks (%d for k_sigma_tc), kinds: "
+                     "none %lld, lds %lld, global %lld, lds exact %lld, global exact %lld; poly degree %d\n", (long long)nb,
+                     n_atoms, tr.n_sig_fb, tr.n_sig_fb_tc, (long long)cnt[0], (long long)cnt[1], (long long)cnt[2],
+                     (long long)cnt[5], (long long)cnt[6], tr.sig_deg);
       }
     }
     PROM_HIP(hipStreamSynchronize(s));

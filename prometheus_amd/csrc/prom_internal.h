@@ -82,6 +82,11 @@ inline int n_tail_moments(int S) { return S == 1 ? 8 : (S + 1) * (S + 2) * (S + 
 #define PROM_SIG_SEG 416   // (LDS slice cap: 416 nodes keep a 3-species k_sigma_tc workgroup at 31 KB; r04o sweep)
 #endif
 constexpr int kSigSeg = PROM_SIG_SEG;
+// k_sigma_tc's LDS slice cap by the number of staged species (24 bytes a node: ~24-31 KB a workgroup).  One species
+// takes slices up to 1,024 nodes: a block's targets over every phase's Doppler shift (C4x10: ~860 nodes for 256
+// wavelengths at 0.001 A under a 0.6 A Doppler spread) stay in LDS instead of the global-record front path.  Host
+// segments mark slices within the cap SigSeg kind & 64.
+constexpr int tc_slice_cap(int nsig) { return nsig <= 1 ? 1024 : (nsig == 2 ? 640 : kSigSeg); }
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
 #ifndef PROM_SIG_ROWS
 #define PROM_SIG_ROWS 8
@@ -143,7 +148,8 @@ struct ScatterDesc {
 // g(t) = clamp((int)fma(t, inv, xs), 0, m - 2) (xs holds -x_lo inv) that the host verified to be within one node of numpy's
 // bracket for every target in the slice.  kind & 3: 0 no guess (general lookup); 1 the slice fits in LDS;
 // 2 too large for LDS, the guess indexes the global records.  kind & 4 (k_seg_exact, at prom_transit_set):
-// the guess IS numpy's bracket for every target of the block's rows (one record read, no compares).
+// the guess IS numpy's bracket for every target of the block's rows (one record read, no compares).  kind & 64: a
+// guess and m <= tc_slice_cap(species of the problem) (k_sigma_tc stages the slice in LDS).
 struct SigSeg {
   int32_t lo, m, kind, pad;
   double xs, inv;
@@ -354,6 +360,8 @@ struct TransitDev {
   DevBuf sig_seg;                           // [n_wav blocks][n_atoms] SigSeg
   DevBuf sig_fb;                            // blocks with an oversize slice (m = 0 for some species)
   int32_t n_sig_fb = 0;
+  DevBuf sig_fb_tc;                         // the same for k_sigma_tc's caps (tc_slice_cap: SigSeg kind & 64)
+  int32_t n_sig_fb_tc = 0;
   bool sig_seg_ok = false;
   // polynomial sigma rows (k_sigma_poly): degree D of the e^a Taylor polynomial for this problem's tables
   // (0: the exp10 path, k_sigma_rows; PROM_SIG_POLY=0 forces it)

@@ -477,8 +477,9 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
   constexpr int NT = UNI ? 1 : R;
   // every species' slice staged at once (one load round, one barrier): per species the nodes x_k (m + 1 of them)
   // and the records' {(chi) E_k, slope_k} (24 bytes a record: four 3-species workgroups per CU)
-  constexpr int SXN = kSigSeg + 2;   // (x_0 .. x_m, padded to 16 bytes)
-  __shared__ double2 ssel[(D > 0 && NT > 1) ? NSIG * kSigSeg : 1];
+  constexpr int CAP = tc_slice_cap(NSIG);   // (nodes per species' slice, SigSeg kind & 64)
+  constexpr int SXN = CAP + 2;              // (x_0 .. x_m, padded to 16 bytes)
+  __shared__ double2 ssel[(D > 0 && NT > 1) ? NSIG * CAP : 1];
   __shared__ double ssx[(D > 0 && NT > 1) ? NSIG * SXN : 1];
   const int tid = threadIdx.x;
   const int32_t RF = rf;
@@ -506,7 +507,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
       lds_ok = false;
     } else {
 #pragma unroll
-      for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 3) == 1;
+      for (int s = 0; s < NSIG; ++s) lds_ok = lds_ok && (seg[wb * NSIG + s].kind & 64) != 0;
       if (!lds_ok) return;   // (a front workgroup's)
     }
   }
@@ -541,30 +542,30 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
   double choff = 0.0;
   if constexpr (D > 0 && NT > 1) {
     if (lds_ok) {
-      // each thread: records tid and tid + 256 of every species' slice (m <= kSigSeg = 512), all loads in flight
-      // before the first LDS write
-      double4 qa[NSIG], qb[NSIG];
+      // each thread: records tid, tid + 256, ... of every species' slice (m <= CAP), all loads in flight before the
+      // first LDS write
+      constexpr int NQ = (CAP + kBlock - 1) / kBlock;
+      double4 q[NSIG][NQ];
 #pragma unroll
       for (int s = 0; s < NSIG; ++s) {
         const double4* __restrict__ rr = tabv.t[s].rec + sgs[s].lo;
-        qa[s] = rr[tid < sgs[s].m ? tid : 0];
-        qb[s] = rr[tid + kBlock < sgs[s].m ? tid + kBlock : 0];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) q[s][j] = rr[tid + j * kBlock < sgs[s].m ? tid + j * kBlock : 0];
       }
 #pragma unroll
       for (int s = 0; s < NSIG; ++s) {
         const double chi = tabv.t[s].chi;
         double* sx = ssx + s * SXN;
-        double2* sel = ssel + s * kSigSeg;
+        double2* sel = ssel + s * CAP;
         const int32_t m = sgs[s].m;
-        if (tid < m) {
-          sx[tid] = qa[s].x;
-          sel[tid] = make_double2(MG ? chi * qa[s].y : qa[s].y, qa[s].z);
-          if (tid == m - 1) sx[m] = qa[s].w;   // the last record's upper node
-        }
-        if (tid + kBlock < m) {
-          sx[tid + kBlock] = qb[s].x;
-          sel[tid + kBlock] = make_double2(MG ? chi * qb[s].y : qb[s].y, qb[s].z);
-          if (tid + kBlock == m - 1) sx[m] = qb[s].w;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+          const int32_t i = tid + j * kBlock;
+          if (i < m) {
+            sx[i] = q[s][j].x;
+            sel[i] = make_double2(MG ? chi * q[s][j].y : q[s][j].y, q[s][j].z);
+            if (i == m - 1) sx[m] = q[s][j].w;   // the last record's upper node
+          }
         }
       }
       __syncthreads();
@@ -664,7 +665,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
       }
     } else if constexpr (D > 0 && NT > 1) {
       const double* sx = ssx + s * SXN;
-      const double2* sel = ssel + s * kSigSeg;
+      const double2* sel = ssel + s * CAP;
       auto lds_rows = [&](auto guard) {
         constexpr bool GD = decltype(guard)::value;
         double xk[NT];
@@ -794,12 +795,14 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   const int32_t n_rows = tr.n_orb;
   const int64_t n_wav = tr.n_wav;
   const int32_t n_blk = (int32_t)grid_for(n_wav);
-  // rows per workgroup: 8 for several species or one shared target row (their lookups fill the workgroup),
-  // 4 for one species with orbital Doppler shift (more workgroups in flight), never more than the problem's
-  // (instantiated: 8 rows with one shared target; 1, 4 or 8 with orbital Doppler shift -- the guarded copy
-  // of the lookups covers workgroups with fewer rows)
+  // rows per workgroup: 8 (every species' slice staged once for 8 phases; one species with orbital Doppler shift
+  // took 4 until round 5: C4x10 0.077 -> 0.064 ms per pipelined step with 8, C4 0.0116 -> 0.0111, profiles/r05h_*),
+  // never more than the problem's (instantiated: 8 rows with one shared target; 1, 4 or 8 with orbital Doppler
+  // shift -- the guarded copy of the lookups covers workgroups with fewer rows).  PROM_TC_R1 (profiling, read once):
+  // 4 rows for one species
   const int deg = tr.sig_deg;
-  const int Rmax = (nsig >= 2 || uni) ? 8 : 4;
+  static const int r1_env = [] { const char* e = std::getenv("PROM_TC_R1"); return e ? std::atoi(e) : 0; }();
+  const int Rmax = (nsig >= 2 || uni) ? 8 : (r1_env == 4 ? 4 : 8);
   const int R = (uni || deg == 0) ? 8 : (n_rows == 1 ? 1 : Rmax);
   const int32_t n_rc = (n_rows + R - 1) / R;
   // front workgroups (oversize blocks): R / 2 rows for one species with fewer than 16384 (block, row) pairs of
@@ -807,7 +810,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   // nor a directory (its slow lookups spread over more workgroups); else all R (C3 with every block guessed:
   // 34.5 -> 32.6 us, profiles/r04t_front_rows_sweep.txt); one shared target: all R
   int RF = R;
-  if (!uni && R >= 2 && ((nsig >= 2 && tr.sig_noguess > 0) || (nsig == 1 && (int64_t)tr.n_sig_fb * n_rows < 16384)))
+  if (!uni && R >= 2 && ((nsig >= 2 && tr.sig_noguess > 0) || (nsig == 1 && (int64_t)tr.n_sig_fb_tc * n_rows < 16384)))
     RF = R / 2;
   // PROM_TC_RF (profiling): rows per front workgroup, 1 .. R (read once)
   static const int rf_env = [] { const char* e = std::getenv("PROM_TC_RF"); return e ? std::atoi(e) : 0; }();
@@ -817,7 +820,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   // (deg == 0: the exp10 lookups read the global arrays in every block -- k_sigma_tc's main grid takes the oversize
   // blocks too, so no front: a front would look them up and write their R rows a second time)
   const bool direct = uni || R == 1 || deg == 0;
-  const int32_t n_fb = direct ? 0 : tr.n_sig_fb;
+  const int32_t n_fb = direct ? 0 : tr.n_sig_fb_tc;
   const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
   const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
   const PolyCoef& pc = poly_coef();
@@ -826,7 +829,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   const SigSeg* seg = tr.sig_seg.as<SigSeg>();
   const SigSeg* seg4 = tr.sig_seg4.as<SigSeg>();
   const int32_t* sdir = tr.sig_dir.as<int32_t>();
-  const int32_t* fb = tr.sig_fb.as<int32_t>();
+  const int32_t* fb = tr.sig_fb_tc.as<int32_t>();
   PROM_REQUIRE(msp || nsig == 1, "transmission curves: one effective absorber only");
 #define PROM_TCK(NS, DG, MGV, RV, UV)                                                                         \
   hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV>), dim3(nb), dim3(kBlock), 0, s, ev_sig0, ev_sig1, 0, tabv, \
@@ -835,7 +838,8 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   do {                                                              \
     if (uni) PROM_TCK(NS, DG, MGV, 8, true);                        \
     else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false);               \
-    else PROM_TCK(NS, DG, MGV, ((NS) == 1 ? 4 : 8), false);         \
+    else if ((NS) == 1 && R == 4) PROM_TCK(NS, DG, MGV, 4, false);   \
+    else PROM_TCK(NS, DG, MGV, 8, false);                           \
   } while (0)
   // degree 8 covers every table with amax <= 0.07 (the high-resolution configs); 14 the rest (coarse tables)
 #define PROM_TCD(NS, MGV)                                                          \
