@@ -14,11 +14,14 @@ several unmerged species take the windowed path (k_order, k_tau_w / k_tau_p), mo
 
 N>1 (launched by torch.distributed.run, one process per GPU), sharding with no collective on the data
 path (torch.distributed carries only the timing barrier and the max-over-ranks time):
-  --scaling strong (default): the global spectrum is the config's grid as it stands (default config
-      C4x10, the 8-GPU workload BASELINE.json names; also C5), split into N shards along --shard-axis
-      (auto: orbital phases when they divide evenly, else contiguous wavelength ranges).
-  --scaling weak: the global spectrum is the config's grid at N-times finer resolution
-      (resolutionLow/N, resolutionHigh/N: ~N x the wavelengths); rank r integrates shard r.
+  --scaling weak (default; SURVEY.md 8e: the path partitions, every rank integrates its own part): every rank a
+      problem the size of the N = 1 workload, so value(N) / value(1) is the scaling the driver computes.
+      --weak-axis phase (default): C3 with N x 16 orbital phases over the same phase range; rank r integrates
+      phases [16 r, 16 r + 16) at all 351,222 wavelengths.  --weak-axis wavelength: the grid at N x finer
+      resolution, contiguous shard r on rank r.
+  --scaling strong: the global spectrum is the config's grid as it stands (default config C4x10, the 8-GPU
+      workload BASELINE.json names; also C4x10p64, C5), split into N shards along --shard-axis (auto: orbital
+      phases when they divide evenly, else contiguous wavelength ranges).
   --shard r/N (one process): only shard r of N of the config's grid, timed alone on one GPU -- one rank's
       work under an N-way strong split.
   --shard-axis phase: strong splits over orbital phases instead (every wavelength, phases [o0, o1)): the
@@ -57,11 +60,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default=None,
-                    help="C1..C5, C4x10 (default: C3 on one GPU; C4x10, the 8-GPU configuration BASELINE.json names, "
-                         "for N > 1)")
+                    help="C1..C5, C4x10, C4x10p64 (default: C3, for N = 1 and for the weak-scaling default of N > 1; "
+                         "C4x10, the 8-GPU configuration BASELINE.json names, with --scaling strong)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
-                    help="N > 1: strong (default; the config's grid split into N shards) or weak (the grid at N x "
-                         "finer resolution, shard r on rank r)")
+                    help="N > 1: weak (default: every rank integrates a problem the size of the config's -- see "
+                         "--weak-axis) or strong (the config's grid split into N shards)")
+    ap.add_argument("--weak-axis", choices=("phase", "wavelength"), default="phase",
+                    help="weak scaling: phase (default; the config with N x its orbital phases over the same "
+                         "orbital-phase range, rank r integrates phases [r n, (r + 1) n) at every wavelength -- "
+                         "the same wavelength grid and phase count per rank as N = 1) or wavelength (the grid at "
+                         "N x finer resolution, contiguous shard r on rank r)")
     ap.add_argument("--shard", default=None, metavar="r/N",
                     help="time only shard r of an N-way split of the config's grid (strong scaling, one process)")
     ap.add_argument("--shard-axis", choices=("wavelength", "phase", "auto"), default="auto",
@@ -82,10 +90,10 @@ def parse():
                     help="oracle sample size (default: ~10 s of reference-speed CPU work per config)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", 1))
-    if a.config is None:
-        a.config = "C4x10" if (world > 1 and a.scaling != "weak") else "C3"
     if a.scaling is None:
-        a.scaling = "strong" if world > 1 else "weak"
+        a.scaling = "weak"
+    if a.config is None:
+        a.config = "C4x10" if (world > 1 and a.scaling == "strong") else "C3"
     return a
 
 
@@ -101,13 +109,20 @@ def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
 
-def global_config(name: str, world: int, scaling: str = "weak") -> dict:
+def global_config(name: str, world: int, scaling: str = "weak", weak_axis: str = "phase") -> dict:
+    """The global problem of an N-rank run.  Weak scaling keeps every rank's work the size of the config's: over
+    phases, N x the orbital phases over the same range (orbphase_border unchanged: a finer phase sampling of the
+    same transit), each rank a contiguous run of the config's phase count; over wavelengths, N x finer
+    resolution."""
     from prometheus_amd import configs
     cfg = configs.get(name)
     if world > 1 and scaling == "weak":
         g = cfg["Grids"]
-        g["resolutionLow"] = g["resolutionLow"] / world
-        g["resolutionHigh"] = g["resolutionHigh"] / world
+        if weak_axis == "phase":
+            g["orbphase_steps"] = int(g["orbphase_steps"]) * world
+        else:
+            g["resolutionLow"] = g["resolutionLow"] / world
+            g["resolutionHigh"] = g["resolutionHigh"] / world
     return cfg
 
 
@@ -273,7 +288,7 @@ def time_runs(dev, prob, steps: int, warmup: int) -> float:
     return (time.perf_counter() - t0) / steps * 1e3
 
 
-def strong_projection(dev_id: int, names=("C4x10", "C5"), parts: int = 8):
+def strong_projection(dev_id: int, names=("C4x10", "C4x10p64", "C5"), parts: int = 8):
     """Strong scaling measured on one GPU: each configuration's full grid, then the largest
     of `parts` wavelength shards (edges on 256 wavelengths) and the largest of `parts` orbital-phase shards,
     all in the pipelined loop.  T(full) / T(shard) is the speedup `parts` GPUs give at best on that axis (no
@@ -288,7 +303,7 @@ def strong_projection(dev_id: int, names=("C4x10", "C5"), parts: int = 8):
         dev = _native.get_device(dev_id)
         host = tr._host_inputs()
         n = len(tr.wavelength)
-        steps, warm = (10, 3) if name == "C5" else (60, 10)
+        steps, warm = (10, 3) if name == "C5" else ((20, 4) if name == "C4x10p64" else (60, 10))
         t_full = time_runs(dev, tr._problem(dev, host, 0, n, 0.0), steps, warm)
         shards = sharding.split(n, parts)
         a, b = max(shards, key=lambda ab: ab[1] - ab[0])
@@ -339,7 +354,7 @@ def main():
     _native.set_default_device(dev_id)
 
     scaling = "strong" if args.shard else args.scaling
-    cfg = global_config(args.config, world, scaling)
+    cfg = global_config(args.config, world, scaling, args.weak_axis)
     cfg_name = args.config
     if any(sp not in ("NaI", "KI", "CaII", "MgI") for sc in cfg["Species"].values() for sp in sc):
         from prometheus_amd.configs import synthetic_molecular_table
@@ -359,7 +374,9 @@ def main():
     o0, o1 = 0, n_orb_global
     opts = 0
     args.shard_axis = resolve_axis(args.shard_axis, n_orb_global, sn)
-    if args.shard_axis == "phase" and (args.shard or scaling == "strong"):
+    if scaling == "weak" and world > 1 and not args.shard:
+        args.shard_axis = args.weak_axis
+    if args.shard_axis == "phase" and (args.shard or scaling == "strong" or (scaling == "weak" and world > 1)):
         w0, w1 = 0, n_wav_global
         o0, o1 = sharding.shard_for_rank(n_orb_global, sn, sr, align=1)
         if o1 <= o0:
@@ -563,6 +580,10 @@ def main():
     if args.shard:
         workload += (", shard %s: phases [%d, %d)" % (args.shard, o0, o1) if args.shard_axis == "phase"
                      else ", shard %s: wavelengths [%d, %d)" % (args.shard, w0, w1))
+    elif world > 1:
+        workload += ", %s scaling over %ss: %d global phases x %d global wavelengths, rank 0 %s" % (
+            scaling, args.shard_axis, n_orb_global, n_wav_global,
+            "phases [%d, %d)" % (o0, o1) if args.shard_axis == "phase" else "wavelengths [%d, %d)" % (w0, w1))
     result = {
         "metric": "spectrum points/sec (phase x wavelength)",
         "value": value,
@@ -580,7 +601,7 @@ def main():
                    "global_wavelengths": n_wav_global, "orbital_phases": n_orb,
                    "chords_per_phase": n_pr, "los_samples": n_x,
                    "parallelism": "%s shards x%d (no collective)" % (
-                       "phase" if (args.shard_axis == "phase" and (args.shard or scaling == "strong")) else "wavelength",
+                       "phase" if (args.shard_axis == "phase" and (args.shard or world > 1)) else "wavelength",
                        world)},
         "roofline": {"bound": dk.get("bound", "hbm"), "kernel": dom, "achieved": dk.get("achieved"),
                      "peak": dk.get("peak", HBM_PEAK_GBS), "unit": dk.get("unit", "GB/s"), "frac": dk.get("frac"),

@@ -22,11 +22,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _bench(tmp, world, config, axis="wavelength"):
-    out = os.path.join(tmp, "w%d_%s" % (world, axis))
+def _bench(tmp, world, config, axis="wavelength", scaling=("--scaling", "strong")):
+    out = os.path.join(tmp, "w%d_%s_%s" % (world, axis, "_".join(scaling) or "default"))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", str(world), "--steps", "3", "--warmup", "1", "--config", config, "--scaling", "strong",
+           "--gpus", str(world), "--steps", "3", "--warmup", "1", "--config", config, *scaling,
            "--shard-axis", axis, "--no-cpu-baseline", "--no-projection", "--dump-R", out]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
@@ -100,8 +100,8 @@ def test_phase_shard_is_full_runs_rows(config, tmp_path):
 
 
 def test_two_rank_bench_default_phase_axis(tmp_path):
-    """N > 1 defaults to strong scaling; --shard-axis auto splits the orbital phases when they divide evenly
-    (C4: 8 phases over 2 ranks): the gathered rows are the single-rank run's, bit for bit."""
+    """--scaling strong --shard-axis auto splits the orbital phases when they divide evenly (C4: 8 phases over 2
+    ranks): the gathered rows are the single-rank run's, bit for bit."""
     res1, (s1,) = _bench(str(tmp_path), 1, "C4", axis="auto")
     res2, sh = _bench(str(tmp_path), 2, "C4", axis="auto")
     assert res2["scaling"] == "strong" and res2["config"]["parallelism"].startswith("phase shards")
@@ -113,3 +113,25 @@ def test_two_rank_bench_default_phase_axis(tmp_path):
         edge = o1
     assert edge == s1[2].shape[0]
     assert np.array_equal(R, s1[2], equal_nan=True)
+
+
+def test_two_rank_weak_default_over_phases(tmp_path):
+    """N > 1 defaults to weak scaling over orbital phases: the config with N x its phases over the same phase range,
+    rank r integrating a run of the config's phase count at every wavelength.  Two ranks of C4 (2 x 8 phases): the
+    gathered rows are bitwise a single-rank run of the 16-phase problem, and value counts both ranks' points."""
+    import copy
+    res2, sh = _bench(str(tmp_path), 2, "C4", axis="auto", scaling=())
+    assert res2["scaling"] == "weak" and res2["config"]["parallelism"].startswith("phase shards")
+    assert res2["config"]["orbital_phases"] == 8 and "weak scaling over phases: 16 global phases" in \
+        res2["config"]["workload"]
+    from prometheus_amd import configs, setupfile
+    cfg = configs.get("C4")
+    cfg["Grids"]["orbphase_steps"] = 16
+    tr = setupfile.build_transit(copy.deepcopy(cfg))
+    R1 = tr.sumOverChords(devices=[0], options=0)
+    R = np.full_like(R1, np.nan)
+    for w0, w1, part, o0, o1 in sh:
+        assert w0 == 0 and w1 == R1.shape[1] and o1 - o0 == 8
+        R[o0:o1] = part
+    assert np.allclose(R, R1, rtol=1e-13, atol=0)
+    assert abs(res2["value"] * res2["ms_per_step"] * 1e-3 - 16 * R1.shape[1]) / (16 * R1.shape[1]) < 1e-9
