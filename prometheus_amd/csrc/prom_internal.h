@@ -344,6 +344,8 @@ struct TransitDev {
   int64_t sig_noguess = 0;                  // (block, species) pairs without a guess or a directory (host count)
   DevBuf sig_dir;                           // the bucket directories (bracket at each bucket's start, slice-relative)
   DevBuf rm_fout;                           // stellar spectrum: [n_wav] unocculted flux sum_c F(c, w) (k_rm_fout, per set)
+  DevBuf rm_ftab;                           // ... [n_pr][n_wav] every chord's flux F(c, w) (k_rm_fout, per set), when it
+  bool rm_ftab_ok = false;                  //     fits PROM_RM_FTAB_MB and a quarter of the free device memory
   DevBuf mol_g;                             // every slot's MolSlotDev::G
   DevBuf mol_rend;                          // [n_orb][n_pr] int32: end of each record's samples in the list
   std::vector<MolSlotDev> mslots;           // host copy

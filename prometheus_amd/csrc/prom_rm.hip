@@ -7,7 +7,7 @@ namespace prom {
 // F(c, w) = rho_c * (F_star(lambda_w / s_c) * clv_c) differs per chord AND wavelength (the Rossiter-
 // McLaughlin shift s_c moves the stellar lines across the disk), so neither the flat-star F_out
 // factorisation nor the windowed tail moments apply: every (chord, wavelength) flux is evaluated.
-// One thread per wavelength, kRmP phases per workgroup.  The unocculted flux Fout(w) = sum_c F(c, w) is a
+// One thread per wavelength, RP phases per workgroup (2, launch_tau_rm).  The unocculted flux Fout(w) = sum_c F(c, w) is a
 // per-set quantity (k_rm_fout); a run visits only the chords blocked or active at some phase of its group
 // (F once per such (chord, wavelength), shared by the group's phases) and subtracts their loss from Fout.
 // F_star(t) = 10^(f_k + slope_k (t - x_k)) is evaluated as 10^f_k * exp(ln10 slope_k (t - x_k)) on the
@@ -15,7 +15,7 @@ namespace prom {
 // rm_slices), bracketed through a slice-local bucket directory; a tile whose slice exceeds kRmStarMax
 // nodes uses the global lookup (sigma_of).  With one shift for every chord (no rotation) F_star is
 // evaluated once per wavelength.
-constexpr int kRmP = 8;            // phases per workgroup
+constexpr int kRmP = 8;            // phases per workgroup (at most; k_tau_rm's RP)
 constexpr int kRmChunk = 64;       // chords staged in LDS per sweep
 constexpr int kRmGroup = 4;        // chords whose F_star lookups are interleaved
 constexpr int kRmDir = 2 * kRmStarMax;   // slice-directory buckets (at most)
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(kBlock) k_rm_fout(const SigTabDev star, const 
                                                     const double* __restrict__ wav, int64_t n_wav,
                                                     const double* __restrict__ crho, const double* __restrict__ cclv,
                                                     const double* __restrict__ cshift, int32_t n_pr,
-                                                    double* __restrict__ fo) {
+                                                    double* __restrict__ fo, double* __restrict__ ftab) {
   __shared__ double sexp[256];
   __shared__ double sx[kRmStarMax], sF[kRmStarMax], sc[kRmStarMax];
   __shared__ int16_t sdir[kRmDir];
@@ -158,7 +158,11 @@ __global__ void __launch_bounds__(kBlock) k_rm_fout(const SigTabDev star, const 
     rm_fstar<UNISTAR>(fsg, lam, sh, st, star, fstar_uni);
 #pragma unroll
     for (int u = 0; u < kRmGroup; ++u)
-      if (c0 + u < n_pr) out += crho[c0 + u] * (fsg[u] * cclv[c0 + u]);
+      if (c0 + u < n_pr) {
+        const double F = crho[c0 + u] * (fsg[u] * cclv[c0 + u]);
+        if (ftab && w < n_wav) ftab[(int64_t)(c0 + u) * n_wav + w] = F;   // (chord-major: a run reads rows)
+        out += F;
+      }
   }
   if (w < n_wav) fo[w] = out;
 }
@@ -167,7 +171,8 @@ __global__ void __launch_bounds__(kBlock) k_rm_fout(const SigTabDev star, const 
 // chords active at o of F (1 - e^-tau) -- the reference's sum_unblocked F e^-tau with every transparent chord's
 // exact F (e^-tau == 1 to the last ulp) left inside Fout.  Only chords blocked or active at some phase of the
 // workgroup's group are visited (a 64-chord chunk is compacted by ballot), so F_star is looked up for those alone.
-template <int NSMAX, bool OCML, bool UNISTAR>
+// FT: F(c, w) read from the per-set table k_rm_fout wrote (ftab[c][w], the same value), no star-table lookups here.
+template <int NSMAX, bool OCML, bool UNISTAR, bool FT, int RP>
 __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__ tabs, int32_t na,
                                                    const SigTabDev star, const int32_t* __restrict__ slices,
                                                    const double* __restrict__ wav, int64_t n_wav,
@@ -178,25 +183,26 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
                                                    const int32_t* __restrict__ flags,
                                                    const double* __restrict__ ncol, int32_t n_pr,
                                                    int32_t n_orb, int32_t* __restrict__ counts,
-                                                   double* __restrict__ R) {
+                                                   const double* __restrict__ ftab, double* __restrict__ R) {
   __shared__ double sexp[256];
-  __shared__ double sx[kRmStarMax], sF[kRmStarMax], sc[kRmStarMax];
-  __shared__ int16_t sdir[kRmDir];
+  constexpr int SM = FT ? 1 : kRmStarMax;
+  __shared__ double sx[SM], sF[SM], sc[SM];
+  __shared__ int16_t sdir[FT ? 1 : kRmDir];
   __shared__ double sRho[kRmChunk], sClv[kRmChunk], sSh[kRmChunk];
-  __shared__ double sN[kRmP * NSMAX * kRmChunk];
+  __shared__ double sN[RP * NSMAX * kRmChunk];
   __shared__ int32_t sMask[kRmChunk], sList[kRmChunk];
-  __shared__ int32_t scnt[kRmP * 3];
+  __shared__ int32_t scnt[RP * 3];
   __shared__ int32_t s_nl;
   sexp[threadIdx.x] = kExp2TableDev[8 * threadIdx.x];   // kBlock == 256
-  const int32_t o0 = blockIdx.y * kRmP;
-  const int32_t np = n_orb - o0 < kRmP ? n_orb - o0 : kRmP;
+  const int32_t o0 = blockIdx.y * RP;
+  const int32_t np = n_orb - o0 < RP ? n_orb - o0 : RP;
   const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
   const double out = fout_w[live ? w : n_wav - 1];
   // chord counts per phase (stats), by the first workgroup of each phase group
   if (blockIdx.x == 0 && counts) {
-    if (threadIdx.x < kRmP * 3) scnt[threadIdx.x] = 0;
+    if (threadIdx.x < RP * 3) scnt[threadIdx.x] = 0;
     __syncthreads();
     for (int p = 0; p < np; ++p)
       for (int32_t i = threadIdx.x; i < n_pr; i += kBlock) {
@@ -212,19 +218,21 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
       for (int k = 3; k < kCnt; ++k) cp[k] = 0;
     }
   }
-  const RmStar st = rm_stage<UNISTAR>(star, slices, sx, sF, sc, sdir, sexp);
+  RmStar st{sx, sF, sc, sdir, sexp, 0.0, 0.0, 0, 0};
+  if constexpr (!FT) st = rm_stage<UNISTAR>(star, slices, sx, sF, sc, sdir, sexp);
+  const int64_t wr = live ? w : n_wav - 1;   // (the table column this lane reads)
   // sigma_s at each of this thread's phases (shift_o * lambda, as getLOSopticalDepth_Batch)
-  double sg[kRmP][NSMAX];
+  double sg[RP][NSMAX];
 #pragma unroll
-  for (int p = 0; p < kRmP; ++p)
+  for (int p = 0; p < RP; ++p)
 #pragma unroll
     for (int s = 0; s < NSMAX; ++s)
       sg[p][s] = (p < np && s < na) ? sigma_of(tabs[s].shift[o0 + p] * lam, tabs[s]) : 0.0;
   double fstar_uni = 0.0;
-  if constexpr (UNISTAR) fstar_uni = sigma_of(lam / cshift[0], star);
-  double loss[kRmP];
+  if constexpr (UNISTAR && !FT) fstar_uni = sigma_of(lam / cshift[0], star);
+  double loss[RP];
 #pragma unroll
-  for (int p = 0; p < kRmP; ++p) loss[p] = 0.0;
+  for (int p = 0; p < RP; ++p) loss[p] = 0.0;
   for (int32_t c0 = 0; c0 < n_pr; c0 += kRmChunk) {
     const int nch = n_pr - c0 < kRmChunk ? n_pr - c0 : kRmChunk;
     __syncthreads();
@@ -266,15 +274,20 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
         cl[u] = sList[cg + u < nl ? cg + u : nl - 1];
         sh[u] = sSh[cl[u]];
       }
-      rm_fstar<UNISTAR>(fsg, lam, sh, st, star, fstar_uni);
+      if constexpr (FT) {
+#pragma unroll
+        for (int u = 0; u < kRmGroup; ++u) fsg[u] = ftab[(int64_t)(c0 + cl[u]) * n_wav + wr];
+      } else {
+        rm_fstar<UNISTAR>(fsg, lam, sh, st, star, fstar_uni);
+      }
 #pragma unroll
       for (int u = 0; u < kRmGroup; ++u) {
         if (cg + u >= nl) break;
         const int c = cl[u];
-        const double Fc = sRho[c] * (fsg[u] * sClv[c]);
+        const double Fc = FT ? fsg[u] : sRho[c] * (fsg[u] * sClv[c]);
         const int32_t mk = __builtin_amdgcn_readfirstlane(sMask[c]);
 #pragma unroll
-        for (int p = 0; p < kRmP; ++p) {
+        for (int p = 0; p < RP; ++p) {
           if (p >= np) break;
           if ((mk >> p) & 1) {
             double tau = 0.0;
@@ -294,7 +307,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
   }
   if (live) {
 #pragma unroll
-    for (int p = 0; p < kRmP; ++p)
+    for (int p = 0; p < RP; ++p)
       if (p < np) R[(int64_t)(o0 + p) * n_wav + w] = (out - loss[p]) / out;
   }
 }
@@ -302,10 +315,21 @@ __global__ void __launch_bounds__(kBlock) k_tau_rm(const SigTabDev* __restrict__
 void launch_rm_fout(hipStream_t s, TransitDev& tr) {
   const unsigned nb = (unsigned)((tr.n_wav + kBlock - 1) / kBlock);
   tr.rm_fout.ensure(sizeof(double) * tr.n_wav);
+  // the per-chord flux table F(c, w) (a function of the chord grid, the star and the wavelengths only, like Fout):
+  // runs then read each listed chord's row instead of looking the stellar spectrum up again (C2 rotating star:
+  // 3.7 GB).  PROM_RM_FTAB_MB caps it (default 24,576; 0: off); it also stays within a quarter of the free memory
+  const double bytes = 8.0 * (double)tr.n_pr * (double)tr.n_wav;
+  static const double cap_mb = [] { const char* e = std::getenv("PROM_RM_FTAB_MB"); return e ? std::atof(e) : 24576.0; }();
+  size_t free_b = 0, total_b = 0;
+  PROM_HIP(hipMemGetInfo(&free_b, &total_b));
+  tr.rm_ftab_ok = !tr.star_uniform && bytes <= cap_mb * 1048576.0 &&
+                  bytes + (double)tr.rm_ftab.cap <= 0.25 * ((double)free_b + (double)tr.rm_ftab.cap);
+  if (tr.rm_ftab_ok) tr.rm_ftab.ensure((size_t)bytes);
+  double* ftab = tr.rm_ftab_ok ? tr.rm_ftab.as<double>() : nullptr;
 #define PROM_RMF(UV)                                                                                       \
   hipLaunchKernelGGL((k_rm_fout<UV>), dim3(nb), dim3(kBlock), 0, s, tr.star_tab, tr.rm_slices.as<int32_t>(),  \
                      tr.wav.as<double>(), tr.n_wav, tr.crho.as<double>(), tr.cclv.as<double>(),                  \
-                     tr.cshift.as<double>(), tr.n_pr, tr.rm_fout.as<double>())
+                     tr.cshift.as<double>(), tr.n_pr, tr.rm_fout.as<double>(), ftab)
   if (tr.star_uniform) PROM_RMF(true);
   else PROM_RMF(false);
 #undef PROM_RMF
@@ -314,17 +338,33 @@ void launch_rm_fout(hipStream_t s, TransitDev& tr) {
 
 void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEvent_t* ev) {
     const SigTabDev star = tr.star_tab;
-    const dim3 g((unsigned)((tr.n_wav + kBlock - 1) / kBlock), (unsigned)((tr.n_orb + kRmP - 1) / kRmP));
+    // phases per workgroup: 2.  Fewer phases hold fewer sigma values and losses in registers (8 phases: 143 VGPRs, 3
+    // waves per SIMD; 2: 4+) and list fewer chords per group (the chords blocked or active at one of its phases),
+    // at the price of reading a chord once per group it is listed in.  C2 rotating star (tools/rm_bench.py,
+    // profiles/r05m_C2_rotating_star.txt): with the flux table 1.71 / 1.22 / 0.74 / 0.81 ms at 8 / 4 / 2 / 1
+    // phases; with on-the-fly lookups 2.45 / 2.11 / 1.67 ms at 8 / 4 / 2.  PROM_RM_P (profiling): 1, 2, 4 or 8
+    static const int rp_env = [] { const char* e = std::getenv("PROM_RM_P"); return e ? std::atoi(e) : 0; }();
+    const int RPv = rp_env == 1 || rp_env == 2 || rp_env == 4 || rp_env == 8 ? rp_env : 2;
+    const dim3 g((unsigned)((tr.n_wav + kBlock - 1) / kBlock), (unsigned)((tr.n_orb + RPv - 1) / RPv));
 #define PROM_RM(NSV, OC)                                                                                \
   do {                                                                                                  \
-    if (tr.star_uniform) { PROM_RM2(NSV, OC, true); } else { PROM_RM2(NSV, OC, false); }                 \
+    if (tr.star_uniform) { PROM_RM2(NSV, OC, true, false); }                                            \
+    else if (tr.rm_ftab_ok) { PROM_RM2(NSV, OC, false, true); }                                         \
+    else { PROM_RM2(NSV, OC, false, false); }                                                           \
   } while (0)
-#define PROM_RM2(NSV, OC, UV)                                                                           \
-  hipExtLaunchKernelGGL((k_tau_rm<NSV, OC, UV>), g, dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, \
+#define PROM_RM2(NSV, OC, UV, FTV)                                                                      \
+  do {                                                                                                  \
+    if (RPv == 1) PROM_RM3(NSV, OC, UV, FTV, 1);                                                        \
+    else if (RPv == 2) PROM_RM3(NSV, OC, UV, FTV, 2);                                                   \
+    else if (RPv == 4) PROM_RM3(NSV, OC, UV, FTV, 4);                                                   \
+    else PROM_RM3(NSV, OC, UV, FTV, 8);                                                                 \
+  } while (0)
+#define PROM_RM3(NSV, OC, UV, FTV, RPV)                                                                 \
+  hipExtLaunchKernelGGL((k_tau_rm<NSV, OC, UV, FTV, RPV>), g, dim3(kBlock), 0, s, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr, 0, \
                         tr.sigtab.as<SigTabDev>(), na, star, tr.rm_slices.as<int32_t>(), tr.wav.as<double>(), \
                         tr.n_wav, tr.crho.as<double>(), tr.cclv.as<double>(), tr.cshift.as<double>(),     \
                         tr.rm_fout.as<double>(), rs.flags.as<int32_t>(), rs.ncol.as<double>(), tr.n_pr, tr.n_orb,                  \
-                        tr.count_evals ? rs.counts.as<int32_t>() : nullptr, rs.R.as<double>())
+                        tr.count_evals ? rs.counts.as<int32_t>() : nullptr, tr.rm_ftab.as<double>(), rs.R.as<double>())
 #define PROM_RM_NS(OC)                       \
   if (na <= 1) PROM_RM(1, OC);               \
   else if (na == 2) PROM_RM(2, OC);          \
@@ -335,6 +375,7 @@ void launch_tau_rm(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, hipEv
 #undef PROM_RM_NS
 #undef PROM_RM
 #undef PROM_RM2
+#undef PROM_RM3
 }
 
 }  // namespace prom
