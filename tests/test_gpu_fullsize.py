@@ -109,3 +109,21 @@ def test_full_size_c4x10_eight_shards_bitwise():
     tr = setupfile.build_transit(configs.get("C4x10"))
     R1 = tr.sumOverChords(devices=[0])
     assert np.array_equal(R1, tr.sumOverChords(devices=[0] * 8))
+
+
+@pytest.mark.parametrize("name", ["C3", "C4x10", "C4x10p64"])
+def test_full_size_tcurve_matches_exact_sums(name):
+    """The transmission-curve path (default) against the exact chord sums (every active chord's e^-tau at every
+    point, no merging, windows or curves: PROM_OPT_NO_WINDOW | PROM_OPT_NO_MERGE) over the WHOLE full-size grid,
+    where the curves' octave count and the column range N_max / N_min are largest.  Bound: the curves' tail and
+    Chebyshev truncation (a few 1e-16 per unit weight) plus rounding, tested at 1e-13 absolute; the full-size
+    grids carry 5.6e6 (C3), 1.5e7 (C4x10) and 1.2e8 (C4x10p64, 64 phases) points."""
+    from prometheus_amd import _native, configs, setupfile
+    tr = setupfile.build_transit(configs.get(name))
+    tr.collect_stats = True
+    R = tr.sumOverChords(devices=[0])
+    assert tr.last_stats[-1]["tau_kernel_variant"] // 10 == 8
+    R_ex = tr.sumOverChords(devices=[0], options=_native.OPT_NO_WINDOW | _native.OPT_NO_MERGE)
+    err = float(np.max(np.abs(R - R_ex)))
+    print("%s full size %s: |R_tc - R_exact| max %.3e" % (name, R.shape, err))
+    assert err < 1e-13
