@@ -699,17 +699,17 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     stg.add(tr.terms_dev, tr.terms.data(), (int64_t)tr.terms.size(), s);
     stg.add(tr.sigma_max_dev, tr.atom_sigma_max.data(), (int64_t)tr.atom_sigma_max.size(), s);
     {
-      // the molecular tables at each slot's temperature, {g(w), g(w + 1)} pairs (one 16-byte load per P node and
-      // sample in k_tau_mol)
+      // the molecular tables at each slot's temperature, one 32-byte bilinear record per (P interval, lambda'
+      // interval) (k_mol_gt: two 16-byte loads per sample in k_tau_mol)
       int64_t g_total = 0;
-      for (const auto& md : tr.mslots) g_total += (int64_t)md.n_p * (md.n_w - 1);
+      for (const auto& md : tr.mslots) g_total += 2 * (int64_t)std::max(md.n_p - 1, 1) * (md.n_w - 1);
       if (g_total > 0) tr.mol_g.ensure(sizeof(double2) * (size_t)g_total);
       int64_t g_off = 0;
       for (auto& md : tr.mslots) {
         md.k_B = pb->k_B > 0.0 ? pb->k_B : 1.381 * std::pow(10.0, -16);
         md.shift = tr.shift.as<double>() + (int64_t)md.scenario * n_orb;
         md.G = tr.mol_g.as<double2>() + g_off;
-        g_off += (int64_t)md.n_p * (md.n_w - 1);
+        g_off += 2 * (int64_t)std::max(md.n_p - 1, 1) * (md.n_w - 1);
         prom::launch_mol_gt(s, md);
       }
     }
@@ -1181,7 +1181,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       if (n_mol > 0) {
         tr.mol_smp.ensure(sizeof(double) * 4 * n_mol * nc * tr.n_x);
         tr.mol_nin.ensure(sizeof(int32_t) * n_mol * nc);
-        tr.mol_lst.ensure(sizeof(double) * 4 * n_mol * nc * tr.n_x);
+        tr.mol_lst.ensure(sizeof(double) * 4 * ((n_mol * tr.n_x + 1) * nc + (int64_t)prom::kMolListPad * n_orb));
         tr.mol_rend.ensure(sizeof(int32_t) * nc);
       }
       rs.flags.ensure(sizeof(int32_t) * nc);

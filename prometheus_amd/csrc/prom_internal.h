@@ -66,6 +66,7 @@ struct DevBuf {
 };
 
 constexpr int kCnt = 8;   // int32 counters per phase in TransitDev::counts
+constexpr int kMolListPad = 4;   // valid zero-weight entries after each phase's molecular sample list (k_mol_list)
 
 // Windowed integration (prom_kernels.hip, "windowed integration"): per-phase ordering limit, the
 // size of the per-phase threshold -> record-index tables, and the number of tail moments for S
@@ -178,7 +179,7 @@ struct MolSlotDev {
   const double* shift;   // [n_orb] Doppler factors of its scenario
   int32_t scenario;
   int32_t pad;
-  const double2* G;      // [n_p][n_w - 1] {g(i, w), g(i, w + 1)}: V lerped to the slot's T (k_mol_gt, per set)
+  const double2* G;      // [max(n_p - 1, 1)][n_w - 1][2] bilinear records of V lerped to the slot's T (k_mol_gt, per set)
 };
 
 // Terms and scenarios of small problems passed by value to the column kernel.
@@ -337,7 +338,7 @@ struct TransitDev {
   DevBuf mol_smp;                           // [n_mol][n_orb][n_pr][n_x] double4 {P weight, n_abs = n chi, P bracket,
                                             //     0} of the in-table samples, compacted to the front of each chord
   DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
-  DevBuf mol_lst;                           // [n_orb][n_pr n_mol n_x] double4: each phase's records' in-table
+  DevBuf mol_lst;                           // [n_orb][n_pr (n_mol n_x + 1) + kMolListPad] double4: each phase's records' in-table
                                             //     samples, one flat list (k_mol_list)
   DevBuf sig_seg4;                          // [n_blk][n_atoms][4] per-wavefront SigSeg of blocks without a guess (kind & 8),
                                             // then the bucket directories' SigSeg (kind & 32)

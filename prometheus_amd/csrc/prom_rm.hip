@@ -15,7 +15,6 @@ namespace prom {
 // rm_slices), bracketed through a slice-local bucket directory; a tile whose slice exceeds kRmStarMax
 // nodes uses the global lookup (sigma_of).  With one shift for every chord (no rotation) F_star is
 // evaluated once per wavelength.
-constexpr int kRmP = 8;            // phases per workgroup (at most; k_tau_rm's RP)
 constexpr int kRmChunk = 64;       // chords staged in LDS per sweep
 constexpr int kRmGroup = 4;        // chords whose F_star lookups are interleaved
 constexpr int kRmDir = 2 * kRmStarMax;   // slice-directory buckets (at most)
