@@ -27,7 +27,7 @@ constexpr uint32_t kMolRec = kMolBilin ? 32u : 16u;
 // k_tau_mol (one molecular slot, table exp): the G records of the workgroup's lambda' node range, all P intervals,
 // staged in LDS (double2 units; 19 KB: with the 8 KB exp table and 4 KB of bracket nodes, 5 workgroups per CU)
 constexpr int kMolStageD2 = 1216;
-constexpr int kMolStageMargin = 3;
+constexpr int kMolStageMargin = 1;
 #ifndef PROM_MOL_STAGE
 #define PROM_MOL_STAGE 1
 #endif
@@ -324,12 +324,13 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
         else acc = acc + fout[ipl[r]] * exp(-tau);
         ++r;
       };
-      constexpr int NB = EX ? 1 : 4;   // (the ocml exp10 path: one sample at a time, few registers)
-      static_assert(NB <= kMolListPad, "k_mol_list pads each phase's list by kMolListPad entries");
-      struct Qb { double4 q[NB]; };
-      for (int32_t k0 = 0; k0 < K; k0 += NB) {
+      // batches of NB samples from k0 (the ocml exp10 path: one sample at a time, few registers)
+      auto batch = [&](auto nbc, int32_t k0) {
+        constexpr int NB = decltype(nbc)::value;
+        static_assert(NB <= kMolListPad, "k_mol_list pads each phase's list by kMolListPad entries");
+        struct Qb { double4 q[NB]; };
         // the batch's entries in one scalar read (k_mol_list pads each phase's list with valid zero-weight
-        // entries: the ones past K are looked up and not added)
+        // entries: any past K are looked up and not added)
         const Qb qb = *reinterpret_cast<const Qb*>(lo + k0);
         double c[NB];
 #pragma unroll
@@ -387,17 +388,33 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
         for (int j = 0; j < NB; ++j) {
           if (k0 + j >= K) break;
           const int32_t code = (int32_t)__double_as_longlong(qb.q[j].z);
-          nsl[M1 ? 0 : (code >> 16) & 3] += (evals != nullptr && !(code & kMolEmpty)) ? 1 : 0;
           if constexpr (!EX) sm = __builtin_fma(qb.q[j].y, c[j], sm);
           else sm += c[j];
           if (code & kMolLast) finish(qb.q[j].w);
         }
+      };
+      if constexpr (EX) {
+        for (int32_t k0 = 0; k0 < K; ++k0) batch(std::integral_constant<int, 1>{}, k0);
+      } else {
+        // fours, then a pair and a single for the phase's last K mod 4 (no lookups past K)
+        int32_t k0 = 0;
+        for (; k0 + 4 <= K; k0 += 4) batch(std::integral_constant<int, 4>{}, k0);
+        if (K - k0 >= 2) {
+          batch(std::integral_constant<int, 2>{}, k0);
+          k0 += 2;
+        }
+        if (k0 < K) batch(std::integral_constant<int, 1>{}, k0);
       }
     };
     if (!EXPK || exact) samples(std::true_type{}, std::false_type{});
     else if (STG && use_st) samples(std::false_type{}, std::true_type{});
     else samples(std::false_type{}, std::false_type{});
     if (evals) {
+      // (stats runs: the phase's listed samples per slot, the zero-weight entries of empty records excluded)
+      for (int32_t k = 0; k < K; ++k) {
+        const int32_t code = (int32_t)__double_as_longlong(lo[k].z);
+        if (!(code & kMolEmpty)) nsl[(code >> 16) & 3] += 1;
+      }
 #pragma unroll
       for (int m = 0; m < 4; ++m) npow += ((inb >> m) & 1u) ? (unsigned long long)nsl[m] : 0ull;
     }
