@@ -689,6 +689,37 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     stg.add(tr.cy, pb->chord_y, tr.n_pr, s);
     stg.add(tr.cz, pb->chord_z, tr.n_pr, s);
     stg.add(tr.cfout, pb->chord_fout, tr.n_pr, s);
+    {
+      // mirror images (y, -z) of the chords, for k_mol_list's merging of equal molecular records: sorted by y,
+      // each unpaired chord with z != 0 takes the first later chord within 1e-9 of (y, -z) (relative to its
+      // radius); k_mol_list verifies the sample lists before merging anything
+      const char* mir_env = std::getenv("PROM_MOL_MIRROR");
+      const bool mir_on = !(mir_env && std::atoi(mir_env) == 0);
+      tr.mirror_h.assign((size_t)tr.n_pr, -1);
+      tr.n_mirror = 0;
+      if (mir_on && tr.n_pr <= prom::kMolMirrorMax) {
+        const double* cy = pb->chord_y;
+        const double* cz = pb->chord_z;
+        std::vector<int32_t> ord((size_t)tr.n_pr);
+        for (int32_t i = 0; i < (int32_t)tr.n_pr; ++i) ord[i] = i;
+        std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return cy[a] < cy[b] || (cy[a] == cy[b] && a < b); });
+        for (size_t a = 0; a < ord.size(); ++a) {
+          const int32_t i = ord[a];
+          if (tr.mirror_h[i] >= 0 || !(cz[i] != 0.0) || !std::isfinite(cy[i]) || !std::isfinite(cz[i])) continue;
+          const double tol = 1e-9 * std::max(std::fabs(cy[i]), std::fabs(cz[i]));
+          for (size_t b = a + 1; b < ord.size() && cy[ord[b]] - cy[i] <= tol; ++b) {
+            const int32_t j = ord[b];
+            if (tr.mirror_h[j] < 0 && std::fabs(cz[j] + cz[i]) <= tol) {
+              tr.mirror_h[i] = j;
+              tr.mirror_h[j] = i;
+              ++tr.n_mirror;
+              break;
+            }
+          }
+        }
+      }
+      stg.add(tr.mirror, tr.mirror_h.data(), tr.n_pr, s);
+    }
     stg.add(tr.x, pb->x, tr.n_x, s);
     stg.add(tr.planet_y, pb->planet_y, n_orb, s);
     stg.add(tr.moon_y, pb->moon_y, (int64_t)tr.n_moons * n_orb, s);

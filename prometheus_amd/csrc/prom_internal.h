@@ -66,6 +66,7 @@ struct DevBuf {
 };
 
 constexpr int kCnt = 8;   // int32 counters per phase in TransitDev::counts
+constexpr int kMolMirrorMax = 8192;   // chords per phase for k_mol_list's mirror merging (32 KB of LDS)
 constexpr int kMolListPad = 4;   // valid zero-weight entries after each phase's molecular sample list (k_mol_list)
 
 // Windowed integration (prom_kernels.hip, "windowed integration"): per-phase ordering limit, the
@@ -338,6 +339,9 @@ struct TransitDev {
   DevBuf mol_smp;                           // [n_mol][n_orb][n_pr][n_x] double4 {P weight, n_abs = n chi, P bracket,
                                             //     0} of the in-table samples, compacted to the front of each chord
   DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
+  DevBuf mirror;                            // [n_pr] int32: each chord's mirror image (z -> -z) or -1 (host-paired)
+  int64_t n_mirror = 0;                     // (mirror pairs; 0: none, or PROM_MOL_MIRROR=0)
+  std::vector<int32_t> mirror_h;            // (host image of mirror)
   DevBuf mol_lst;                           // [n_orb][n_pr (n_mol n_x + 1) + kMolListPad] double4: each phase's records' in-table
                                             //     samples, one flat list (k_mol_list)
   DevBuf sig_seg4;                          // [n_blk][n_atoms][4] per-wavefront SigSeg of blocks without a guess (kind & 8),

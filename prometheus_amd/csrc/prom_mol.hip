@@ -28,6 +28,10 @@ constexpr uint32_t kMolRec = kMolBilin ? 32u : 16u;
 // staged in LDS (double2 units; 19 KB: with the 8 KB exp table and 4 KB of bracket nodes, 5 workgroups per CU)
 constexpr int kMolStageD2 = 1216;
 constexpr int kMolStageMargin = 1;
+#ifndef PROM_MOL_MTOL
+#define PROM_MOL_MTOL 40
+#endif
+constexpr double kMolMirrorTol = 1.0 / (double)(1ull << PROM_MOL_MTOL);
 #ifndef PROM_MOL_STAGE
 #define PROM_MOL_STAGE 1
 #endif
@@ -435,10 +439,11 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
                                                      const int32_t* __restrict__ mnin,
                                                      const double* __restrict__ recs, int32_t n_st, int32_t n_pr,
                                                      int32_t n_orb, int32_t n_x, int64_t lst_stride,
-                                                     int32_t fold_empty, double4* __restrict__ lst,
-                                                     int32_t* __restrict__ rend) {
+                                                     int32_t fold_empty, const int32_t* __restrict__ mirror,
+                                                     double4* __restrict__ lst, int32_t* __restrict__ rend) {
   __shared__ int32_t wsum[kBlock / 64];
   __shared__ double wfe[kBlock / 64];
+  __shared__ int32_t rmap[kMolMirrorMax];   // chord -> this phase's record (mirror merging)
   const int32_t o = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int32_t n_act = counts[o * kCnt];
@@ -447,6 +452,18 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
   const bool fold = fold_empty && counts[o * kCnt + 3] == 0;
   const int64_t nc = (int64_t)n_orb * n_pr;
   double4* lo = lst + (int64_t)o * lst_stride;
+  // Mirror merging (folded phases, mirror != null: the launcher passes it for n_pr <= kMolMirrorMax): chord ip and
+  // its mirror image mirror[ip] (z -> -z, paired on the host) see the same densities about a body on the y axis, so
+  // when both are active records with equal sample lists -- every slot's in-table count, P brackets equal, P
+  // weights and n_abs within kMolMirrorTol (relative) -- their tau agree to ~2^-42 and the pair is integrated once,
+  // by the lower record with the summed weight (the bound of k_chords' column merging, R moves by < 1e-13)
+  const bool mrg = fold && mirror != nullptr;
+  if (mrg) {
+    for (int32_t ip = tid; ip < n_pr; ip += kBlock) rmap[ip] = -1;
+    __syncthreads();
+    for (int32_t r = tid; r < n_act; r += kBlock) rmap[act_ip[(int64_t)o * n_pr + r]] = r;
+    __syncthreads();
+  }
   int32_t base = 0;
   double fe_sum = 0.0;
   for (int32_t r0 = 0; r0 < n_act; r0 += kBlock) {
@@ -454,8 +471,30 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
     const int32_t ip = r < n_act ? act_ip[(int64_t)o * n_pr + r] : 0;
     int32_t cnt = 0;
     for (int32_t m = 0; m < n_mol; ++m) cnt += r < n_act ? mnin[(int64_t)m * nc + (int64_t)o * n_pr + ip] : 0;
-    const double F = r < n_act ? recs[((int64_t)o * n_pr + r) * n_st] : 0.0;
-    const int32_t len = r < n_act ? (fold ? cnt : max(cnt, 1)) : 0;
+    double F = r < n_act ? recs[((int64_t)o * n_pr + r) * n_st] : 0.0;
+    int32_t partner = -1;
+    if (mrg && r < n_act && cnt > 0) {
+      const int32_t ipp = mirror[ip];
+      const int32_t p = ipp >= 0 ? rmap[ipp] : -1;
+      if (p >= 0 && p != r) {
+        bool eq = true;
+        for (int32_t m = 0; m < n_mol && eq; ++m) {
+          const int64_t ca = (int64_t)m * nc + (int64_t)o * n_pr + ip, cb = (int64_t)m * nc + (int64_t)o * n_pr + ipp;
+          const int32_t nin = mnin[ca];
+          eq = nin == mnin[cb];
+          for (int32_t k = 0; k < nin && eq; ++k) {
+            const double4 a = msmp[ca * n_x + k], b = msmp[cb * n_x + k];
+            eq = __double_as_longlong(a.z) == __double_as_longlong(b.z) && fabs(a.x - b.x) <= kMolMirrorTol &&
+                 fabs(a.y - b.y) <= kMolMirrorTol * fmax(fabs(a.y), fabs(b.y));
+          }
+        }
+        if (eq) partner = p;
+      }
+    }
+    // (the lower record of a merged pair carries both weights, the upper one lists nothing)
+    if (partner >= 0 && r < partner) F = F + recs[((int64_t)o * n_pr + partner) * n_st];
+    const bool skip = partner >= 0 && r > partner;
+    const int32_t len = r < n_act ? (skip ? 0 : (fold ? cnt : max(cnt, 1))) : 0;
     const int32_t inc = wave_prefix<int32_t>(len, OpAdd());
     const double fe = wave_prefix<double>(fold && r < n_act && cnt == 0 ? F : 0.0, OpAdd());
     __syncthreads();
@@ -468,7 +507,7 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
       tot += wsum[w];
       fe_sum += wfe[w];
     }
-    if (r < n_act) {
+    if (r < n_act && !skip) {
       const int32_t end = pos + len;
       if (cnt == 0 && !fold)
         lo[pos++] = make_double4(0.0, 0.0, __longlong_as_double((long long)(kMolEmpty | kMolLast)), F);
@@ -484,6 +523,7 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
       }
       rend[(int64_t)o * n_pr + r] = end;
     }
+    if (r < n_act && skip) rend[(int64_t)o * n_pr + r] = pos;
     base += tot;
   }
   // kMolListPad valid entries past the list (slot 0, P bracket 0, zero weights): k_tau_mol reads its samples in
@@ -530,8 +570,9 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
     const int64_t lst_stride = (int64_t)tr.n_pr * (tr.n_mol * tr.n_x + 1) + kMolListPad;
     hipLaunchKernelGGL(k_mol_list, dim3((unsigned)tr.n_orb), dim3(kBlock), 0, s, tr.molslot.as<MolSlotDev>(), tr.n_mol,
                        counts, aip, tr.mol_smp.as<double4>(), tr.mol_nin.as<int32_t>(), recs, 1 + na, tr.n_pr,
-                       tr.n_orb, tr.n_x, lst_stride, (int32_t)(na == 0 && tr.exp_mode), tr.mol_lst.as<double4>(),
-                       tr.mol_rend.as<int32_t>());
+                       tr.n_orb, tr.n_x, lst_stride, (int32_t)(na == 0 && tr.exp_mode),
+                       tr.n_mirror > 0 && tr.n_pr <= kMolMirrorMax ? tr.mirror.as<int32_t>() : nullptr,
+                       tr.mol_lst.as<double4>(), tr.mol_rend.as<int32_t>());
     PROM_HIP(hipGetLastError());
 #define PROM_TAUM(NSV, EK)                                                                                  \
   if (tr.n_mol == 1) PROM_TAUM1(NSV, EK, true); else PROM_TAUM1(NSV, EK, false)

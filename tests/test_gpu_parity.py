@@ -142,6 +142,19 @@ def test_transit_ocml_exp_mode(dev, name):
         assert rel(R_ocml, d["R"]) < 1e-12
 
 
+def test_molecular_mirror_merging(dev, monkeypatch):
+    """Mirror-image chords (z -> -z) with equal molecular sample lists are integrated once with the summed weight
+    (k_mol_list): R with merging agrees with the unmerged R to 1e-13 and with the reference's golden R."""
+    d = load("transit_C5r")
+    tr = _product_transit(json.loads(str(d["config"])))
+    R_m = tr.sumOverChords(devices=[0])
+    monkeypatch.setenv("PROM_MOL_MIRROR", "0")
+    R_u = tr.sumOverChords(devices=[0])
+    print("C5r mirror merging: rel diff %.3e, vs golden %.3e / %.3e" % (rel(R_m, R_u), rel(R_m, d["R"]), rel(R_u, d["R"])))
+    assert rel(R_m, R_u) < 1e-13
+    assert rel(R_m, d["R"]) < R_TOL and rel(R_u, d["R"]) < R_TOL
+
+
 @pytest.mark.parametrize("name", ["C1", "C2r", "C4r", "exomoon"])
 def test_chord_merging(dev, name, monkeypatch):
     """Merging chords with equal (2^-40) column densities moves R by <= 2^-40/e.  Checked with
