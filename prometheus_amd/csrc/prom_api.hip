@@ -1198,22 +1198,24 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       }
     // work buffers
     const int64_t nc = n_orb * tr.n_pr;
-    tr.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
-    // pipelining needs every per-run buffer in the slot: the generic column path (k_ntot + k_columns:
-    // n_x > 64, > 8 terms or > 4 scenarios) keeps n(c, x) in the shared tr.ntot, so it runs one slot
+    // pipelining needs every per-run buffer in the slot (n(c, x), the molecular samples and lists are); the
+    // fast atomic paths and the molecular path run pipelined, the generic atomic column path (k_ntot +
+    // k_columns: n_x > 64, > 8 terms or > 4 scenarios) and the stellar-spectrum path one slot
     const bool cols8 = n_mol == 0 && tr.n_x <= 64 && tr.n_terms <= 8 && tr.n_sc <= 4;
     const bool fast = tr.exp_mode && n_mol == 0 && n_atoms >= 1 && n_atoms <= prom::kWinMaxSpecies && tr.window &&
                       !tr.star && cols8;
-    tr.depth = fast ? ctx->pipeline : 1;
+    const bool mol_pipe = n_mol > 0 && !tr.star;
+    tr.depth = (fast || mol_pipe) ? ctx->pipeline : 1;
     for (int si = 0; si < tr.depth; ++si) {
     prom::RunSlot& rs = tr.slot[si];
+      if (!cols8) rs.ntot.ensure(sizeof(double) * tr.n_sc * nc * tr.n_x);
       rs.ncol.ensure(sizeof(double) * std::max<int64_t>(n_atoms, 1) * nc);
-      tr.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
+      rs.molcol.ensure(sizeof(double) * std::max<int64_t>(n_mol, 1) * nc);
       if (n_mol > 0) {
-        tr.mol_smp.ensure(sizeof(double) * 4 * n_mol * nc * tr.n_x);
-        tr.mol_nin.ensure(sizeof(int32_t) * n_mol * nc);
-        tr.mol_lst.ensure(sizeof(double) * 4 * ((n_mol * tr.n_x + 1) * nc + (int64_t)prom::kMolListPad * n_orb));
-        tr.mol_rend.ensure(sizeof(int32_t) * nc);
+        rs.mol_smp.ensure(sizeof(double) * 4 * n_mol * nc * tr.n_x);
+        rs.mol_nin.ensure(sizeof(int32_t) * n_mol * nc);
+        rs.mol_lst.ensure(sizeof(double) * 4 * ((n_mol * tr.n_x + 1) * nc + (int64_t)prom::kMolListPad * n_orb));
+        rs.mol_rend.ensure(sizeof(int32_t) * nc);
       }
       rs.flags.ensure(sizeof(int32_t) * nc);
       rs.recs.ensure(sizeof(double) * nc * (1 + n_atoms));

@@ -259,6 +259,15 @@ struct RunSlot {
   DevBuf wmom;                              // [n_orb][n_pr + 1][K] suffix tail moments
   DevBuf evals;                             // [64] uint64 exp-evaluation counters (stats runs)
   DevBuf sig;                               // resampled sigma_s(shift lambda_w) [sig rows][n_atoms or 1][n_wav]
+  // the generic column path's and the molecular path's per-run buffers (per slot: pipelined runs)
+  DevBuf ntot;                              // [n_sc][n_orb][n_pr][n_x]
+  DevBuf molcol;                            // [n_mol][n_orb][n_pr] sum_x n_abs*dx (for the bound)
+  DevBuf mol_smp;                           // [n_mol][n_orb][n_pr][n_x] double4 {P weight, n_abs = n chi, P bracket,
+                                            //     0} of the in-table samples, compacted to the front of each chord
+  DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
+  DevBuf mol_lst;                           // [n_orb][n_pr (n_mol n_x + 1) + kMolListPad] double4: each phase's records' in-table
+                                            //     samples, one flat list (k_mol_list)
+  DevBuf mol_rend;                          // [n_orb][n_pr] int32: end of each record's samples in the list
                                             //     (one row, or one per phase with orbital Doppler shift)
   DevBuf zfl;                               // merged species: some chi_s sigma_s not > 0 [sig rows][n_wav] uint8
   DevBuf tq;                                // resampled path: Q ranges of the two halves of each 128-lambda
@@ -302,8 +311,6 @@ struct TransitDev {
   DevBuf scdev;                             // [n_sc] ScDev (density + tabulated pointer)
   DevBuf terms_dev;                         // [n_terms] TermDev
   DevBuf tab;                               // tabulated densities, raw host order, concatenated
-  DevBuf ntot;                              // [n_sc][n_orb][n_pr][n_x]
-  DevBuf molcol;                            // [n_mol][n_orb][n_pr] sum_x n_abs*dx (for the bound)
   DevBuf sigma;                             // [n_atoms][n_orb][n_wav]
   DevBuf sigma_max_dev;                     // [n_atoms]
   DevBuf sigtab;                            // [n_atoms] SigTabDev
@@ -336,14 +343,9 @@ struct TransitDev {
   hipEvent_t* kprof = nullptr;
   uint32_t kprof_mask = 0;
   DevBuf molslot;                           // [n_mol] MolSlotDev
-  DevBuf mol_smp;                           // [n_mol][n_orb][n_pr][n_x] double4 {P weight, n_abs = n chi, P bracket,
-                                            //     0} of the in-table samples, compacted to the front of each chord
-  DevBuf mol_nin;                           // [n_mol][n_orb][n_pr] int32 their count
   DevBuf mirror;                            // [n_pr] int32: each chord's mirror image (z -> -z) or -1 (host-paired)
   int64_t n_mirror = 0;                     // (mirror pairs; 0: none, or PROM_MOL_MIRROR=0)
   std::vector<int32_t> mirror_h;            // (host image of mirror)
-  DevBuf mol_lst;                           // [n_orb][n_pr (n_mol n_x + 1) + kMolListPad] double4: each phase's records' in-table
-                                            //     samples, one flat list (k_mol_list)
   DevBuf sig_seg4;                          // [n_blk][n_atoms][4] per-wavefront SigSeg of blocks without a guess (kind & 8),
                                             // then the bucket directories' SigSeg (kind & 32)
   int64_t sig_noguess = 0;                  // (block, species) pairs without a guess or a directory (host count)
@@ -352,7 +354,6 @@ struct TransitDev {
   DevBuf rm_ftab;                           // ... [n_pr][n_wav] every chord's flux F(c, w) (k_rm_fout, per set), when it
   bool rm_ftab_ok = false;                  //     fits PROM_RM_FTAB_MB and a quarter of the free device memory
   DevBuf mol_g;                             // every slot's MolSlotDev::G
-  DevBuf mol_rend;                          // [n_orb][n_pr] int32: end of each record's samples in the list
   std::vector<MolSlotDev> mslots;           // host copy
   std::vector<int64_t> tab_off;             // per scenario offset into `tab` (-1: none)
   int32_t star_table_id = -1;               // prom_transit_problem.star_table (invalidation on free)

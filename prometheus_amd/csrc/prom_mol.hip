@@ -206,12 +206,21 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
       // no load; otherwise search (first phase) or walk from the previous phase's bracket
       if (!kMolWCache || h < 0 || !(wb.x < lw && lw <= wb.y)) {
         if (h < 0) {
-          int64_t lo = 0, hi = nw - 1;
-          while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (W[mid] < lw) lo = mid; else hi = mid;
+          // first phase: the linear guess on the node range, kept when it is scipy's bracket (uniform grids, e.g.
+          // ExoMol's bin edges: two loads instead of a ~16-load dependent bisection), else bisection
+          const double W0 = W[0], WN = W[nw - 1];
+          int64_t g = (int64_t)((lw - W0) * ((double)(nw - 1) / (WN - W0)));
+          g = g < 0 ? 0 : (g > nw - 2 ? nw - 2 : g);
+          if (W[g] < lw && lw <= W[g + 1]) {
+            h = g;
+          } else {
+            int64_t lo = 0, hi = nw - 1;
+            while (hi - lo > 1) {
+              const int64_t mid = (lo + hi) >> 1;
+              if (W[mid] < lw) lo = mid; else hi = mid;
+            }
+            h = lo;
           }
-          h = lo;
         } else {
           while (h < nw - 2 && W[h + 1] < lw) ++h;
           while (h > 0 && !(W[h] < lw)) --h;
@@ -533,19 +542,31 @@ __global__ void __launch_bounds__(kBlock) k_mol_list(const MolSlotDev* __restric
 }
 
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3, int32_t) {
-  // phase groups: at least ~16 waves per SIMD over the whole grid (65,536 over 1,024 SIMDs), so the last round of
-  // the equally long waves is a small tail (one group of all 32 C5 phases left a 4th round ~5 % full: 1.58x on
-  // the step against 4-phase pieces, BENCH_r03 phase_shard); each group's first phase binary-searches the lambda'
-  // bracket, the others walk it.  PROM_MOL_PPG (profiling): phases per group.
+  // Phase groups: a workgroup runs ppg phases of its 256 wavelengths after a prologue (exp table, first bracket,
+  // the LDS stage) worth ~1.4 phases of samples on C5, so fewer, longer groups amortise it, against the tail of the
+  // last round of workgroups.  ppg minimises (workgroups / resident slots + 1/2) x (1.4 + ppg) (C5 sweeps,
+  // profiles/r05c5b_ppg_sweep.txt: full grid 16 of 32 phases per group, a wavelength shard 8, a 4-phase shard 4;
+  // the previous rule, >= 16 waves per SIMD, gave 1, 1 and 8 and a 1.8x slower shard).  PROM_MOL_PPG: fixed.
   const int64_t n_tiles = (tr.n_wav + kBlock - 1) / kBlock;
-  int32_t groups = (int32_t)std::max<int64_t>(1, std::min<int64_t>(tr.n_orb, (65536 + 4 * n_tiles - 1) / (4 * n_tiles)));
-  int32_t ppg = (tr.n_orb + groups - 1) / groups;
-  // equal groups: the next phase count that divides the phases (C5: 7 -> 8, four groups of 8; a short last group
-  // ends early and leaves its CUs idle: profiles/r04o_C5_ppg_sweep.txt)
-  while (ppg < tr.n_orb && tr.n_orb % ppg != 0 && ppg < 2 * ((tr.n_orb + groups - 1) / groups)) ++ppg;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    PROM_HIP(hipGetDevice(&dev));
+    PROM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (cus <= 0) cus = 256;
+  }
+  const double slots = 5.0 * cus;   // (k_tau_mol's LDS: five workgroups per CU)
+  int32_t ppg = 1;
+  double best = 1e300;
+  for (int32_t p = 1; p <= tr.n_orb; ++p) {
+    const int64_t grp = (tr.n_orb + p - 1) / p;
+    if (p > 1 && (tr.n_orb + p - 2) / (p - 1) == grp) continue;   // (same group count: the smaller ppg)
+    const double c = ((double)(n_tiles * grp) / slots + 0.5) * (1.4 + (double)p);
+    if (c <= best) { best = c; ppg = p; }
+  }
   if (const char* e = std::getenv("PROM_MOL_PPG"))
     if (std::atoi(e) > 0) ppg = std::min(tr.n_orb, std::atoi(e));
-  groups = (tr.n_orb + ppg - 1) / ppg;
+  const int32_t groups = (tr.n_orb + ppg - 1) / ppg;
   const dim3 g((unsigned)n_tiles, (unsigned)groups);
   const double* wav = tr.wav.as<double>();
   const double* recs = rs.recs.as<double>();
@@ -569,17 +590,17 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
     }
     const int64_t lst_stride = (int64_t)tr.n_pr * (tr.n_mol * tr.n_x + 1) + kMolListPad;
     hipLaunchKernelGGL(k_mol_list, dim3((unsigned)tr.n_orb), dim3(kBlock), 0, s, tr.molslot.as<MolSlotDev>(), tr.n_mol,
-                       counts, aip, tr.mol_smp.as<double4>(), tr.mol_nin.as<int32_t>(), recs, 1 + na, tr.n_pr,
+                       counts, aip, rs.mol_smp.as<double4>(), rs.mol_nin.as<int32_t>(), recs, 1 + na, tr.n_pr,
                        tr.n_orb, tr.n_x, lst_stride, (int32_t)(na == 0 && tr.exp_mode),
                        tr.n_mirror > 0 && tr.n_pr <= kMolMirrorMax ? tr.mirror.as<int32_t>() : nullptr,
-                       tr.mol_lst.as<double4>(), tr.mol_rend.as<int32_t>());
+                       rs.mol_lst.as<double4>(), rs.mol_rend.as<int32_t>());
     PROM_HIP(hipGetLastError());
 #define PROM_TAUM(NSV, EK)                                                                                  \
   if (tr.n_mol == 1) PROM_TAUM1(NSV, EK, true); else PROM_TAUM1(NSV, EK, false)
 #define PROM_TAUM1(NSV, EK, M1V)                                                                            \
   hipExtLaunchKernelGGL((k_tau_mol<NSV, EK, M1V>), g, dim3(kBlock), 0, s, kps, kpe, 0, tr.sigtab_v, tr.molslot.as<MolSlotDev>(), \
                      tr.n_mol, lst_stride, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav,     \
-                     tr.delta_x, tr.mol_lst.as<double4>(), tr.mol_rend.as<int32_t>(), R,                     \
+                     tr.delta_x, rs.mol_lst.as<double4>(), rs.mol_rend.as<int32_t>(), R,                     \
                      tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr)
 #define PROM_TAUM_NS(EK)                \
   switch (na) {                         \

@@ -2303,7 +2303,7 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       if (m.kind == PROM_DENSITY_TABULATED || m.kind == PROM_DENSITY_GRIDDED) tab = tr.tab.as<double>() + tr.tab_off[sc];
       hipLaunchKernelGGL(k_ntot, dim3(grid_for(per)), dim3(kBlock), 0, s, m, sc, tr.x.as<double>(), tr.n_x,
                          tr.cy.as<double>(), tr.cz.as<double>(), tr.n_pr, tr.n_orb, tr.body_x.as<double>(),
-                         tr.body_y.as<double>(), tab, tr.ntot.as<double>());
+                         tr.body_y.as<double>(), tab, rs.ntot.as<double>());
       PROM_HIP(hipGetLastError());
     }
     double mol_max = 0.0;
@@ -2311,17 +2311,17 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
       if (t.is_molecule) mol_max = std::max(mol_max, std::pow(10.0, mtables[t.table].vmax));
     if (tr.n_mol > 0) {
       hipLaunchKernelGGL(k_mol_prep, dim3(grid_for(nc * tr.n_mol, 64)), dim3(64), 0, s, tr.molslot.as<MolSlotDev>(),
-                         tr.n_mol, tr.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
-                         tr.mol_smp.as<double4>(), tr.mol_nin.as<int32_t>(),
-                         tr.molcol.as<double>());
+                         tr.n_mol, rs.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
+                         rs.mol_smp.as<double4>(), rs.mol_nin.as<int32_t>(),
+                         rs.molcol.as<double>());
       PROM_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_columns, dim3(grid_for(nc, 64)), dim3(64), 0, s, tr.terms_dev.as<TermDev>(),
-                       tr.n_terms, tr.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
+                       tr.n_terms, rs.ntot.as<double>(), tr.n_x, tr.n_pr, tr.n_orb, tr.delta_x,
                        tr.cy.as<double>(), tr.cz.as<double>(), tr.planet_y.as<double>(), tr.planet_R,
                        tr.n_moons, tr.moon_y.as<double>(), tr.moon_R.as<double>(),
                        tr.sigma_max_dev.as<double>(), mol_max, tr.cull_tau, rs.ncol.as<double>(),
-                       tr.molcol.as<double>(), rs.flags.as<int32_t>());
+                       rs.molcol.as<double>(), rs.flags.as<int32_t>());
     PROM_HIP(hipGetLastError());
     kp_rec(tr, PROM_K_COLUMNS, true, s);
   }
