@@ -693,6 +693,8 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       // mirror images (y, -z) of the chords, for k_mol_list's merging of equal molecular records: sorted by y,
       // each unpaired chord with z != 0 takes the first later chord within 1e-9 of (y, -z) (relative to its
       // radius); k_mol_list verifies the sample lists before merging anything
+      const char* stg_env = std::getenv("PROM_MOL_STAGE");
+      tr.mol_stage = !(stg_env && std::atoi(stg_env) == 0);
       const char* mir_env = std::getenv("PROM_MOL_MIRROR");
       const bool mir_on = !(mir_env && std::atoi(mir_env) == 0);
       tr.mirror_h.assign((size_t)tr.n_pr, -1);

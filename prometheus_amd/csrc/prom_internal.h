@@ -345,6 +345,7 @@ struct TransitDev {
   DevBuf molslot;                           // [n_mol] MolSlotDev
   DevBuf mirror;                            // [n_pr] int32: each chord's mirror image (z -> -z) or -1 (host-paired)
   int64_t n_mirror = 0;                     // (mirror pairs; 0: none, or PROM_MOL_MIRROR=0)
+  bool mol_stage = true;                    // k_tau_mol's LDS stage of G (PROM_MOL_STAGE=0: global reads, validation)
   std::vector<int32_t> mirror_h;            // (host image of mirror)
   DevBuf sig_seg4;                          // [n_blk][n_atoms][4] per-wavefront SigSeg of blocks without a guess (kind & 8),
                                             // then the bucket directories' SigSeg (kind & 32)

@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
                                                     int32_t n_orb, int32_t phases_per_group, int64_t n_wav,
                                                     double delta_x, const double4* __restrict__ lst,
                                                     const int32_t* __restrict__ rend, double* __restrict__ R,
-                                                    unsigned long long* __restrict__ evals) {
+                                                    unsigned long long* __restrict__ evals, int32_t stage) {
   __shared__ double etab[kMolExpN];   // exp table 2^(i/1024)
   if (EXPK)
     for (int i = threadIdx.x; i < kMolExpN; i += kBlock) etab[i] = kExp2TableDev[i * (PROM_EXP2_TABLE_N / kMolExpN)];
@@ -154,6 +154,9 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
                                                valid ? (int)((uint32_t)(kMolBilin ? max(ms[m].n_p - 1, 1) : ms[m].n_p) * rowbv[m]) : 0,
                                                0x00020000);
   }
+  double shp[M1 ? 1 : 4];   // each slot's Doppler factor at the previous phase (uniform)
+#pragma unroll
+  for (int m = 0; m < (M1 ? 1 : 4); ++m) shp[m] = __builtin_nan("");
   int64_t iwv[4] = {-1, -1, -1, -1};
   double twv[4] = {0.0, 0.0, 0.0, 0.0};
   // the lane's current bracket nodes {W[h], W[h + 1]} per slot (a phase whose lambda' stays inside them reuses h
@@ -171,7 +174,7 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
   __shared__ double2 gst[STG ? kMolStageD2 : 1];
   __shared__ int32_t red[2][kBlock / 64];
   int32_t st_lo = 0, st_n = 0;
-  bool st_done = false;
+  bool st_done = stage == 0;   // (PROM_MOL_STAGE=0: every sample reads global memory)
   bool wasc = false;   // the wave's wavelengths ascending (lane order)
   if constexpr (STG) {
     const double prev = __shfl_up(lam, 1);
@@ -195,7 +198,12 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
       if (m >= n_mol) break;
       const double* __restrict__ W = ms[m].W;
       const int64_t nw = ms[m].n_w;
-      const double lw = ms[m].shift[o] * lam;
+      // the previous phase's Doppler factor (no orbital Doppler shift: every phase's): the same bracket, weight
+      // and in-table bit, nothing to do
+      const double sh = ms[m].shift[o];
+      if (sh == shp[m]) continue;
+      shp[m] = sh;
+      const double lw = sh * lam;
       // scipy: i = searchsorted(W, lw, 'left') - 1 clipped to [0, n-2], fill outside [W[0], W[n-1]]
       const bool ok = ((tin >> m) & 1u) && lw >= W[0] && lw <= W[nw - 1];
       inb = ok ? (inb | (1u << m)) : (inb & ~(1u << m));
@@ -601,7 +609,7 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
   hipExtLaunchKernelGGL((k_tau_mol<NSV, EK, M1V>), g, dim3(kBlock), 0, s, kps, kpe, 0, tr.sigtab_v, tr.molslot.as<MolSlotDev>(), \
                      tr.n_mol, lst_stride, wav, recs, aip, fo, counts, tf, fs, tr.n_pr, tr.n_orb, ppg, tr.n_wav,     \
                      tr.delta_x, rs.mol_lst.as<double4>(), rs.mol_rend.as<int32_t>(), R,                     \
-                     tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr)
+                     tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr, tr.mol_stage ? 1 : 0)
 #define PROM_TAUM_NS(EK)                \
   switch (na) {                         \
     case 0: PROM_TAUM(0, EK); break;    \

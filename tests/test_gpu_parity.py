@@ -155,6 +155,28 @@ def test_molecular_mirror_merging(dev, monkeypatch):
     assert rel(R_m, d["R"]) < R_TOL and rel(R_u, d["R"]) < R_TOL
 
 
+def test_molecular_lds_stage_matches_global_reads(dev, monkeypatch):
+    """k_tau_mol's LDS stage of the G records returns the global records' values: R bitwise with the stage
+    disabled (PROM_MOL_STAGE=0, every sample read from global memory)."""
+    d = load("transit_C5r")
+    tr = _product_transit(json.loads(str(d["config"])))
+    R_s = tr.sumOverChords(devices=[0])
+    monkeypatch.setenv("PROM_MOL_STAGE", "0")
+    R_g = tr.sumOverChords(devices=[0])
+    assert np.array_equal(R_s, R_g)
+    assert rel(R_s, d["R"]) < R_TOL
+
+
+def test_molecular_pipelined_runs(dev):
+    """Molecular runs rotate over the pipeline slots (per-slot samples and lists): every run's R is the same."""
+    d = load("transit_C5r")
+    tr = _product_transit(json.loads(str(d["config"])))
+    R = [tr.sumOverChords(devices=[0]) for _ in range(6)]
+    for r in R[1:]:
+        assert np.array_equal(r, R[0])
+    assert rel(R[0], d["R"]) < R_TOL
+
+
 @pytest.mark.parametrize("name", ["C1", "C2r", "C4r", "exomoon"])
 def test_chord_merging(dev, name, monkeypatch):
     """Merging chords with equal (2^-40) column densities moves R by <= 2^-40/e.  Checked with
