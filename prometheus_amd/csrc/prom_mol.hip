@@ -121,9 +121,12 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
                                                     const int32_t* __restrict__ rend, double* __restrict__ R,
                                                     unsigned long long* __restrict__ evals, int32_t stage) {
   __shared__ double etab[kMolExpN];   // exp table 2^(i/1024)
-  if (EXPK)
+  // (with the LDS stage the table is filled in the stage's load round and barrier, below)
+  const bool etab_late = M1 && EXPK && kMolBilin && PROM_MOL_STAGE && stage != 0;
+  if (EXPK && !etab_late) {
     for (int i = threadIdx.x; i < kMolExpN; i += kBlock) etab[i] = kExp2TableDev[i * (PROM_EXP2_TABLE_N / kMolExpN)];
-  __syncthreads();
+    __syncthreads();
+  }
   const int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
@@ -285,6 +288,10 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
           // each side (later phases' ranges stay inside it unless lambda' moves that far; a wave whose range leaves
           // it reads that phase's records from global memory)
           const int wid = threadIdx.x >> 6;
+          double et[kMolExpN / kBlock];   // (the exp table's loads in flight across the range exchange)
+#pragma unroll
+          for (int j = 0; j < kMolExpN / kBlock; ++j)
+            et[j] = kExp2TableDev[(threadIdx.x + j * kBlock) * (PROM_EXP2_TABLE_N / kMolExpN)];
           if ((threadIdx.x & 63) == 0) { red[0][wid] = mn; red[1][wid] = mx; }
           __syncthreads();
           int32_t gmn = 0x7fffffff, gmx = -1;
@@ -306,6 +313,8 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
               st_n = n_;
             }
           }
+#pragma unroll
+          for (int j = 0; j < kMolExpN / kBlock; ++j) etab[threadIdx.x + j * kBlock] = et[j];
           __syncthreads();
           st_done = true;
         }
