@@ -462,6 +462,12 @@ __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h
 // 32-byte records from the global table.  NT = R target rows with orbital Doppler shift, NT = 1 without (UNI:
 // the R phases of the workgroup share one Y per wavelength).  Then each (phase, wavelength): R = T_o(Y).
 // (build macro PROM_TC_WPE: pin the lookup kernel's waves per SIMD, for occupancy sweeps)
+#ifndef PROM_TC_FG
+#define PROM_TC_FG 2    // rows per group of global-record lookups in k_sigma_tc's front / directory paths
+#endif
+#ifndef PROM_TC_LG4
+#define PROM_TC_LG4 1   // 1: k_sigma_tc's LDS lookups in groups of 4 rows (register pressure; A/B)
+#endif
 #ifdef PROM_TC_WPE
 #define PROM_TC_ATTR __attribute__((amdgpu_waves_per_eu(PROM_TC_WPE, PROM_TC_WPE)))
 #else
@@ -602,7 +608,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
       if ((sg.kind & 3) == 0 && (sg.kind & 32)) {
         // a bucket directory over the slice (kind & 32: seg4[pad] = {slice lo, buckets + 1, its offset in sdir,
         // the linear map to buckets}): the bucket's bracket, verified on the host within one node of numpy's
-        constexpr int G = NT < 4 ? NT : 4;
+        constexpr int G = NT < PROM_TC_FG ? NT : PROM_TC_FG;
         const SigSeg dg = seg4[sg.pad];
         const int32_t* __restrict__ dv = sdir + dg.pad;
         const double4* __restrict__ rr = tb.rec + dg.lo;
@@ -633,7 +639,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
       }
       if ((sgw.kind & 3) > 0) {
         const bool exact = (sgw.kind & 4) != 0;
-        constexpr int G = NT < 4 ? NT : 4;
+        constexpr int G = NT < PROM_TC_FG ? NT : PROM_TC_FG;
         const double4* __restrict__ rr = tb.rec + sgw.lo;
 #pragma unroll
         for (int r0g = 0; r0g < NT; r0g += G) {
@@ -668,26 +674,32 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
       const double2* sel = ssel + s * CAP;
       auto lds_rows = [&](auto guard) {
         constexpr bool GD = decltype(guard)::value;
-        double xk[NT];
-        double2 el[NT];
+        constexpr int LG = PROM_TC_LG4 ? (NT < 4 ? NT : 4) : NT;   // rows per group of lookups in flight
 #pragma unroll
-        for (int r = 0; r < NT; ++r) {
-          if (GD && r >= ncap) break;
-          const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
-          if (exact) {
-            xk[r] = sx[g];
-            el[r] = sel[g];
-          } else {
-            const double2 xx = make_double2(sx[g], sx[g + 1]);
-            const int32_t k = tt[r] < xx.x ? g - 1 : (tt[r] >= xx.y ? g + 1 : g);
-            xk[r] = sx[k];
-            el[r] = sel[k];
+        for (int r0g = 0; r0g < NT; r0g += LG) {
+          double xk[LG];
+          double2 el[LG];
+#pragma unroll
+          for (int rr = 0; rr < LG; ++rr) {
+            const int r = r0g + rr;
+            if (GD && r >= ncap) break;
+            const int32_t g = seg_guess(tt[r], sg.xs, sg.inv, sg.m);
+            if (exact) {
+              xk[rr] = sx[g];
+              el[rr] = sel[g];
+            } else {
+              const double2 xx = make_double2(sx[g], sx[g + 1]);
+              const int32_t k = tt[r] < xx.x ? g - 1 : (tt[r] >= xx.y ? g + 1 : g);
+              xk[rr] = sx[k];
+              el[rr] = sel[k];
+            }
           }
-        }
 #pragma unroll
-        for (int r = 0; r < NT; ++r) {
-          if (GD && r >= ncap) break;
-          emit(r, el[r].x, exp_taylor<D>(el[r].y * (tt[r] - xk[r]), pc));
+          for (int rr = 0; rr < LG; ++rr) {
+            const int r = r0g + rr;
+            if (GD && r >= ncap) break;
+            emit(r, el[rr].x, exp_taylor<D>(el[rr].y * (tt[r] - xk[rr]), pc));
+          }
         }
       };
       if (ncap >= NT) lds_rows(std::false_type{});
