@@ -465,6 +465,9 @@ __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h
 #ifndef PROM_TC_FG
 #define PROM_TC_FG 2    // rows per group of global-record lookups in k_sigma_tc's front / directory paths
 #endif
+#ifndef PROM_TC_LGN
+#define PROM_TC_LGN 4   // (its group size)
+#endif
 #ifndef PROM_TC_LG4
 #define PROM_TC_LG4 1   // 1: k_sigma_tc's LDS lookups in groups of 4 rows (register pressure; A/B)
 #endif
@@ -674,7 +677,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
       const double2* sel = ssel + s * CAP;
       auto lds_rows = [&](auto guard) {
         constexpr bool GD = decltype(guard)::value;
-        constexpr int LG = PROM_TC_LG4 ? (NT < 4 ? NT : 4) : NT;   // rows per group of lookups in flight
+        constexpr int LG = PROM_TC_LG4 ? (NT < PROM_TC_LGN ? NT : PROM_TC_LGN) : NT;   // rows per group of lookups in flight
 #pragma unroll
         for (int r0g = 0; r0g < NT; r0g += LG) {
           double xk[LG];
