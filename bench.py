@@ -483,7 +483,8 @@ def main():
         # SURVEY.md 8d rule (ii): per chord-wavelength n_x table lookups (P-lerp + 10^v + FMA) against the
         # measured table-exp rate (profiles/r02u_fp64_exp_peak.json: 2.8e12/s)
         # (the device counts them in stats runs: exp_evals = the 10^v of in-table samples + one e^-tau per
-        # record and wavelength; out-of-table samples are skipped, k_mol_prep compacts them away)
+        # record and wavelength; out-of-table samples are skipped, k_mol_prep compacts them away; a mirror-merged
+        # chord pair's samples are listed and counted once -- pow10 is the evaluations performed)
         # achieved / peak / frac in one unit (10^v per second); the byte figures move under "hbm"
         pow10 = max(0, int(st["exp_evals"]) - int(st["tau_records"]) * n_w)
         km = kernels[tau_kernel]
