@@ -8,14 +8,17 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/prom_api.hip", "csrc/prom_transit.hip", "csrc/prom_fn.hip", "csrc/prom_mol.hip", "csrc/prom_tcurve.hip",
-           "csrc/prom_rm.hip", "csrc/prom_sigma.hip"]
-HEADERS = ["csrc/prom_internal.h", "csrc/prom_device.h", "csrc/faddeeva.h", "csrc/exp2_table.h",
+           "csrc/prom_rm.hip", "csrc/prom_sigma.hip", "csrc/prom_window.hip",
+           "csrc/prom_tw.hip"]
+HEADERS = ["csrc/prom_internal.h", "csrc/prom_device.h", "csrc/prom_tc.h", "csrc/faddeeva.h", "csrc/exp2_table.h",
            "csrc/exp2_table_body.h", "../include/prom_hip.h"]
 OUT = os.path.join(HERE, "libprom_hip.so")
 ARCH = os.environ.get("PROM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=" + ARCH, "-ffp-contract=off", "-fPIC", "-Wall",
          "-Wno-unused-function"]
 OBJDIR = os.path.join(HERE, "build")
+# per-source flags: k_sigma_tw without machine LICM (its rare passes' hoisted constants set the register peak)
+SRC_FLAGS = {"csrc/prom_tw.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def hipcc() -> str:
@@ -47,7 +50,7 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = OUT, 
         if only is not None and src not in only:
             return os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
         obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
-        cmd = [cc] + FLAGS + list(extra) + ["-c", os.path.join(HERE, src), "-o", obj]
+        cmd = [cc] + FLAGS + SRC_FLAGS.get(src, []) + list(extra) + ["-c", os.path.join(HERE, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True, cwd=HERE)

@@ -891,8 +891,54 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       // pointing at buffers a later (failed) set may have reallocated
       tr.seg_key_valid = false;
       seg_key_keep = seg_reuse;   // the stored key stays as it is (re-validated at the end)
+      if (!seg_reuse) tr.tw_ok = false;
+      // target windows (k_sigma_tw, prom_window.hip): every atomic slot on one set of Doppler factors (one scenario),
+      // n_orb >= 2; built with the sigma segments (the same inputs) and kept when they are reused.  PROM_TW=0 (read at
+      // every set): none, k_sigma_tc's wavelength blocks
+      const char* e_tw = std::getenv("PROM_TW");
+      const bool tw_off = e_tw && std::atoi(e_tw) == 0;
+      auto build_tw = [&]() {
+        tr.tw_ok = false;
+        tr.n_tw = 0;
+        std::vector<const std::vector<double>*> tabs;
+        int32_t sc_tw = -1;
+        bool one = n_orb >= 2;
+        for (const auto& t : tr.terms) {
+          if (t.is_molecule) continue;
+          if (sc_tw < 0) sc_tw = t.scenario;
+          for (int64_t o = 0; o < n_orb; ++o)
+            if (!(sh[t.scenario * n_orb + o] == sh[sc_tw * n_orb + o])) one = false;
+          tabs.push_back(&ctx->tables[t.table].hx);
+        }
+        if (!one || sc_tw < 0 || tw_off) return;
+        // (profiling knobs, read once: wavelengths per row, points per window, pool nodes)
+        static const int rowcap = [] { const char* e = std::getenv("PROM_TW_ROWCAP"); return e ? std::max(1, std::atoi(e)) : 256; }();
+        static const int64_t pmax = [] { const char* e = std::getenv("PROM_TW_PMAX"); return e ? std::max(1, std::atoi(e)) : 8192; }();
+        static const int pool = [] {
+          const char* e = std::getenv("PROM_TW_POOL");
+          return e ? std::max(2, std::min(prom::kTwPoolMax, std::atoi(e))) : prom::kTwPoolMax;
+        }();
+        std::vector<prom::SigSeg> twseg;
+        std::vector<int32_t> twrow;
+        int32_t nw = 0;
+        if (!prom::build_target_windows(pb->wavelength, tr.n_wav, sh.data() + (int64_t)sc_tw * n_orb, (int32_t)n_orb, tabs,
+                                        pool, rowcap, pmax, twseg, twrow, nw))
+          return;
+        stg.add(tr.tw_seg, twseg.data(), (int64_t)twseg.size(), s);
+        stg.add(tr.tw_row, twrow.data(), (int64_t)twrow.size(), s);
+        tr.n_tw = nw;
+        tr.tw_ok = true;
+        if (std::getenv("PROM_DEBUG")) {
+          int64_t k1 = 0, k2 = 0, k0 = 0;
+          for (const auto& e : twseg) ((e.kind & 3) == 1 ? k1 : (e.kind & 3) == 2 ? k2 : k0) += 1;
+          std::fprintf(stderr, "[prom] target windows: %d (slices: %lld staged, %lld global, %lld searched)\n", nw,
+                       (long long)k1, (long long)k2, (long long)k0);
+        }
+      };
       if (seg_reuse) {
         tr.sig_seg_ok = true;
+        if (tw_off) tr.tw_ok = false;
+        else if (!tr.tw_ok) build_tw();
       } else if (want_seg && n_atoms >= 1 && n_atoms <= 4) {
         tr.seg_key_valid = false;
         const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;
@@ -1086,6 +1132,7 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         stg.add(tr.sig_fb, fbl.data(), (int64_t)fbl.size(), s);
         stg.add(tr.sig_fb_tc, fbt.data(), (int64_t)fbt.size(), s);
         tr.sig_seg_ok = true;
+        build_tw();
         // the key is committed only after the segments have reached the device (end of this call):
         // a set that throws later must not leave a key that a retry would reuse (validation segments never)
         seg_key_new = !no_guess && use_dir;

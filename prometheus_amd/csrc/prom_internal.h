@@ -89,6 +89,7 @@ constexpr int kSigSeg = PROM_SIG_SEG;
 // wavelengths at 0.001 A under a 0.6 A Doppler spread) stay in LDS instead of the global-record front path.  Host
 // segments mark slices within the cap SigSeg kind & 64.
 constexpr int tc_slice_cap(int nsig) { return nsig <= 1 ? 1024 : (nsig == 2 ? 640 : kSigSeg); }
+constexpr int kTwPoolMax = 800;   // k_sigma_tw: table nodes staged per target window, all species (kTwPool)
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
 #ifndef PROM_SIG_ROWS
 #define PROM_SIG_ROWS 8
@@ -199,7 +200,7 @@ struct SigTabs4 {
 constexpr int kTcHdr = 16;
 constexpr int kTcD = 16;
 enum : int { kTcHNmax = 0, kTcHTfrac = 1, kTcHFsum = 2, kTcHT0 = 3 /* .. 8: tail coefficients t_0 .. t_5 */,
-             kTcHL = 9, kTcHFlags = 10 /* 1: opaque above the table, 2: non-finite columns */, kTcHNact = 11 };
+             kTcHL = 9, kTcHFlags = 10 /* 1: opaque above the table, 2: non-finite columns, 4: truncated at the octave cap */, kTcHNact = 11 };
 constexpr int kTcMaxOctaves = 64;
 constexpr int kTcChain = 4;                          // octaves per table exp (k_tc_build)
 constexpr int kTcPartMax = 16;                       // chord parts per (phase, chain)
@@ -372,6 +373,12 @@ struct TransitDev {
   DevBuf sig_fb_tc;                         // the same for k_sigma_tc's caps (tc_slice_cap: SigSeg kind & 64)
   int32_t n_sig_fb_tc = 0;
   bool sig_seg_ok = false;
+  // target windows (prom_window.hip, k_sigma_tw): per window and atomic slot a SigSeg (kind 1: pad = pool offset),
+  // per window boundary and row the first wavelength; built with the sigma segments (same inputs, same reuse)
+  DevBuf tw_seg;                            // [n_tw][n_atoms] SigSeg
+  DevBuf tw_row;                            // [n_tw + 1][n_orb] int32
+  int32_t n_tw = 0;
+  bool tw_ok = false;
   // polynomial sigma rows (k_sigma_poly): degree D of the e^a Taylor polynomial for this problem's tables
   // (0: the exp10 path, k_sigma_rows; PROM_SIG_POLY=0 forces it)
   int32_t sig_deg = 0;
@@ -470,6 +477,13 @@ double reduce_max(hipStream_t s, const double* v, int64_t n, double* scratch_dev
 // prom_gridded_density (prom_fn.hip)
 void launch_gridded(hipStream_t s, const double* g, int32_t nx, int32_t ny, int32_t nz, int64_t n,
                     const double* px, const double* py, const double* pz, double* out);
+// k_sigma_tw (prom_tw.hip): the lookups + curves over the problem's target windows (tr.tw_ok)
+void launch_sigma_tw(hipStream_t s, TransitDev& tr, int32_t nsig, int32_t deg, const TcArgs& ta, hipEvent_t ev0,
+                     hipEvent_t ev1);
+// target windows of the Doppler-shifted lookups (prom_window.hip): false when the inputs do not allow them
+bool build_target_windows(const double* wav, int64_t n_wav, const double* shift, int32_t n_rows,
+                          const std::vector<const std::vector<double>*>& tabs, int32_t pool, int32_t rowcap,
+                          int64_t pmax, std::vector<SigSeg>& seg_out, std::vector<int32_t>& row_out, int32_t& n_win);
 // AtomTable::rec from a table's x and y, and the per-interval |a| bounds (prom_fn.hip)
 void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec, double* amax);
 void launch_scatter(hipStream_t s, const char* base, const ScatterDesc* d, int32_t n);

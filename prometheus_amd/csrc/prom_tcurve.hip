@@ -24,25 +24,9 @@
 //                 truncated at the host's octave cap) the exact sum over the phase's chords.
 // So |R - R_exact| is a few 1e-16 plus the rounding of the sums, against the windowed path's 4e-14.  A phase
 // with a non-finite column takes the reference's chord order with ocml exp (the NaN pattern), as before.
-#include "prom_device.h"
+#include "prom_tc.h"
 
 namespace prom {
-
-constexpr double kTcEps = 0x1p-7;        // tail threshold of q
-constexpr int kTcExpEps = -7;            // its binary exponent
-constexpr double kTcSat = 40.0;          // tau above which a chord is opaque (e^-40 = 4e-18)
-
-// q = Y N_max's binary exponent (q normal and >= 2^-7)
-__device__ __forceinline__ int32_t tc_exponent(double q) {
-  return (int32_t)((__builtin_bit_cast(unsigned long long, q) >> 52) & 0x7ff) - 1023;
-}
-
-// octaves [0, L) that cover q in [eps, qhi]: 0 when qhi < eps, INT32_MAX when not finite
-__device__ __forceinline__ int32_t tc_octaves(double qhi) {
-  if (!(qhi >= kTcEps)) return 0;
-  if (!(qhi <= 1.0e300)) return 0x7fffffff;
-  return tc_exponent(qhi) - kTcExpEps + 1;
-}
 
 // Reductions over the 64 lanes of a wavefront on DPP moves (quad permutes, half-row and row mirrors) and four
 // readlanes: no LDS round trips, a fixed combination order, a wave-uniform result.
@@ -205,7 +189,7 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
   // table extent: octaves up to the host's bound of q = Y N_max, or up to q = 40 N_max / N_min (every chord
   // opaque beyond it), whichever comes first; lg caps it
   const bool fin = nnf == 0 && nmax > 0.0 && nact > 0;
-  int32_t L = 0, top_opaque = 0;
+  int32_t L = 0, top_opaque = 0, trunc = 0;
   if (fin) {
     const int32_t L1 = ybound > 0.0 ? tc_octaves(ybound * nmax * (1.0 + 0x1p-40)) : 0x7fffffff;
     const int32_t L2 = tc_octaves(kTcSat * (nmax / nmin));
@@ -214,6 +198,7 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
       top_opaque = 1;
     } else {
       L = L1 < lg ? L1 : lg;
+      trunc = L1 > lg ? 4 : 0;   // (the lookups may need the exact sum beyond the table: header flag 4)
     }
   }
   const int32_t j0 = ch * kTcChain;
@@ -399,7 +384,7 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
 #pragma unroll
     for (int e = 0; e < 6; ++e) h[kTcHT0 + e] = t[e];
     h[kTcHL] = (double)L;
-    h[kTcHFlags] = (double)(top_opaque | (nnf ? 2 : 0));
+    h[kTcHFlags] = (double)(top_opaque | (nnf ? 2 : 0) | trunc);
     h[kTcHNact] = (double)nact;
     if (counts) {
       int32_t* cn = counts + o * kCnt;
@@ -412,47 +397,6 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
 #ifdef PROM_TRACE
   if (tid == 0) tq[4] = wall_clock64();
 #endif
-}
-
-// T_o(Y) for a phase whose columns are finite (header h, its table rows tabo)
-__device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h, const double* __restrict__ tabo,
-                                          const int32_t* __restrict__ fl, const double* __restrict__ nc,
-                                          const double* __restrict__ fout, int32_t n_pr, unsigned long long* evals) {
-  const double q = Y * h[kTcHNmax];
-  const double tf = h[kTcHTfrac];
-  if (q < kTcEps) {
-    double p = h[kTcHT0 + 5];
-#pragma unroll
-    for (int e = 4; e >= 0; --e) p = __builtin_fma(p, q, h[kTcHT0 + e]);
-    return tf + p;
-  }
-  const int32_t nact = (int32_t)h[kTcHNact];
-  if (!(q == q)) return nact > 0 ? q : tf;   // NaN cross-section: NaN wherever a chord absorbs
-  const int32_t L = (int32_t)h[kTcHL];
-  const int32_t j = q <= 1.0e300 ? tc_exponent(q) - kTcExpEps : 0x7fffffff;
-  if (j < L) {
-    // v = log2 of q's mantissa, in [0, 1); Clenshaw in u = 2 v - 1
-    const double m = __builtin_bit_cast(double, (__builtin_bit_cast(unsigned long long, q) & 0x000fffffffffffffull) |
-                                                    0x3ff0000000000000ull);
-    const double u = __builtin_fma(2.0, log2(m), -1.0);
-    const double* c = tabo + (int64_t)j * kTcD;
-    double b1 = 0.0, b2 = 0.0;
-#pragma unroll
-    for (int k = kTcD - 1; k >= 1; --k) {
-      const double b0 = __builtin_fma(2.0 * u, b1, c[k] - b2);
-      b2 = b1;
-      b1 = b0;
-    }
-    return tf + (__builtin_fma(u, b1, c[0] - b2));
-  }
-  if ((int32_t)h[kTcHFlags] & 1) return tf;   // every chord opaque (tau >= 40)
-  // beyond a truncated table: the exact sum over the phase's active chords, in chord order
-  const double inv_fs = 1.0 / h[kTcHFsum];
-  double a = 0.0;
-  for (int32_t c = 0; c < n_pr; ++c)
-    if (fl[c] == 0) a += (fout[c] * inv_fs) * exp(-(nc[c] * Y));
-  if (evals) atomicAdd(&evals[threadIdx.x & 63], (unsigned long long)nact);
-  return tf + a;
 }
 
 // ---- sigma lookups + transmission curves -> R --------------------------------------------------------------
@@ -476,38 +420,44 @@ __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h
 #else
 #define PROM_TC_ATTR
 #endif
-template <int NSIG, int D, bool MG, int R, bool UNI>
-__global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
+template <int NSIG, int D, bool MG, int R, bool UNI, int RG>
+__global__ void __launch_bounds__(kBlock * RG) PROM_TC_ATTR k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
                                                      int64_t n_wav, int32_t n_rows, const SigSeg* __restrict__ seg,
                                                      const SigSeg* __restrict__ seg4, const int32_t* __restrict__ sdir,
                                                      const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
                                                      int32_t n_rc, int32_t rf, const TcArgs ta) {
-  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per workgroup");
+  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per thread");
+  static_assert(RG == 1 || RG == 2 || RG == 4, "1, 2 or 4 row groups per workgroup");
   constexpr int NT = UNI ? 1 : R;
+  constexpr int NTH = kBlock * RG;          // threads: RG groups of 256 (one wavelength each) x R rows
   // every species' slice staged at once (one load round, one barrier): per species the nodes x_k (m + 1 of them)
   // and the records' {(chi) E_k, slope_k} (24 bytes a record: four 3-species workgroups per CU)
   constexpr int CAP = tc_slice_cap(NSIG);   // (nodes per species' slice, SigSeg kind & 64)
   constexpr int SXN = CAP + 2;              // (x_0 .. x_m, padded to 16 bytes)
   __shared__ double2 ssel[(D > 0 && NT > 1) ? NSIG * CAP : 1];
   __shared__ double ssx[(D > 0 && NT > 1) ? NSIG * SXN : 1];
-  const int tid = threadIdx.x;
+  // tid: the workgroup's thread (staging, headers); lt: the wavelength of the block; rg: the row group.  RG > 1: one
+  // slice stage serves RG x R rows (C3's 16 phases: one stage per block instead of two workgroups each staging it)
+  const int tid = threadIdx.x, lt = RG == 1 ? tid : tid & (kBlock - 1), rg = RG == 1 ? 0 : tid >> 8;
   const int32_t RF = rf;
-  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * ((n_rows + RF - 1) / RF);
+  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * ((n_rows + RF * RG - 1) / (RF * RG));
   int64_t bid = blockIdx.x, wb;
-  int32_t r0, rcap = R;
+  int32_t r0, rw, rcap = R;   // (rw: the workgroup's first row, r0: this row group's)
   bool lds_ok = true;
   if (bid < n_front) {
     const int64_t i = bid % n_fb8;
     if (i >= n_fb) return;
     wb = fb[i];
-    r0 = (int32_t)(bid / n_fb8) * RF;
+    rw = (int32_t)(bid / n_fb8) * RF * RG;
+    r0 = rw + rg * RF;
     rcap = RF;
     lds_ok = false;
   } else {
     bid -= n_front;
     const int64_t grp = bid / (8 * n_rc), rem = bid % (8 * n_rc);
     wb = grp * 8 + rem % 8;
-    r0 = (int32_t)(rem / 8) * R;
+    rw = (int32_t)(rem / 8) * R * RG;
+    r0 = rw + rg * R;
     if (wb >= n_blk) return;
     if constexpr (NT == 1 || D == 0) {
       // one target row (one phase, or phases sharing one Doppler factor): no LDS slices -- each lane reads its
@@ -525,17 +475,17 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
 #pragma unroll
   for (int s = 0; s < NSIG; ++s) sgs[s] = seg[wb * NSIG + s];
   // the rows' curve headers, staged with the slices (read after the lookups: no load round at the end)
-  __shared__ double shdr[R * kTcHdr];
-  if (tid < R * kTcHdr) {
-    const int32_t rr = r0 + tid / kTcHdr;
+  __shared__ double shdr[R * RG * kTcHdr];
+  if (tid < R * RG * kTcHdr) {
+    const int32_t rr = rw + tid / kTcHdr;
     shdr[tid] = ta.hdr[(int64_t)(rr < n_rows ? rr : n_rows - 1) * kTcHdr + tid % kTcHdr];
   }
   const int32_t rlim = r0 + rcap < n_rows ? r0 + rcap : n_rows;
-  rcap = rlim - r0;
+  rcap = RG == 1 ? rlim - r0 : (rlim > r0 ? rlim - r0 : 0);
 #ifdef PROM_TRACE
   const unsigned long long tr_t0 = wall_clock64();
 #endif
-  const int64_t w = wb * kBlock + tid;
+  const int64_t w = wb * kBlock + lt;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
   // the rows' targets, once: every species of the effective absorber belongs to one density scenario (species
@@ -553,13 +503,13 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
     if (lds_ok) {
       // each thread: records tid, tid + 256, ... of every species' slice (m <= CAP), all loads in flight before the
       // first LDS write
-      constexpr int NQ = (CAP + kBlock - 1) / kBlock;
+      constexpr int NQ = (CAP + NTH - 1) / NTH;
       double4 q[NSIG][NQ];
 #pragma unroll
       for (int s = 0; s < NSIG; ++s) {
         const double4* __restrict__ rr = tabv.t[s].rec + sgs[s].lo;
 #pragma unroll
-        for (int j = 0; j < NQ; ++j) q[s][j] = rr[tid + j * kBlock < sgs[s].m ? tid + j * kBlock : 0];
+        for (int j = 0; j < NQ; ++j) q[s][j] = rr[tid + j * NTH < sgs[s].m ? tid + j * NTH : 0];
       }
 #pragma unroll
       for (int s = 0; s < NSIG; ++s) {
@@ -569,7 +519,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
         const int32_t m = sgs[s].m;
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
-          const int32_t i = tid + j * kBlock;
+          const int32_t i = tid + j * NTH;
           if (i < m) {
             sx[i] = q[s][j].x;
             sel[i] = make_double2(MG ? chi * q[s][j].y : q[s][j].y, q[s][j].z);
@@ -637,7 +587,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
         continue;
       }
       if ((sg.kind & 3) == 0 && (sg.kind & 8)) {
-        const SigSeg sub = seg4[((int64_t)wb * NSIG + s) * 4 + (tid >> 6)];
+        const SigSeg sub = seg4[((int64_t)wb * NSIG + s) * 4 + (lt >> 6)];
         if (sub.m > 0) sgw = sub;
       }
       if ((sgw.kind & 3) > 0) {
@@ -719,7 +669,7 @@ __global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4
     if (r >= rcap) break;
     const int32_t o = r0 + r;
     const double Y = acc[UNI ? 0 : r];
-    const double* h = shdr + r * kTcHdr;
+    const double* h = shdr + (RG == 1 ? r : r0 - rw + r) * kTcHdr;
     double v;
     if (!((int32_t)h[kTcHFlags] & 2)) {
       v = tc_eval(Y, h, ta.tab + (int64_t)o * ta.lg * kTcD, ta.flags + (int64_t)o * ta.n_pr,
@@ -819,7 +769,12 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   static const int r1_env = [] { const char* e = std::getenv("PROM_TC_R1"); return e ? std::atoi(e) : 0; }();
   const int Rmax = (nsig >= 2 || uni) ? 8 : (r1_env == 4 ? 4 : 8);
   const int R = (uni || deg == 0) ? 8 : (n_rows == 1 ? 1 : Rmax);
-  const int32_t n_rc = (n_rows + R - 1) / R;
+  // row groups per workgroup (RG x 256 threads, one slice stage for RG x R rows): 2 when the rows need more than one
+  // group of R (C3: 16 phases), else 1; PROM_TC_RG (read once) forces 1 or 2
+  static const int rg_env = [] { const char* e = std::getenv("PROM_TC_RG"); return e ? std::atoi(e) : 0; }();
+  int RG = (!uni && R == 8 && deg > 0 && n_rows > R) ? 2 : 1;
+  if ((rg_env == 1 || rg_env == 2) && !uni && R == 8 && deg > 0) RG = rg_env;
+  const int32_t n_rc = (n_rows + R * RG - 1) / (R * RG);
   // front workgroups (oversize blocks): R / 2 rows for one species with fewer than 16384 (block, row) pairs of
   // them (profiles/r03_sigma_rf_sweep.txt), or for several species when some block has neither a linear guess
   // nor a directory (its slow lookups spread over more workgroups); else all R (C3 with every block guessed:
@@ -836,7 +791,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   // blocks too, so no front: a front would look them up and write their R rows a second time)
   const bool direct = uni || R == 1 || deg == 0;
   const int32_t n_fb = direct ? 0 : tr.n_sig_fb_tc;
-  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
+  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF * RG - 1) / (RF * RG));
   const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
   const PolyCoef& pc = poly_coef();
   const SigTabs4& tabv = tr.sigtab_v;
@@ -846,27 +801,38 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   const int32_t* sdir = tr.sig_dir.as<int32_t>();
   const int32_t* fb = tr.sig_fb_tc.as<int32_t>();
   PROM_REQUIRE(msp || nsig == 1, "transmission curves: one effective absorber only");
-#define PROM_TCK(NS, DG, MGV, RV, UV)                                                                         \
-  hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV>), dim3(nb), dim3(kBlock), 0, s, ev_sig0, ev_sig1, 0, tabv, \
-                        pc, wav, n_wav, n_rows, seg, seg4, sdir, fb, n_fb, n_blk, n_rc, RF, ta)
+  if (tr.tw_ok && !uni && deg > 0 && n_rows >= 2 && tr.n_tw > 0) {
+    // target windows (k_sigma_tw, prom_tw.hip)
+    launch_sigma_tw(s, tr, nsig, deg, ta, ev_sig0, ev_sig1);
+    return;
+  }
+#define PROM_TCK(NS, DG, MGV, RV, UV, RGV)                                                                         \
+  hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV, RGV>), dim3(nb), dim3(kBlock * RGV), 0, s, ev_sig0, ev_sig1, 0, \
+                        tabv, pc, wav, n_wav, n_rows, seg, seg4, sdir, fb, n_fb, n_blk, n_rc, RF, ta)
 #define PROM_TCR(NS, DG, MGV)                                       \
   do {                                                              \
-    if (uni) PROM_TCK(NS, DG, MGV, 8, true);                        \
-    else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false);               \
-    else if ((NS) == 1 && R == 4) PROM_TCK(NS, DG, MGV, 4, false);   \
-    else PROM_TCK(NS, DG, MGV, 8, false);                           \
+    if (uni) PROM_TCK(NS, DG, MGV, 8, true, 1);                     \
+    else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false, 1);            \
+    else if ((NS) == 1 && R == 4) PROM_TCK(NS, DG, MGV, 4, false, 1);   \
+    else if (RG == 2) PROM_TCK(NS, DG, MGV, 8, false, 2);           \
+    else PROM_TCK(NS, DG, MGV, 8, false, 1);                        \
   } while (0)
   // degree 8 covers every table with amax <= 0.07 (the high-resolution configs); 14 the rest (coarse tables)
 #define PROM_TCD(NS, MGV)                                                          \
-  if (deg == 0) { if (uni) PROM_TCK(NS, 0, MGV, 8, true); else PROM_TCK(NS, 0, MGV, 8, false); } \
+  if (deg == 0) { if (uni) PROM_TCK(NS, 0, MGV, 8, true, 1); else PROM_TCK(NS, 0, MGV, 8, false, 1); } \
   else if (deg <= 8) PROM_TCR(NS, 8, MGV);                                       \
   else PROM_TCR(NS, 14, MGV);
+#ifdef PROM_TC_DEV_ONE
+  // (development builds: the C3 instantiations only, for quick resource-usage checks)
+  PROM_TCR(3, 8, true);
+#else
   switch (nsig) {
     case 1: PROM_TCD(1, false) break;
     case 2: PROM_TCD(2, true) break;
     case 3: PROM_TCD(3, true) break;
     default: PROM_TCD(4, true) break;
   }
+#endif
 #undef PROM_TCD
 #undef PROM_TCR
 #undef PROM_TCK
