@@ -76,6 +76,10 @@ def parse():
                     help="strong splits (--shard, --scaling strong): contiguous wavelength ranges, orbital-phase "
                          "ranges (every wavelength, phases [o0, o1)), or auto (default): phases when every rank "
                          "gets the same number of them, else wavelengths")
+    ap.add_argument("--strong", default="C4x10,C4x10p128", metavar="CONFIGS",
+                    help="N > 1: after the main leg, also time these configurations split over the N ranks in "
+                         "contiguous wavelength shards (the north-star strong-scaling axis; the line's `strong` "
+                         "object, with each one's full grid timed on rank 0 alone for the speedup); '' to skip")
     ap.add_argument("--no-projection", action="store_true",
                     help="skip the strong-scaling projection (C4x10 and C5, full grid vs shard 0 of 8)")
     ap.add_argument("--kernel-runs", type=int, default=20,
@@ -328,6 +332,53 @@ def strong_projection(dev_id: int, names=("C4x10", "C4x10p64", "C5"), parts: int
                      "phase_shard": {"phases": [pa, pb], "ms_shard": t_pshard,
                                      "projected_speedup": t_full / t_pshard, "kernel_ms_shard": k_pshard}}
         del tr
+    return out
+
+
+def strong_leg(name: str, dev_id: int, dist, rank: int, world: int, steps: int, warmup: int, dump_dir=None):
+    """Strong scaling on the wavelength axis inside the N-rank process group (BASELINE.json configs[3]:
+    the torus exosphere wavelength-sharded across the GPUs; memoryHandler.py:55-66 is the chunker this replaces):
+    the configuration's grid in N contiguous 256-aligned wavelength shards, one per rank, barrier + max-over-ranks
+    timing as the main leg; then its full grid on rank 0 alone (the others wait at a barrier), the one-GPU time the
+    speedup is taken against."""
+    from prometheus_amd import _native, configs, setupfile, sharding
+    tr = setupfile.build_transit(configs.get(name))
+    dev = _native.get_device(dev_id)
+    host = tr._host_inputs()
+    n = len(tr.wavelength)
+    n_orb = len(host["orb"])
+    w0, w1 = sharding.shard_for_rank(n, world, rank)
+    dev.transit_set(tr._problem(dev, host, w0, w1, 0.0))
+    dev.transit_run()
+    dev.synchronize()
+    for _ in range(warmup):
+        dev.transit_run()
+    dev.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dev.transit_run()
+    dev.synchronize()
+    t1 = time.perf_counter()
+    dist.barrier()
+    elapsed, total_pts = sharding.reduce_timing(dist, t1 - t0, (w1 - w0) * n_orb)
+    if dump_dir:
+        os.makedirs(dump_dir, exist_ok=True)
+        np.save(os.path.join(dump_dir, "R_rank%d.npy" % rank), dev.transit_result())
+        with open(os.path.join(dump_dir, "range_rank%d.json" % rank), "w") as fh:
+            json.dump({"w0": int(w0), "w1": int(w1), "n_wav": int(n), "o0": 0, "o1": int(n_orb),
+                       "n_orb": int(n_orb), "world": world}, fh)
+    ms_full = None
+    if rank == 0:
+        ms_full = time_runs(dev, tr._problem(dev, host, 0, n, 0.0), steps, warmup)
+    dist.barrier()
+    ms_step = elapsed / steps * 1e3
+    out = {"workload": "%s (%s), %d wavelengths x %d phases, %d contiguous wavelength shards (256-aligned), one per "
+                       "rank" % (name, describe(configs.get(name)), n, n_orb, world),
+           "axis": "wavelength", "value": total_pts * steps / elapsed, "unit": "spectrum points/s",
+           "ms_per_step": ms_step, "steps": steps, "warmup": warmup,
+           "ms_full_grid_one_gpu": ms_full, "speedup_vs_one_gpu": (ms_full / ms_step) if ms_full else None}
+    del tr
     return out
 
 
@@ -626,6 +677,14 @@ def main():
     }
     if proj is not None:
         result["strong_scaling_projection"] = proj
+    if dist and args.strong and not args.shard:
+        # (after the main leg; its problem is released first)
+        del prob
+        strong = {}
+        for name in [c for c in args.strong.split(",") if c]:
+            strong[name] = strong_leg(name, dev_id, dist, rank, world, args.steps, args.warmup,
+                                      os.path.join(args.dump_R, "strong_" + name) if args.dump_R else None)
+        result["strong"] = strong
     if cpu is not None:
         result["cpu_baseline"] = cpu
     if dist:

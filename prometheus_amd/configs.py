@@ -107,6 +107,14 @@ def c4x10p64():
     return cfg
 
 
+def c4x10p128():
+    """C4x10 at 128 orbital phases (2.4e8 spectrum points): the >= 1 ms one-GPU strong-scaling workload of the
+    N > 1 bench line (bench.py `strong`), split over the ranks by wavelength."""
+    cfg = c4x10()
+    cfg["Grids"]["orbphase_steps"] = 128
+    return cfg
+
+
 def c5():
     """hydrostatic + synthetic H2O table, 1-2 micron at 1e-10 cm (1e6 points), 32 phases."""
     return {"Fundamentals": _fund(False),
@@ -172,7 +180,8 @@ def synthetic_mdot(path, n=40, seed=5):
 TIDAL = {"q": 3.34, "tau": 1.2e4, "mass": 22.99 * _AMU, "sigma_v": 10. * _KMS}
 
 
-PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C4x10p64": c4x10p64, "C5": c5, "exomoon": exomoon}
+PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C4x10p64": c4x10p64, "C4x10p128": c4x10p128,
+           "C5": c5, "exomoon": exomoon}
 
 
 def get(name: str) -> dict:

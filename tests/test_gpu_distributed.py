@@ -135,3 +135,28 @@ def test_two_rank_weak_default_over_phases(tmp_path):
         R[o0:o1] = part
     assert np.allclose(R, R1, rtol=1e-13, atol=0)
     assert abs(res2["value"] * res2["ms_per_step"] * 1e-3 - 16 * R1.shape[1]) / (16 * R1.shape[1]) < 1e-9
+
+
+def test_two_rank_line_carries_strong_wavelength_split(tmp_path):
+    """Every N > 1 line carries `strong`: configurations split over the ranks in contiguous wavelength shards (the
+    north-star axis, BASELINE.json configs[3]), timed in the same process group, with the full grid on rank 0 alone
+    for the speedup.  Two ranks, weak main leg (C4 over phases) and a strong C4 leg: the strong shards gathered on
+    the host are bitwise a single-rank run of C4."""
+    res1, (s1,) = _bench(str(tmp_path), 1, "C4")
+    res2, _ = _bench(str(tmp_path), 2, "C4", axis="auto", scaling=("--strong", "C4"))
+    st = res2["strong"]["C4"]
+    assert res2["scaling"] == "weak" and st["axis"] == "wavelength"
+    assert st["value"] > 0 and st["ms_per_step"] > 0 and st["ms_full_grid_one_gpu"] > 0 and st["speedup_vs_one_gpu"] > 0
+    assert "2 contiguous wavelength shards" in st["workload"]
+    out = os.path.join(str(tmp_path), "w2_auto_--strong_C4", "strong_C4")
+    R = np.full_like(s1[2], np.nan)
+    edge = 0
+    for r in range(2):
+        with open(os.path.join(out, "range_rank%d.json" % r)) as fh:
+            rg = json.load(fh)
+        part = np.load(os.path.join(out, "R_rank%d.npy" % r))
+        assert rg["w0"] == edge and part.shape == (R.shape[0], rg["w1"] - rg["w0"])
+        R[:, rg["w0"]:rg["w1"]] = part
+        edge = rg["w1"]
+    assert edge == R.shape[1]
+    assert np.array_equal(R, s1[2])
