@@ -8,7 +8,8 @@ with Na I + Ca II + Mg I, orbital Doppler shift on, 351,222 wavelengths x 16 orb
 2,400 chords x 30 samples, WASP-49b).  One step = one pass of the hot path over the whole spectrum
 with all inputs resident in HBM (prom_transit_run): on the default transmission-curve path
 k_columns8 (densities, column densities, culling), k_tc_build (every phase's transmission curve
-T_o) and k_sigma_tc (sigma of the merged absorber at every phase's Doppler shift, R = T_o(Y));
+T_o) and k_sigma_tw (sigma of the merged absorber at every phase's Doppler shift over target windows,
+R = T_o(Y); k_sigma_tc without orbital Doppler shift between the phases);
 several unmerged species take the windowed path (k_order, k_tau_w / k_tau_p), molecules k_tau_mol.
 --config C2 gives the configs[1] line.
 
@@ -487,7 +488,9 @@ def main():
     tv = st.get("tau_kernel_variant", 0) // 10
     fused = tv in (5, 6)
     sig_tau = tv == 7
-    tcurve = tv == 8
+    tcurve = tv in (8, 9)
+    # 9: the same with the Doppler-shifted lookups over target windows (prom_tw.hip: k_sigma_tw)
+    sig_name = "k_sigma_tw" if tv == 9 else "k_sigma_tc"
     mol = bool(getattr(prob, "n_molecules", 0))
     tau_kernel = "k_tau_mol" if mol else {2: "k_tau_w", 3: "k_tau_p", 4: "k_tau_rm"}.get(tv, "k_tau")
     # k_tau_p in the pipelined loop: its span on the device clock (first workgroup start -> last workgroup end)
@@ -559,7 +562,7 @@ def main():
             # transmission curves: R written (every point), the wavelengths and the table nodes read; the
             # per-phase curve tables (kTcD coefficients per octave) are L2-resident and not counted
             sig_bytes = 8 * n_orb * n_w + 8 * n_w + 16 * nodes
-            kernels["k_sigma_tc"] = dict(hbm(sig_bytes, kms["sigma"]), ms=kms["sigma"], lookups=lookups,
+            kernels[sig_name] = dict(hbm(sig_bytes, kms["sigma"]), ms=kms["sigma"], lookups=lookups,
                                          table_nodes=nodes, lookups_per_s=lookups / (kms["sigma"] * 1e-3))
         elif sig_tau:
             # fused rows: R written (every point but the heavy half tiles' -- counted whole), the wavelengths and
@@ -597,7 +600,7 @@ def main():
     # rocprofv3 kernel names: the fused rows are k_sigma_poly<..., true>, the row kernels k_sigma_poly<..., false>
     # (or k_sigma_rows)
     sym, suffix = {"k_sigma_tau": ("prom::k_sigma_poly", ", true>"), "k_sigma": ("prom::k_sigma", ""),
-                   "k_sigma_tc": ("prom::k_sigma_tc", "")}.get(dom, ("prom::" + dom, ""))
+                   "k_sigma_tc": ("prom::k_sigma_tc", ""), "k_sigma_tw": ("prom::k_sigma_tw", "")}.get(dom, ("prom::" + dom, ""))
     traffic = latest_profile_traffic(sym, cfg_name, suffix)
     # latency of one run alone on an idle device (host clock: submit, kernels, synchronize; no stats
     # instrumentation), median of 20 -- what one retrieval sample waits for with inputs resident; not `value`

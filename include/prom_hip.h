@@ -224,7 +224,10 @@ typedef struct prom_transit_stats {
                                     3  planned windowed integration k_tau_p (k_order + k_windows heavy lists);
                                     4  stellar spectrum / CLV / RM rotation k_tau_rm;
                                     8  transmission curves, the default for one effective absorber:
-                                       k_columns8 -> k_tc_build -> k_sigma_tc (prom_tcurve.hip)          */
+                                       k_columns8 -> k_tc_build -> k_sigma_tc (prom_tcurve.hip; no orbital
+                                       Doppler shift between the phases, one phase, or coarse tables);
+                                    9  transmission curves with the Doppler-shifted lookups over target
+                                       windows: k_columns8 -> k_tc_build -> k_sigma_tw (prom_tw.hip)       */
   int32_t tau_kernel_variant_exact_phases;  /* phases integrated on the exact (ocml) path because a
                                                column density was not finite                      */
 } prom_transit_stats;

@@ -69,7 +69,8 @@ KERNEL_IDS = ("columns", "sigma", "order", "windows", "tau", "tc_build", "sigma_
 # prom_transit_stats.tau_kernel_variant // 10 -> the integration path the run took (prom_hip.h)
 VARIANT_PATHS = {0: "k_tau (ocml exp, validation)", 1: "k_tau / k_tau_mol (table exp)", 2: "k_tau_w (windowed)",
                  3: "k_tau_p (planned windows)", 4: "k_tau_rm (stellar spectrum)",
-                 8: "k_tc_build + k_sigma_tc (transmission curves)"}
+                 8: "k_tc_build + k_sigma_tc (transmission curves)",
+                 9: "k_tc_build + k_sigma_tw (transmission curves, target-window lookups)"}
 OPT_OCML_EXP = 1
 OPT_NO_MERGE = 2
 OPT_NO_WINDOW = 4

@@ -115,6 +115,21 @@ def c4x10p128():
     return cfg
 
 
+def c2moon():
+    """Two density scenarios at C2 size (190,205 wavelengths x 8 phases x 2,400 chords): barometric Na I + K I and a
+    moon exosphere of Na I, orbital Doppler shift on -- the planet's and the moon's Doppler factors, chords blocked by
+    the moon.  The optical depths of the scenarios add (gasProperties.py:906-954) and cannot merge into one absorber,
+    so the run takes the windowed path (k_order, k_tau_p) rather than the transmission curves."""
+    _, Rp, _ = _system()
+    return {"Fundamentals": dict(_fund(True), ExomoonSource=True),
+            "Scenarios": {"barometric": {"T": 3000., "P_0": 1e4, "mu": 2.3 * _AMU}, "exomoon": {"q_moon": 3.34}},
+            "Architecture": {"planetName": "WASP-49b", "R_moon": 1.822e8, "a_moon": 1.44 * Rp,
+                             "starting_orbphase_moon": 0.65 * 2. * 3.141592653589793},
+            "Species": {"barometric": {"NaI": {"chi": 1e-6}, "KI": {"chi": 1e-6}},
+                        "exomoon": {"NaI": {"sigma_v": 10. * _KMS, "Nparticles": 1e32}}},
+            "Grids": _grids(5880e-8, 7710e-8, 1e-10, 1e-11)}
+
+
 def c5():
     """hydrostatic + synthetic H2O table, 1-2 micron at 1e-10 cm (1e6 points), 32 phases."""
     return {"Fundamentals": _fund(False),
@@ -181,7 +196,7 @@ TIDAL = {"q": 3.34, "tau": 1.2e4, "mass": 22.99 * _AMU, "sigma_v": 10. * _KMS}
 
 
 PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C4x10p64": c4x10p64, "C4x10p128": c4x10p128,
-           "C5": c5, "exomoon": exomoon}
+           "C5": c5, "C2moon": c2moon, "exomoon": exomoon}
 
 
 def get(name: str) -> dict:

@@ -893,10 +893,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       seg_key_keep = seg_reuse;   // the stored key stays as it is (re-validated at the end)
       if (!seg_reuse) tr.tw_ok = false;
       // target windows (k_sigma_tw, prom_window.hip): every atomic slot on one set of Doppler factors (one scenario),
-      // n_orb >= 2; built with the sigma segments (the same inputs) and kept when they are reused.  PROM_TW=0 (read at
-      // every set): none, k_sigma_tc's wavelength blocks
+      // n_orb >= 2; built with the sigma segments (the same inputs) and kept when they are reused.  By default for one
+      // atomic species (C4x10: k_sigma_tw 52 against k_sigma_tc's 60 us); several merged species keep k_sigma_tc's
+      // wavelength blocks (C3: 36.7 against 31.7 us isolated, equal pipelined steps).  PROM_TW (read at
+      // every set): 0 never, 1 always
       const char* e_tw = std::getenv("PROM_TW");
-      const bool tw_off = e_tw && std::atoi(e_tw) == 0;
+      const bool tw_off = (e_tw && std::atoi(e_tw) == 0) || (!(e_tw && std::atoi(e_tw) == 1) && n_atoms != 1);
       auto build_tw = [&]() {
         tr.tw_ok = false;
         tr.n_tw = 0;
@@ -911,28 +913,34 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
           tabs.push_back(&ctx->tables[t.table].hx);
         }
         if (!one || sc_tw < 0 || tw_off) return;
-        // (profiling knobs, read once: wavelengths per row, points per window, pool nodes)
+        // (profiling knobs, read once: wavelengths per row, points per window, LDS doubles per workgroup)
         static const int rowcap = [] { const char* e = std::getenv("PROM_TW_ROWCAP"); return e ? std::max(1, std::atoi(e)) : 256; }();
         static const int64_t pmax = [] { const char* e = std::getenv("PROM_TW_PMAX"); return e ? std::max(1, std::atoi(e)) : 8192; }();
-        static const int pool = [] {
-          const char* e = std::getenv("PROM_TW_POOL");
-          return e ? std::max(2, std::min(prom::kTwPoolMax, std::atoi(e))) : prom::kTwPoolMax;
+        static const int lamcap = [] {   // (wavelengths staged per window at most; 0: never)
+          const char* e = std::getenv("PROM_TW_LAMCAP");
+          return e ? std::max(0, std::min(prom::kTwLamCap, std::atoi(e))) : prom::kTwLamCap;
+        }();
+        static const int lds = [] {
+          const char* e = std::getenv("PROM_TW_LDS");
+          return e ? std::max(16, std::min(prom::kTwLds, std::atoi(e))) : prom::kTwLds;
         }();
         std::vector<prom::SigSeg> twseg;
-        std::vector<int32_t> twrow;
+        std::vector<int32_t> twrow, twlam;
         int32_t nw = 0;
         if (!prom::build_target_windows(pb->wavelength, tr.n_wav, sh.data() + (int64_t)sc_tw * n_orb, (int32_t)n_orb, tabs,
-                                        pool, rowcap, pmax, twseg, twrow, nw))
+                                        lds, lamcap, rowcap, pmax, twseg, twrow, twlam, nw))
           return;
         stg.add(tr.tw_seg, twseg.data(), (int64_t)twseg.size(), s);
         stg.add(tr.tw_row, twrow.data(), (int64_t)twrow.size(), s);
+        stg.add(tr.tw_lam, twlam.data(), (int64_t)twlam.size(), s);
         tr.n_tw = nw;
         tr.tw_ok = true;
+        tr.tw_new = true;
         if (std::getenv("PROM_DEBUG")) {
-          int64_t k1 = 0, k2 = 0, k0 = 0;
-          for (const auto& e : twseg) ((e.kind & 3) == 1 ? k1 : (e.kind & 3) == 2 ? k2 : k0) += 1;
-          std::fprintf(stderr, "[prom] target windows: %d (slices: %lld staged, %lld global, %lld searched)\n", nw,
-                       (long long)k1, (long long)k2, (long long)k0);
+          int64_t k[4] = {0, 0, 0, 0};
+          for (const auto& e : twseg) k[e.kind & 3] += 1;
+          std::fprintf(stderr, "[prom] target windows: %d (slices: %lld staged, %lld global, %lld staged unguessed, "
+                       "%lld outside the table)\n", nw, (long long)k[1], (long long)k[2], (long long)k[3], (long long)k[0]);
         }
       };
       if (seg_reuse) {
@@ -1330,6 +1338,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
     tr.last = 0;
     stg.flush(ctx, s);
     if (tr.star) prom::launch_rm_fout(s, tr);   // per set: the unocculted flux of every wavelength
+    if (tr.tw_new) {
+      // windows built by this call: mark the slices whose guess is numpy's bracket at every target (PROM_TW_EXACT=0:
+      // never, for comparisons)
+      const char* e_ex = std::getenv("PROM_TW_EXACT");
+      if (!(e_ex && std::atoi(e_ex) == 0)) prom::launch_tw_exact(s, tr, n_atoms);
+      tr.tw_new = false;
+    }
     if (seg_key_new) {
       // segments built by this call: mark those whose guess is numpy's bracket for every target
       const int64_t nb = (tr.n_wav + prom::kSigBlockW - 1) / prom::kSigBlockW;

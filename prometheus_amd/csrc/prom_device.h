@@ -156,7 +156,7 @@ __device__ __forceinline__ int32_t seg_guess(double t, double b, double inv, int
   // map (prom_api.hip sigma segments).  Every target lies in the slice, so f is within rounding of
   // [0, m - 1] and truncating first, clamping the integer after, gives the same g
   const int32_t g = (int32_t)__builtin_fma(t, inv, b);
-  return g < 0 ? 0 : (g > m - 2 ? m - 2 : g);
+  return max(min(g, m - 2), 0);   // (one v_med3_i32; m >= 2)
 }
 
 struct InvFact {

@@ -89,7 +89,8 @@ constexpr int kSigSeg = PROM_SIG_SEG;
 // wavelengths at 0.001 A under a 0.6 A Doppler spread) stay in LDS instead of the global-record front path.  Host
 // segments mark slices within the cap SigSeg kind & 64.
 constexpr int tc_slice_cap(int nsig) { return nsig <= 1 ? 1024 : (nsig == 2 ? 640 : kSigSeg); }
-constexpr int kTwPoolMax = 800;   // k_sigma_tw: table nodes staged per target window, all species (kTwPool)
+constexpr int kTwLds = 2560;      // k_sigma_tw: LDS doubles per workgroup (20 KB): staged nodes (3 each) + wavelengths
+constexpr int kTwLamCap = 1024;   // ... wavelengths staged per window at most
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
 #ifndef PROM_SIG_ROWS
 #define PROM_SIG_ROWS 8
@@ -377,8 +378,10 @@ struct TransitDev {
   // per window boundary and row the first wavelength; built with the sigma segments (same inputs, same reuse)
   DevBuf tw_seg;                            // [n_tw][n_atoms] SigSeg
   DevBuf tw_row;                            // [n_tw + 1][n_orb] int32
+  DevBuf tw_lam;                            // [n_tw][2] int32: the wavelengths [lw0, lw1) staged per window (lw1 = lw0: none)
   int32_t n_tw = 0;
   bool tw_ok = false;
+  bool tw_new = false;                      // (built by this set: the exact marks are still to come)
   // polynomial sigma rows (k_sigma_poly): degree D of the e^a Taylor polynomial for this problem's tables
   // (0: the exp10 path, k_sigma_rows; PROM_SIG_POLY=0 forces it)
   int32_t sig_deg = 0;
@@ -403,6 +406,7 @@ struct TransitDev {
   hipGraphExec_t gexec[kMaxSlots] = {};
   bool graphs = false;
   int depth = 1;                            // slots in use: fast path = pipeline depth, else 1
+  int cu_count = 0;                         // the context device's compute units (launch_tau_mol; 0: not queried yet)
   int last = 0;                             // slot of the most recent run
 };
 
@@ -467,7 +471,8 @@ void launch_seg_exact(hipStream_t s, int32_t nsig, const SigTabs4& tabv, const d
                       int32_t n_rows, SigSeg* seg, int32_t* flags);
 // the transmission-curve path after the column kernel: k_tc_build, k_sigma_tc (prom_tcurve.hip);
 // the event pairs (may be null) ride on the two kernels' dispatch packets
-void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,
+// (true: the lookups ran over target windows, k_sigma_tw)
+bool launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,
                    hipEvent_t ev_sig1, hipEvent_t ev_tb0, hipEvent_t ev_tb1);
 void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3 g, int32_t ppg);
 void launch_mol_gt(hipStream_t s, const MolSlotDev& md);
@@ -480,10 +485,13 @@ void launch_gridded(hipStream_t s, const double* g, int32_t nx, int32_t ny, int3
 // k_sigma_tw (prom_tw.hip): the lookups + curves over the problem's target windows (tr.tw_ok)
 void launch_sigma_tw(hipStream_t s, TransitDev& tr, int32_t nsig, int32_t deg, const TcArgs& ta, hipEvent_t ev0,
                      hipEvent_t ev1);
+// ... per set after new windows: mark the exact guesses (SigSeg kind |= 4)
+void launch_tw_exact(hipStream_t s, TransitDev& tr, int32_t nsig);
 // target windows of the Doppler-shifted lookups (prom_window.hip): false when the inputs do not allow them
 bool build_target_windows(const double* wav, int64_t n_wav, const double* shift, int32_t n_rows,
-                          const std::vector<const std::vector<double>*>& tabs, int32_t pool, int32_t rowcap,
-                          int64_t pmax, std::vector<SigSeg>& seg_out, std::vector<int32_t>& row_out, int32_t& n_win);
+                          const std::vector<const std::vector<double>*>& tabs, int32_t lds, int32_t lamcap,
+                          int32_t rowcap, int64_t pmax, std::vector<SigSeg>& seg_out, std::vector<int32_t>& row_out,
+                          std::vector<int32_t>& lam_out, int32_t& n_win);
 // AtomTable::rec from a table's x and y, and the per-interval |a| bounds (prom_fn.hip)
 void launch_table_recs(hipStream_t s, const double* x, const double* y, int64_t n, double4* rec, double* amax);
 void launch_scatter(hipStream_t s, const char* base, const ScatterDesc* d, int32_t n);

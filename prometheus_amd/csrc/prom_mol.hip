@@ -171,8 +171,9 @@ __global__ void __launch_bounds__(kBlock) k_tau_mol(const SigTabs4 tabv, const M
   // lambda' nodes, and a workgroup's 256 wavelengths cover a few tens of nodes at most (C5: ~6-27), so the records
   // of [st_lo, st_lo + st_n) x all intervals are copied to LDS once and the samples read them there: one 32-byte LDS
   // read pair per sample instead of two vector-L1 loads (the L1's 64 bytes per clock per CU bound the global
-  // variant, profiles/r05y_*).  Restaged when a phase's node range leaves the staged one (rarely: the Doppler
-  // factors move lambda' by ~1e-6); a range too wide for the buffer takes the global path for that phase.
+  // variant, profiles/r05y_*).  Staged once, at the group's first phase; a later phase whose node range leaves the
+  // staged one (rarely: the Doppler factors move lambda' by ~1e-6), or a range too wide for the buffer, reads those
+  // records from global memory for that phase.
   constexpr bool STG = M1 && EXPK && kMolBilin && PROM_MOL_STAGE;
   __shared__ double2 gst[STG ? kMolStageD2 : 1];
   __shared__ int32_t red[2][kBlock / 64];
@@ -565,13 +566,15 @@ void launch_tau_mol(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t na, dim3
   // profiles/r05c5b_ppg_sweep.txt: full grid 16 of 32 phases per group, a wavelength shard 8, a 4-phase shard 4;
   // the previous rule, >= 16 waves per SIMD, gave 1, 1 and 8 and a 1.8x slower shard).  PROM_MOL_PPG: fixed.
   const int64_t n_tiles = (tr.n_wav + kBlock - 1) / kBlock;
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
+  // (the CU count of this context's device, cached in its TransitDev: one host thread per device under
+  // sumOverChords(devices=...), each with its own context)
+  if (tr.cu_count <= 0) {
+    int dev = 0, n = 0;
     PROM_HIP(hipGetDevice(&dev));
-    PROM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    if (cus <= 0) cus = 256;
+    PROM_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    tr.cu_count = n > 0 ? n : 256;
   }
+  const int cus = tr.cu_count;
   const double slots = 5.0 * cus;   // (k_tau_mol's LDS: five workgroups per CU)
   int32_t ppg = 1;
   double best = 1e300;

@@ -733,7 +733,7 @@ extern "C" int32_t prom_tc_trace_read(unsigned long long* out, int32_t n, int32_
 }
 #endif
 
-void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,
+bool launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, bool msp, hipEvent_t ev_sig0,
                    hipEvent_t ev_sig1, hipEvent_t ev_tb0, hipEvent_t ev_tb1) {
   const int32_t lg = tr.tc_lg;
   unsigned long long* evals = tr.count_evals ? rs.evals.as<unsigned long long>() : nullptr;
@@ -769,10 +769,10 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   static const int r1_env = [] { const char* e = std::getenv("PROM_TC_R1"); return e ? std::atoi(e) : 0; }();
   const int Rmax = (nsig >= 2 || uni) ? 8 : (r1_env == 4 ? 4 : 8);
   const int R = (uni || deg == 0) ? 8 : (n_rows == 1 ? 1 : Rmax);
-  // row groups per workgroup (RG x 256 threads, one slice stage for RG x R rows): 2 when the rows need more than one
-  // group of R (C3: 16 phases), else 1; PROM_TC_RG (read once) forces 1 or 2
+  // row groups per workgroup (RG x 256 threads, one slice stage for RG x R rows): 1; PROM_TC_RG=2 (read once, A/B)
+  // stages a block's slice once for 16 rows
   static const int rg_env = [] { const char* e = std::getenv("PROM_TC_RG"); return e ? std::atoi(e) : 0; }();
-  int RG = (!uni && R == 8 && deg > 0 && n_rows > R) ? 2 : 1;
+  int RG = 1;   // (RG = 2 measured slower on C3: 37.7 against 32.1 us, 4 waves per SIMD at 101 VGPRs; r06b)
   if ((rg_env == 1 || rg_env == 2) && !uni && R == 8 && deg > 0) RG = rg_env;
   const int32_t n_rc = (n_rows + R * RG - 1) / (R * RG);
   // front workgroups (oversize blocks): R / 2 rows for one species with fewer than 16384 (block, row) pairs of
@@ -804,7 +804,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   if (tr.tw_ok && !uni && deg > 0 && n_rows >= 2 && tr.n_tw > 0) {
     // target windows (k_sigma_tw, prom_tw.hip)
     launch_sigma_tw(s, tr, nsig, deg, ta, ev_sig0, ev_sig1);
-    return;
+    return true;
   }
 #define PROM_TCK(NS, DG, MGV, RV, UV, RGV)                                                                         \
   hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV, RGV>), dim3(nb), dim3(kBlock * RGV), 0, s, ev_sig0, ev_sig1, 0, \
@@ -837,6 +837,7 @@ void launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
 #undef PROM_TCR
 #undef PROM_TCK
   PROM_HIP(hipGetLastError());
+  return false;
 }
 
 }  // namespace prom

@@ -2255,9 +2255,10 @@ void launch_transit(hipStream_t s, TransitDev& tr, RunSlot& rs, const std::vecto
     hipEvent_t e_tb1 = ev ? (stage_events ? ev1 : ev[2]) : nullptr;
     hipEvent_t e_sg0 = (ev && stage_events) ? ev[2] : nullptr;
     hipEvent_t e_sg1 = ev ? ev[3] : nullptr;
-    launch_tcurve(s, tr, rs, nsig, msp, kp_start(tr, PROM_K_SIGMA_TC, e_sg0), kp_stop(tr, PROM_K_SIGMA_TC, e_sg1),
-                  kp_start(tr, PROM_K_TC_BUILD, nullptr), kp_stop(tr, PROM_K_TC_BUILD, e_tb1));
-    *variant = 80 + na;
+    const bool tw = launch_tcurve(s, tr, rs, nsig, msp, kp_start(tr, PROM_K_SIGMA_TC, e_sg0),
+                                  kp_stop(tr, PROM_K_SIGMA_TC, e_sg1), kp_start(tr, PROM_K_TC_BUILD, nullptr),
+                                  kp_stop(tr, PROM_K_TC_BUILD, e_tb1));
+    *variant = tw ? 90 + na : 80 + na;
     return;
   }
   if (cols8) {

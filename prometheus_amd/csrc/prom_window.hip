@@ -10,12 +10,16 @@
 //
 // Windows are grown greedily over candidate boundaries (the targets of a reference row, extended below and above
 // by the rows with the smallest and largest factors) while every row keeps <= rowcap wavelengths, the window
-// <= pmax points and the species' slices <= pool nodes together.  Per species the slice [lo, lo + m) holds the
+// <= pmax points, and the species' slices and the wavelengths the rows read fit the workgroup's LDS (lds doubles:
+// 24 bytes a node, 8 a wavelength, <= lamcap wavelengths).  Per species the slice [lo, lo + m) holds the
 // bracket of every target in the window and a linear guess g(t) = clamp((int)fma(t, inv, xs), 0, m - 2) verified
 // (as prom_transit_set's sigma segments) to be within one node of numpy's bracket over the window's target range;
-// a window whose guess fails is shortened (bisection) and, as a single candidate interval, keeps kind 0 (the
-// table's own bracket search).  kind 1: staged at pool offset pad; 2: guess into the global records; 0: none.
+// a window whose guess fails is shortened (bisection); a single candidate interval without one (a slice across a
+// change of the table's node spacing) is searched in LDS.  kind 1: staged at pool offset pad, guessed; 2: guess into
+// the global records (slice larger than the pool); 3: staged, binary search; 0: targets outside the table (numpy's
+// end rules: the table's own search, the kernel's second pass).
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <thread>
 
@@ -67,15 +71,24 @@ bool window_slice(const std::vector<double>& X, int64_t lo, int64_t hi, double t
 struct Win {
   std::vector<int32_t> start;   // per row
   std::vector<SigSeg> seg;      // per species
+  int32_t lw0 = 0, lw1 = 0;     // the wavelengths any row of the window reads (staged with the slices)
 };
 
 }  // namespace
 
 bool build_target_windows(const double* wav, int64_t n_wav, const double* shift, int32_t n_rows,
-                          const std::vector<const std::vector<double>*>& tabs, int32_t pool, int32_t rowcap,
-                          int64_t pmax, std::vector<SigSeg>& seg_out, std::vector<int32_t>& row_out, int32_t& n_win) {
+                          const std::vector<const std::vector<double>*>& tabs, int32_t lds, int32_t lamcap,
+                          int32_t rowcap, int64_t pmax, std::vector<SigSeg>& seg_out, std::vector<int32_t>& row_out,
+                          std::vector<int32_t>& lam_out, int32_t& n_win) {
   const int NS = (int)tabs.size();
-  if (n_wav < 1 || n_wav >= INT32_MAX || n_rows < 1 || NS < 1 || NS > 4 || rowcap < 1 || pmax < 1) return false;
+  if (n_wav < 1 || n_wav >= INT32_MAX || n_rows < 1 || NS < 1 || NS > 4 || rowcap < 1 || pmax < 1 || lds < 16 ||
+      lamcap < 0)
+    return false;
+  // lamfit: grow windows only while their wavelengths fit the LDS beside the slices (else they are staged only where
+  // they happen to fit, and read from global memory elsewhere)
+  const bool lamfit = lamcap > 0 && [] { const char* e = std::getenv("PROM_TW_LAMFIT"); return e && std::atoi(e) != 0; }();
+  // LDS budget in doubles: 3 per staged node ({E, L} and x), one more x per species, one per staged wavelength
+  auto fits = [&](int64_t nodes, int64_t lam) { return 3 * nodes + NS + lam <= lds && lam <= lamcap; };
   for (int64_t w = 0; w < n_wav; ++w)
     if (!(wav[w] > 0.0) || !std::isfinite(wav[w]) || (w > 0 && !(wav[w] > wav[w - 1]))) return false;
   for (int32_t o = 0; o < n_rows; ++o)
@@ -136,14 +149,19 @@ bool build_target_windows(const double* wav, int64_t n_wav, const double* shift,
       while (e < j1) {
         const int64_t e2 = e + 1;
         const double bv = bnd(e2);
-        int64_t tot = 0, mx = 0;
+        int64_t tot = 0, mx = 0, la = INT64_MAX, lz = 0;
         for (int32_t o = 0; o < n_rows; ++o) {
           int64_t p = Pb[o];
           while (p < n_wav && tgt(o, p) < bv) ++p;
           Pt[o] = p;
           tot += p - Pa[o];
           mx = std::max(mx, p - Pa[o]);
+          if (p > Pa[o]) {
+            la = std::min(la, Pa[o]);
+            lz = std::max(lz, p);
+          }
         }
+        const int64_t lam = lz > la ? lz - la : 0;
         const double thi = t_hi(e2);
         int64_t nodes = 0;
         for (int s = 0; s < NS; ++s) {
@@ -152,7 +170,7 @@ bool build_target_windows(const double* wav, int64_t n_wav, const double* shift,
           while (h < (int64_t)X.size() - 2 && X[h + 1] <= thi) ++h;
           nodes += h + 1 - blo[s] + 1;
         }
-        if (e2 > j + 1 && (mx > rowcap || tot > pmax || nodes > pool)) break;
+        if (e2 > j + 1 && (mx > rowcap || tot > pmax || !fits(nodes, lamfit ? lam : 0))) break;
         e = e2;
         Pb.swap(Pt);
         for (int s = 0; s < NS; ++s) {
@@ -173,7 +191,10 @@ bool build_target_windows(const double* wav, int64_t n_wav, const double* shift,
           if (inr) {
             const int64_t lo = T[s].bracket(a), hi = T[s].bracket(z) + 1;
             if (window_slice(X, lo, hi, a, z, sg)) sg.kind = 2;
-            else ok = false;
+            else {
+              sg.kind = 4;   // (in range, no guess: staged and searched when it fits the pool)
+              ok = false;
+            }
           }
           if (commit) wn.seg[s] = sg;
         }
@@ -192,14 +213,30 @@ bool build_target_windows(const double* wav, int64_t n_wav, const double* shift,
         if (e > K) for (int32_t o = 0; o < n_rows; ++o) Pb[o] = n_wav;
       }
       try_e(e, true);
+      // the wavelengths the window's rows read
+      int64_t la = INT64_MAX, lz = 0;
+      for (int32_t o = 0; o < n_rows; ++o)
+        if (Pb[o] > Pa[o]) {
+          la = std::min(la, Pa[o]);
+          lz = std::max(lz, Pb[o]);
+        }
+      const int64_t lam = lz > la ? lz - la : 0;
+      wn.lw0 = lz > la ? (int32_t)la : 0;
+      int64_t need = 0;   // (the slices come first; the wavelengths are staged only in what LDS they leave)
+      for (int s = 0; s < NS; ++s)
+        if (wn.seg[s].kind == 2 || wn.seg[s].kind == 4) need += wn.seg[s].m;
+      wn.lw1 = fits(need, lam) ? (int32_t)(wn.lw0 + lam) : wn.lw0;   // (lw1 = lw0: global loads)
+      const int64_t pool = (lds - NS - (wn.lw1 - wn.lw0)) / 3;
       // pool offsets for the guessed slices, species order, while they fit
       int32_t off = 0;
       for (int s = 0; s < NS; ++s) {
         SigSeg& sg = wn.seg[s];
-        if (sg.kind == 2 && off + sg.m <= pool) {
-          sg.kind = 1;
+        if ((sg.kind == 2 || sg.kind == 4) && off + sg.m <= pool) {
+          sg.kind = sg.kind == 2 ? 1 : 3;
           sg.pad = off;
           off += sg.m;
+        } else if (sg.kind == 4) {
+          sg.kind = 0;
         }
       }
       int64_t tot = 0;
@@ -225,11 +262,14 @@ bool build_target_windows(const double* wav, int64_t n_wav, const double* shift,
   }
   seg_out.clear();
   row_out.clear();
+  lam_out.clear();
   n_win = 0;
   for (auto& p : parts)
     for (auto& wn : p) {
       row_out.insert(row_out.end(), wn.start.begin(), wn.start.end());
       seg_out.insert(seg_out.end(), wn.seg.begin(), wn.seg.end());
+      lam_out.push_back(wn.lw0);
+      lam_out.push_back(wn.lw1);
       ++n_win;
     }
   for (int32_t o = 0; o < n_rows; ++o) row_out.push_back((int32_t)n_wav);

@@ -147,10 +147,15 @@ def test_molecular_mirror_merging(dev, monkeypatch):
     (k_mol_list): R with merging agrees with the unmerged R to 1e-13 and with the reference's golden R."""
     d = load("transit_C5r")
     tr = _product_transit(json.loads(str(d["config"])))
+    tr.collect_stats = True
     R_m = tr.sumOverChords(devices=[0])
+    ev_m = tr.last_stats[-1]["exp_evals"]
     monkeypatch.setenv("PROM_MOL_MIRROR", "0")
     R_u = tr.sumOverChords(devices=[0])
-    print("C5r mirror merging: rel diff %.3e, vs golden %.3e / %.3e" % (rel(R_m, R_u), rel(R_m, d["R"]), rel(R_u, d["R"])))
+    ev_u = tr.last_stats[-1]["exp_evals"]
+    print("C5r mirror merging: rel diff %.3e, vs golden %.3e / %.3e, evaluations %d -> %d"
+          % (rel(R_m, R_u), rel(R_m, d["R"]), rel(R_u, d["R"]), ev_u, ev_m))
+    assert ev_m < ev_u   # (pairs were merged: fewer 10^v evaluations)
     assert rel(R_m, R_u) < 1e-13
     assert rel(R_m, d["R"]) < R_TOL and rel(R_u, d["R"]) < R_TOL
 
@@ -168,13 +173,21 @@ def test_molecular_lds_stage_matches_global_reads(dev, monkeypatch):
 
 
 def test_molecular_pipelined_runs(dev):
-    """Molecular runs rotate over the pipeline slots (per-slot samples and lists): every run's R is the same."""
+    """Molecular runs rotate over the pipeline slots (per-slot samples and lists): every run's R is the same, with
+    the runs issued back to back (several in flight on the slots' streams) before one result is read."""
     d = load("transit_C5r")
     tr = _product_transit(json.loads(str(d["config"])))
-    R = [tr.sumOverChords(devices=[0]) for _ in range(6)]
+    R = [tr.sumOverChords(devices=[0]) for _ in range(3)]
     for r in R[1:]:
         assert np.array_equal(r, R[0])
     assert rel(R[0], d["R"]) < R_TOL
+    host = tr._host_inputs()
+    prob = tr._problem(dev, host, 0, len(tr.wavelength), 0.0)
+    dev.transit_set(prob)
+    for _ in range(7):   # (> the 4 pipeline slots: every slot reused while earlier runs may still be in flight)
+        dev.transit_run()
+    Rp = dev.transit_result()
+    assert np.array_equal(Rp, R[0])
 
 
 @pytest.mark.parametrize("name", ["C1", "C2r", "C4r", "exomoon"])
@@ -419,7 +432,7 @@ def test_species_merge(dev, name, monkeypatch):
     st_s = tr.last_stats[-1]
     print(name, "variants", st_m["tau_kernel_variant"], st_s["tau_kernel_variant"],
           "exp evals %d -> %d" % (st_s["exp_evals"], st_m["exp_evals"]), "max rel diff %.3e" % rel(R_m, R_s))
-    assert st_m["tau_kernel_variant"] == 81 and st_s["tau_kernel_variant"] == 32
+    assert st_m["tau_kernel_variant"] in (81, 91) and st_s["tau_kernel_variant"] == 32
     assert rel(R_m, R_s) < 1e-13
     if name != "C2":
         assert rel(R_m, load("transit_" + name)["R"]) < R_TOL
@@ -488,7 +501,7 @@ def test_nonfinite_columns_exact_path(dev, plan, monkeypatch):
     print("plan", plan, "exact phases", st["exact_phases"], "NaN points", int(np.isnan(Ro).sum()), "variant",
           st["tau_kernel_variant"])
     assert st["exact_phases"] == 1
-    assert (st["tau_kernel_variant"] == 81) == tcurve
+    assert (st["tau_kernel_variant"] in (81, 91)) == tcurve
     assert np.array_equal(np.isnan(R), np.isnan(Ro))
     m = ~np.isnan(Ro)
     assert rel(R[m], Ro[m]) < R_TOL

@@ -54,7 +54,7 @@ def test_tcurve_default_and_golden(dev, name):
     tr.collect_stats = True
     R = tr.sumOverChords(devices=[0])
     st = tr.last_stats[-1]
-    assert st["tau_kernel_variant"] == 81, st   # the transmission-curve path took the run
+    assert st["tau_kernel_variant"] in (81, 91), st   # the transmission-curve path took the run
     assert rel(R, d["R"]) < R_TOL
 
 
@@ -92,7 +92,7 @@ def test_tcurve_against_previous_path(dev, name, monkeypatch):
     tr = _transit(cfg)
     tr.collect_stats = True
     R0 = tr.sumOverChords(devices=[0])
-    assert tr.last_stats[-1]["tau_kernel_variant"] != 81
+    assert tr.last_stats[-1]["tau_kernel_variant"] not in (81, 91)
     assert float(np.max(np.abs(R - R0))) < 1e-13
 
 
@@ -126,7 +126,7 @@ def test_tcurve_exp10_lookups(dev, name, monkeypatch):
     tr = _transit(cfg)
     tr.collect_stats = True
     R0 = tr.sumOverChords(devices=[0])
-    assert tr.last_stats[-1]["tau_kernel_variant"] == 81
+    assert tr.last_stats[-1]["tau_kernel_variant"] in (81, 91)
     assert rel(R0, R) < 1e-13
     assert rel(R0, d["R"]) < R_TOL
 

@@ -4,7 +4,8 @@ cross-section lookups of the transmission-curve path grouped by target value ins
 Every lookup evaluates fl(chi E_k) e^a of numpy's bracket k (gasProperties.py:941-954 via n_interp_log,
 :34-51), whatever window, slice kind or pass it falls in, so R must be BITWISE the wavelength-block kernel's
 (k_sigma_tc, PROM_TW=0) -- on the golden configs, at full size (C3, C4, C4x10), for wavelength shards and with
-the host's window caps forced small (many windows, slices on the global-record and searched paths).
+the host's window caps forced small (many windows, slices on the global-record and searched paths).  The windows
+are the default for one atomic species; PROM_TW=1 forces them for C3's three merged species.
 """
 import numpy as np
 import pytest
@@ -29,6 +30,7 @@ def _windows_line(capfd):
 @pytest.mark.parametrize("name", ["C3", "C4", "exomoon"])
 def test_windows_bitwise_reduced(name, monkeypatch, capfd):
     monkeypatch.setenv("PROM_DEBUG", "1")
+    monkeypatch.setenv("PROM_TW", "1")   # (the default for one species; forced for C3's three)
     tr = _transit(name, reduced=True)
     R = tr.sumOverChords(devices=[0])
     line = _windows_line(capfd)
@@ -42,6 +44,7 @@ def test_windows_bitwise_reduced(name, monkeypatch, capfd):
 @pytest.mark.parametrize("name", ["C3", "C4", "C4x10"])
 def test_windows_bitwise_full_size(name, monkeypatch, capfd):
     monkeypatch.setenv("PROM_DEBUG", "1")
+    monkeypatch.setenv("PROM_TW", "1")
     tr = _transit(name)
     R = tr.sumOverChords(devices=[0])
     line = _windows_line(capfd)
@@ -52,23 +55,30 @@ def test_windows_bitwise_full_size(name, monkeypatch, capfd):
     assert np.array_equal(R, R0)
 
 
-def test_windows_shards_bitwise():
+def test_windows_shards_bitwise(monkeypatch):
     """Wavelength shards build their own windows; R is bitwise the one-shard R."""
+    monkeypatch.setenv("PROM_TW", "1")
     tr = _transit("C4x10")
     R1 = tr.sumOverChords(devices=[0])
     assert np.array_equal(R1, tr.sumOverChords(devices=[0, 0, 0]))
 
 
-@pytest.mark.parametrize("caps", [("8", "64", "800"), ("4", "32", "24"), ("256", "8192", "2")])
+@pytest.mark.parametrize("caps", [("8", "64", "2560"), ("4", "32", "96"), ("256", "8192", "16"),
+                                  ("256", "8192", "2560", "0"), ("256", "8192", "2560", "1024", "1"),
+                                  ("256", "8192", "2560", "0", "0", "0")])
 def test_windows_small_caps_bitwise(caps, monkeypatch, capfd):
-    """Window caps (wavelengths per row, points per window, pool nodes) in a fresh process each: tiny windows,
-    slices over the pool (global records, kind 2) and a 2-node pool (almost every slice global).  The caps are
-    read once per process, so each case runs in a subprocess."""
+    """Window caps (wavelengths per row, points per window, LDS doubles[, staged wavelengths, windows grown only while
+    their wavelengths fit, exact-guess marks]) in a fresh process each: tiny windows, slices over the LDS budget (global
+    records, kind 2), a 16-double budget (almost every slice global), wavelengths never staged / always staged, the
+    bracket test on every lookup.  The knobs are read once per process, so each case runs in a subprocess."""
     import json
     import os
     import subprocess
     import sys
-    env = dict(os.environ, PROM_TW_ROWCAP=caps[0], PROM_TW_PMAX=caps[1], PROM_TW_POOL=caps[2], PROM_DEBUG="1")
+    env = dict(os.environ, PROM_TW_ROWCAP=caps[0], PROM_TW_PMAX=caps[1], PROM_TW_LDS=caps[2], PROM_DEBUG="1",
+               PROM_TW="1")
+    for k, v in zip(("PROM_TW_LAMCAP", "PROM_TW_LAMFIT", "PROM_TW_EXACT"), caps[3:]):
+        env[k] = v
     code = (
         "import numpy as np, json, os\n"
         "from prometheus_amd import configs, setupfile\n"

@@ -86,6 +86,7 @@ def test_header_documents_kernel_ids_and_variants():
     src = "".join(open(os.path.join(root, "prometheus_amd", "csrc", f)).read()
                   for f in ("prom_transit.hip", "prom_mol.hip", "prom_tcurve.hip"))
     launched = {int(v) // 10 for v in re.findall(r"\*variant = (\d+)", src)}
+    launched |= {int(v) // 10 for v in re.findall(r"\*variant = tw \? (\d+) \+ na : (?:\d+)", src)}
     launched |= {1, 2}   # *variant = na + (exp_mode ? (windowed ? 20 : 10) : 0)
     assert launched <= documented, launched - documented
     call = src[src.index("launch_tcurve(s, tr, rs"):]

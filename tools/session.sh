@@ -32,7 +32,7 @@ if has extra; then
 fi
 if has stats; then
   (cd /tmp && PROM_PIPELINE=${PIPE:-4} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_$CFG -o run --output-format csv -- \
-     python3 $GRAFT_REPO_ROOT/bench.py --config $CFG --no-cpu-baseline --steps 50 --warmup 5 > $O/stats_$CFG.log 2>&1) \
+     python3 $GRAFT_REPO_ROOT/bench.py --config $CFG --no-cpu-baseline --no-projection --steps 50 --warmup 5 > $O/stats_$CFG.log 2>&1) \
     || { tail -20 $O/stats_$CFG.log; exit 1; }
   python3 tools/kstats.py $O/stats_$CFG/run_kernel_stats.csv
 fi
@@ -40,7 +40,7 @@ if has traffic; then
   mkdir -p $O/traffic_$CFG
   for c in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/traffic_$CFG/$c -o $c -- \
-       python3 $GRAFT_REPO_ROOT/bench.py --config $CFG --no-cpu-baseline --steps 10 --warmup 2 > $O/traffic_$CFG/$c.log 2>&1) \
+       python3 $GRAFT_REPO_ROOT/bench.py --config $CFG --no-cpu-baseline --no-projection --steps 10 --warmup 2 > $O/traffic_$CFG/$c.log 2>&1) \
       || { echo "$c pass failed"; exit 1; }
   done
   python3 tools/traffic_summary.py $O/traffic_$CFG > $O/traffic_$CFG/summary.json && grep -A6 "k_tau\|k_columns8\|k_order\|k_sig" $O/traffic_$CFG/summary.json | head -40
