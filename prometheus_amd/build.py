@@ -17,8 +17,10 @@ ARCH = os.environ.get("PROM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=" + ARCH, "-ffp-contract=off", "-fPIC", "-Wall",
          "-Wno-unused-function"]
 OBJDIR = os.path.join(HERE, "build")
-# per-source flags: k_sigma_tw without machine LICM (its rare passes' hoisted constants set the register peak)
-SRC_FLAGS = {"csrc/prom_tw.hip": ["-mllvm", "-disable-machine-licm"]}
+# per-source flags (none at present; PROM_BUILD_NO_SRC_FLAGS drops them for A/B variant builds)
+SRC_FLAGS = {}
+if os.environ.get("PROM_BUILD_NO_SRC_FLAGS"):   # (variant builds, A/B of the per-source flags)
+    SRC_FLAGS = {}
 
 
 def hipcc() -> str:

@@ -48,6 +48,29 @@ __device__ __forceinline__ double tc_clenshaw(double q, const double* __restrict
   return __builtin_fma(u, b1, c0 - b2);
 }
 
+// The exact chord sums in chord order with ocml exp: non-finite columns (nf: the reference's order, the NaN pattern --
+// tau is NaN for an infinite column where some chi_s sigma_s is not > 0, zr) or beyond a table truncated at the host's
+// octave cap (F_out / F_sum weights).  Not inlined and not optimised: inlined, machine LICM hoists ocml exp's constants
+// out of the lookup kernels' loops and their register allocation grows by ~10-20 VGPRs for paths that run only in
+// pathological cases (k_sigma_tw; k_sigma_tc keeps them inline: there the call's saved registers cost more); the
+// operations and their order are the inlined code's (tc_eval, k_sigma_tc), so the sums are bitwise the same
+__device__ __noinline__ __attribute__((optnone)) double tc_chord_sum(double Y, bool nf, bool zr, double fs,
+                                                                    const int32_t* __restrict__ fl,
+                                                                    const double* __restrict__ nc,
+                                                                    const double* __restrict__ fout, int32_t n_pr) {
+  const double inv_fs = 1.0 / fs;
+  double a = 0.0;
+  for (int32_t ci = 0; ci < n_pr; ++ci) {
+    if (fl[ci] != 0) continue;
+    const double N = nc[ci];
+    double tau = N * Y;
+    if (nf && zr && !__builtin_isfinite(N)) tau = __builtin_nan("");
+    const double e = exp(-tau);
+    a = nf ? a + fout[ci] * e : a + (fout[ci] * inv_fs) * e;
+  }
+  return a;
+}
+
 // T_o(Y) for a phase whose columns are finite (header h, its table rows tabo)
 __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h, const double* __restrict__ tabo,
                                           const int32_t* __restrict__ fl, const double* __restrict__ nc,

@@ -24,6 +24,15 @@
 //                 truncated at the host's octave cap) the exact sum over the phase's chords.
 // So |R - R_exact| is a few 1e-16 plus the rounding of the sums, against the windowed path's 4e-14.  A phase
 // with a non-finite column takes the reference's chord order with ocml exp (the NaN pattern), as before.
+//
+// Codegen dependence (k_tc_build's hand-off between the parts of a (phase, chain)): the parts' sums are published
+// with relaxed agent-scope atomic stores, which gfx950 emits as write-through global_store ... sc1, each storing wave
+// waits vmcnt(0), then one agent-scope atomic add per workgroup; the last arriver reads with relaxed agent-scope
+// atomic loads (global_load ... sc1).  This is MI355X_MICROARCH.md's measured sc1 form, used in place of an
+// agent-scope release/acquire pair (whose release is a buffer_wbl2 of the whole XCD L2: 1.7-6.5 us per workgroup and
+// run).  It relies on the relaxed agent-scope atomics compiling to sc1 accesses; a compiler that lowered them
+// otherwise would need the fences back.  tests/test_gpu_tcurve.py (curves against the exact sums, many parts) would
+// show a stale partial sum as a wrong curve.
 #include "prom_tc.h"
 
 namespace prom {
@@ -420,44 +429,38 @@ __global__ void __launch_bounds__(kTcB2) k_tc_build(const int32_t* __restrict__ 
 #else
 #define PROM_TC_ATTR
 #endif
-template <int NSIG, int D, bool MG, int R, bool UNI, int RG>
-__global__ void __launch_bounds__(kBlock * RG) PROM_TC_ATTR k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
+template <int NSIG, int D, bool MG, int R, bool UNI>
+__global__ void __launch_bounds__(kBlock) PROM_TC_ATTR k_sigma_tc(const SigTabs4 tabv, const PolyCoef pc, const double* __restrict__ wav,
                                                      int64_t n_wav, int32_t n_rows, const SigSeg* __restrict__ seg,
                                                      const SigSeg* __restrict__ seg4, const int32_t* __restrict__ sdir,
                                                      const int32_t* __restrict__ fb, int32_t n_fb, int32_t n_blk,
                                                      int32_t n_rc, int32_t rf, const TcArgs ta) {
-  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per thread");
-  static_assert(RG == 1 || RG == 2 || RG == 4, "1, 2 or 4 row groups per workgroup");
+  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "1 to 16 rows per workgroup");
   constexpr int NT = UNI ? 1 : R;
-  constexpr int NTH = kBlock * RG;          // threads: RG groups of 256 (one wavelength each) x R rows
   // every species' slice staged at once (one load round, one barrier): per species the nodes x_k (m + 1 of them)
   // and the records' {(chi) E_k, slope_k} (24 bytes a record: four 3-species workgroups per CU)
   constexpr int CAP = tc_slice_cap(NSIG);   // (nodes per species' slice, SigSeg kind & 64)
   constexpr int SXN = CAP + 2;              // (x_0 .. x_m, padded to 16 bytes)
   __shared__ double2 ssel[(D > 0 && NT > 1) ? NSIG * CAP : 1];
   __shared__ double ssx[(D > 0 && NT > 1) ? NSIG * SXN : 1];
-  // tid: the workgroup's thread (staging, headers); lt: the wavelength of the block; rg: the row group.  RG > 1: one
-  // slice stage serves RG x R rows (C3's 16 phases: one stage per block instead of two workgroups each staging it)
-  const int tid = threadIdx.x, lt = RG == 1 ? tid : tid & (kBlock - 1), rg = RG == 1 ? 0 : tid >> 8;
+  const int tid = threadIdx.x;
   const int32_t RF = rf;
-  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * ((n_rows + RF * RG - 1) / (RF * RG));
+  const int64_t n_fb8 = ((int64_t)n_fb + 7) / 8 * 8, n_front = n_fb8 * ((n_rows + RF - 1) / RF);
   int64_t bid = blockIdx.x, wb;
-  int32_t r0, rw, rcap = R;   // (rw: the workgroup's first row, r0: this row group's)
+  int32_t r0, rcap = R;
   bool lds_ok = true;
   if (bid < n_front) {
     const int64_t i = bid % n_fb8;
     if (i >= n_fb) return;
     wb = fb[i];
-    rw = (int32_t)(bid / n_fb8) * RF * RG;
-    r0 = rw + rg * RF;
+    r0 = (int32_t)(bid / n_fb8) * RF;
     rcap = RF;
     lds_ok = false;
   } else {
     bid -= n_front;
     const int64_t grp = bid / (8 * n_rc), rem = bid % (8 * n_rc);
     wb = grp * 8 + rem % 8;
-    rw = (int32_t)(rem / 8) * R * RG;
-    r0 = rw + rg * R;
+    r0 = (int32_t)(rem / 8) * R;
     if (wb >= n_blk) return;
     if constexpr (NT == 1 || D == 0) {
       // one target row (one phase, or phases sharing one Doppler factor): no LDS slices -- each lane reads its
@@ -475,17 +478,17 @@ __global__ void __launch_bounds__(kBlock * RG) PROM_TC_ATTR k_sigma_tc(const Sig
 #pragma unroll
   for (int s = 0; s < NSIG; ++s) sgs[s] = seg[wb * NSIG + s];
   // the rows' curve headers, staged with the slices (read after the lookups: no load round at the end)
-  __shared__ double shdr[R * RG * kTcHdr];
-  if (tid < R * RG * kTcHdr) {
-    const int32_t rr = rw + tid / kTcHdr;
+  __shared__ double shdr[R * kTcHdr];
+  if (tid < R * kTcHdr) {
+    const int32_t rr = r0 + tid / kTcHdr;
     shdr[tid] = ta.hdr[(int64_t)(rr < n_rows ? rr : n_rows - 1) * kTcHdr + tid % kTcHdr];
   }
   const int32_t rlim = r0 + rcap < n_rows ? r0 + rcap : n_rows;
-  rcap = RG == 1 ? rlim - r0 : (rlim > r0 ? rlim - r0 : 0);
+  rcap = rlim - r0;
 #ifdef PROM_TRACE
   const unsigned long long tr_t0 = wall_clock64();
 #endif
-  const int64_t w = wb * kBlock + lt;
+  const int64_t w = wb * kBlock + tid;
   const bool live = w < n_wav;
   const double lam = wav[live ? w : n_wav - 1];
   // the rows' targets, once: every species of the effective absorber belongs to one density scenario (species
@@ -503,13 +506,13 @@ __global__ void __launch_bounds__(kBlock * RG) PROM_TC_ATTR k_sigma_tc(const Sig
     if (lds_ok) {
       // each thread: records tid, tid + 256, ... of every species' slice (m <= CAP), all loads in flight before the
       // first LDS write
-      constexpr int NQ = (CAP + NTH - 1) / NTH;
+      constexpr int NQ = (CAP + kBlock - 1) / kBlock;
       double4 q[NSIG][NQ];
 #pragma unroll
       for (int s = 0; s < NSIG; ++s) {
         const double4* __restrict__ rr = tabv.t[s].rec + sgs[s].lo;
 #pragma unroll
-        for (int j = 0; j < NQ; ++j) q[s][j] = rr[tid + j * NTH < sgs[s].m ? tid + j * NTH : 0];
+        for (int j = 0; j < NQ; ++j) q[s][j] = rr[tid + j * kBlock < sgs[s].m ? tid + j * kBlock : 0];
       }
 #pragma unroll
       for (int s = 0; s < NSIG; ++s) {
@@ -519,7 +522,7 @@ __global__ void __launch_bounds__(kBlock * RG) PROM_TC_ATTR k_sigma_tc(const Sig
         const int32_t m = sgs[s].m;
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
-          const int32_t i = tid + j * NTH;
+          const int32_t i = tid + j * kBlock;
           if (i < m) {
             sx[i] = q[s][j].x;
             sel[i] = make_double2(MG ? chi * q[s][j].y : q[s][j].y, q[s][j].z);
@@ -587,7 +590,7 @@ __global__ void __launch_bounds__(kBlock * RG) PROM_TC_ATTR k_sigma_tc(const Sig
         continue;
       }
       if ((sg.kind & 3) == 0 && (sg.kind & 8)) {
-        const SigSeg sub = seg4[((int64_t)wb * NSIG + s) * 4 + (lt >> 6)];
+        const SigSeg sub = seg4[((int64_t)wb * NSIG + s) * 4 + (tid >> 6)];
         if (sub.m > 0) sgw = sub;
       }
       if ((sgw.kind & 3) > 0) {
@@ -669,7 +672,7 @@ __global__ void __launch_bounds__(kBlock * RG) PROM_TC_ATTR k_sigma_tc(const Sig
     if (r >= rcap) break;
     const int32_t o = r0 + r;
     const double Y = acc[UNI ? 0 : r];
-    const double* h = shdr + (RG == 1 ? r : r0 - rw + r) * kTcHdr;
+    const double* h = shdr + r * kTcHdr;
     double v;
     if (!((int32_t)h[kTcHFlags] & 2)) {
       v = tc_eval(Y, h, ta.tab + (int64_t)o * ta.lg * kTcD, ta.flags + (int64_t)o * ta.n_pr,
@@ -769,12 +772,7 @@ bool launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   static const int r1_env = [] { const char* e = std::getenv("PROM_TC_R1"); return e ? std::atoi(e) : 0; }();
   const int Rmax = (nsig >= 2 || uni) ? 8 : (r1_env == 4 ? 4 : 8);
   const int R = (uni || deg == 0) ? 8 : (n_rows == 1 ? 1 : Rmax);
-  // row groups per workgroup (RG x 256 threads, one slice stage for RG x R rows): 1; PROM_TC_RG=2 (read once, A/B)
-  // stages a block's slice once for 16 rows
-  static const int rg_env = [] { const char* e = std::getenv("PROM_TC_RG"); return e ? std::atoi(e) : 0; }();
-  int RG = 1;   // (RG = 2 measured slower on C3: 37.7 against 32.1 us, 4 waves per SIMD at 101 VGPRs; r06b)
-  if ((rg_env == 1 || rg_env == 2) && !uni && R == 8 && deg > 0) RG = rg_env;
-  const int32_t n_rc = (n_rows + R * RG - 1) / (R * RG);
+  const int32_t n_rc = (n_rows + R - 1) / R;
   // front workgroups (oversize blocks): R / 2 rows for one species with fewer than 16384 (block, row) pairs of
   // them (profiles/r03_sigma_rf_sweep.txt), or for several species when some block has neither a linear guess
   // nor a directory (its slow lookups spread over more workgroups); else all R (C3 with every block guessed:
@@ -791,7 +789,7 @@ bool launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
   // blocks too, so no front: a front would look them up and write their R rows a second time)
   const bool direct = uni || R == 1 || deg == 0;
   const int32_t n_fb = direct ? 0 : tr.n_sig_fb_tc;
-  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF * RG - 1) / (RF * RG));
+  const int64_t n_front = (int64_t)((n_fb + 7) / 8) * 8 * ((n_rows + RF - 1) / RF);
   const unsigned nb = (unsigned)(n_front + (n_fb >= n_blk ? 0 : (int64_t)((n_blk + 7) / 8) * 8 * n_rc));
   const PolyCoef& pc = poly_coef();
   const SigTabs4& tabv = tr.sigtab_v;
@@ -806,20 +804,19 @@ bool launch_tcurve(hipStream_t s, TransitDev& tr, RunSlot& rs, int32_t nsig, boo
     launch_sigma_tw(s, tr, nsig, deg, ta, ev_sig0, ev_sig1);
     return true;
   }
-#define PROM_TCK(NS, DG, MGV, RV, UV, RGV)                                                                         \
-  hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV, RGV>), dim3(nb), dim3(kBlock * RGV), 0, s, ev_sig0, ev_sig1, 0, \
-                        tabv, pc, wav, n_wav, n_rows, seg, seg4, sdir, fb, n_fb, n_blk, n_rc, RF, ta)
+#define PROM_TCK(NS, DG, MGV, RV, UV)                                                                         \
+  hipExtLaunchKernelGGL((k_sigma_tc<NS, DG, MGV, RV, UV>), dim3(nb), dim3(kBlock), 0, s, ev_sig0, ev_sig1, 0, tabv, \
+                        pc, wav, n_wav, n_rows, seg, seg4, sdir, fb, n_fb, n_blk, n_rc, RF, ta)
 #define PROM_TCR(NS, DG, MGV)                                       \
   do {                                                              \
-    if (uni) PROM_TCK(NS, DG, MGV, 8, true, 1);                     \
-    else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false, 1);            \
-    else if ((NS) == 1 && R == 4) PROM_TCK(NS, DG, MGV, 4, false, 1);   \
-    else if (RG == 2) PROM_TCK(NS, DG, MGV, 8, false, 2);           \
-    else PROM_TCK(NS, DG, MGV, 8, false, 1);                        \
+    if (uni) PROM_TCK(NS, DG, MGV, 8, true);                        \
+    else if (R == 1) PROM_TCK(NS, DG, MGV, 1, false);               \
+    else if ((NS) == 1 && R == 4) PROM_TCK(NS, DG, MGV, 4, false);   \
+    else PROM_TCK(NS, DG, MGV, 8, false);                           \
   } while (0)
   // degree 8 covers every table with amax <= 0.07 (the high-resolution configs); 14 the rest (coarse tables)
 #define PROM_TCD(NS, MGV)                                                          \
-  if (deg == 0) { if (uni) PROM_TCK(NS, 0, MGV, 8, true, 1); else PROM_TCK(NS, 0, MGV, 8, false, 1); } \
+  if (deg == 0) { if (uni) PROM_TCK(NS, 0, MGV, 8, true); else PROM_TCK(NS, 0, MGV, 8, false); } \
   else if (deg <= 8) PROM_TCR(NS, 8, MGV);                                       \
   else PROM_TCR(NS, 14, MGV);
 #ifdef PROM_TC_DEV_ONE

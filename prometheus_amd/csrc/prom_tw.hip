@@ -22,25 +22,6 @@ namespace prom {
 // evaluates fl(chi E_k) e^a (or E_k e^a - offset) of numpy's bracket k, so R does not depend on the windows: bitwise
 // equal to k_sigma_tc's and for any wavelength or phase shard.
 
-// the second pass's chord sums in chord order with ocml exp: non-finite columns (nf: the reference's order, NaN for an
-// infinite column where some chi_s sigma_s is not > 0) or beyond a truncated table (F_out / F_sum weights).  Not
-// inlined and not optimised: inlined, machine LICM hoists ocml exp's constants out of the second pass's loop and the
-// kernel's register allocation grows by ~20 VGPRs for a path that runs only in pathological cases (66 against 77 VGPRs)
-__device__ __noinline__ __attribute__((optnone)) double tw_chord_sum(double Y, bool nf, bool zr, double fs, const int32_t* __restrict__ fl,
-                                            const double* __restrict__ nc, const double* __restrict__ fout, int32_t n_pr) {
-  const double inv_fs = 1.0 / fs;
-  double a = 0.0;
-  for (int32_t ci = 0; ci < n_pr; ++ci) {
-    if (fl[ci] != 0) continue;
-    const double N = nc[ci];
-    double tau = N * Y;
-    if (nf && zr && !__builtin_isfinite(N)) tau = __builtin_nan("");
-    const double e = exp(-tau);
-    a = nf ? a + fout[ci] * e : a + (fout[ci] * inv_fs) * e;
-  }
-  return a;
-}
-
 template <int NSIG, int D, bool MG>
 __global__ void __launch_bounds__(kBlock) k_sigma_tw(const SigTabs4 tabv, const SigTabDev* __restrict__ tabp,
                                                      const PolyCoef pc, const double* __restrict__ wav,
@@ -310,7 +291,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tw(const SigTabs4 tabv, const 
           v = tc_eval_full(Y, h, ctab + (int64_t)o * ta.lg * kTcD);
         } else {
           const double fs = h[kTcHFsum];
-          const double a = tw_chord_sum(Y, nf, zr, fs, ta.flags + (int64_t)o * ta.n_pr, ta.ncol + (int64_t)o * ta.n_pr,
+          const double a = tc_chord_sum(Y, nf, zr, fs, ta.flags + (int64_t)o * ta.n_pr, ta.ncol + (int64_t)o * ta.n_pr,
                                         ta.fout, ta.n_pr);
           if (beyond && ta.evals) atomicAdd(&ta.evals[threadIdx.x & 63], (unsigned long long)(int32_t)h[kTcHNact]);
           v = nf ? (a + h[kTcHTfrac] * fs) / fs : h[kTcHTfrac] + a;
