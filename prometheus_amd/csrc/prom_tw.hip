@@ -3,7 +3,7 @@
 
 namespace prom {
 
-// ---- sigma lookups + transmission curves over target windows (the default with orbital Doppler shift) ------
+// ---- sigma lookups + transmission curves over target windows (one species with orbital Doppler shift) ----
 // The targets t = shift_o lambda_w of all rows, not the wavelengths, are cut into windows (host: prom_window.hip):
 // window b holds, per row o, the contiguous wavelengths w in [W[b][o], W[b+1][o]) whose targets fall in the
 // window's target interval (at most a few hundred per row).  Per species the table nodes those targets reach are
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tw(const SigTabs4 tabv, const 
                                                      const double* __restrict__ ctab, double* __restrict__ Rout) {
   // (hdr, shift, ctab, Rout: TcArgs' hdr, tabv.t[0].shift, tab and R as __restrict__ parameters -- with the kernel's
   // stores provably elsewhere, the row's header and Doppler factor become scalar loads)
-  static_assert(D > 0, "polynomial lookups only (coarse tables take k_sigma_tw)");
+  static_assert(D > 0, "polynomial lookups only (coarse tables take k_sigma_tc)");
   // LDS: [0, 2 tot) the records {(chi) E_k, L_k} (species s at 2 pad), then tot + NSIG node x's (species s at pad + s:
   // x_lo .. x_{lo+m}), then the window's wavelengths
   __shared__ double2 lds2[kTwLds / 2 + 32];   // (+ 64 doubles: the staged wavelengths' padding, read past lw1)

@@ -1,4 +1,4 @@
-// Target windows of the Doppler-shifted cross-section lookups (host side, per set; k_sigma_tw in prom_tcurve.hip).
+// Target windows of the Doppler-shifted cross-section lookups (host side, per set; k_sigma_tw in prom_tw.hip).
 //
 // With orbital Doppler shift every (phase o, wavelength w) looks the tables up at t = shift_o lambda_w
 // (gasProperties.py:941-954: getSigmaAbs(wavelength / dopplerShift)-style shifted grids, one per phase).  A
