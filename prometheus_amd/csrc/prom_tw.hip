@@ -22,7 +22,7 @@ namespace prom {
 // evaluates fl(chi E_k) e^a (or E_k e^a - offset) of numpy's bracket k, so R does not depend on the windows: bitwise
 // equal to k_sigma_tc's and for any wavelength or phase shard.
 
-template <int NSIG, int D, bool MG>
+template <int NSIG, int D, bool MG, int RP>
 __global__ void __launch_bounds__(kBlock) k_sigma_tw(const SigTabs4 tabv, const SigTabDev* __restrict__ tabp,
                                                      const PolyCoef pc, const double* __restrict__ wav,
                                                      int64_t n_wav, int32_t n_rows, const SigSeg* __restrict__ wseg,
@@ -117,12 +117,9 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tw(const SigTabs4 tabv, const 
   const int32_t* __restrict__ wa = wrow + (int64_t)b * n_rows;
   const int32_t* __restrict__ wz = wa + n_rows;
   // first pass: windows whose every species has a staged, guessed slice (kind 1), rows whose curve is complete (header
-  // flags 2 and 4 clear).  Waves take whole rows round robin (G waves per row when there are fewer than 4), each row's
-  // Doppler factor and curve header loaded once into scalar registers, then the row's chunks of 64 wavelengths.  The
-  // wavelengths come from the window's LDS stage when it holds them; else a row's are loaded up to four chunks at a
-  // time before any of them is computed (one vmcnt wait -- which also waits for the earlier stores -- per batch)
+  // flags 2 and 4 clear).  Waves take whole rows (or row pairs) round robin, each row's Doppler factor and curve header
+  // loaded once into scalar registers, then the rows' chunks of 64 wavelengths
   if (!wrare) {
-    const int32_t G = n_rows >= 4 ? 1 : (n_rows == 1 ? 4 : 2);   // waves per row
     // per species, hoisted by hand (the compiler keeps them as per-lookup arithmetic otherwise): the slice's LDS
     // bases (lookup address = g * 8 + base), and the guess's offset and the polynomial's leading coefficient held in
     // VGPRs (a 64-bit FMA takes one scalar operand: either would be copied to VGPRs before every use)
@@ -139,86 +136,163 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tw(const SigTabs4 tabv, const 
     double cdv = pc.c[D];
     asm volatile("" : "+v"(cdv));
     const double* lamb = slam + lane - lw0;   // (the staged wavelengths, this lane's column; 64 entries of padding)
-    for (int32_t o = __builtin_amdgcn_readfirstlane(wv / G); o < n_rows; o += 4 / G) {
-      const double* h = hdr + (int64_t)o * kTcHdr;
-      if ((int32_t)h[kTcHFlags] & 6) continue;   // (second pass)
-      const int32_t w0 = wa[o], w1 = wz[o];
-      const double sh = shift[o];
-      const double* tabo = ctab + (int64_t)o * ta.lg * kTcD;
-      double* const Rrow = Rout + (int64_t)o * n_wav + lane;   // (this lane's column of the row)
-      // MODE 0: every guess exact; 1: guesses with the one-node test; 2: as 1, kind-3 slices by bisection
-      auto chunk = [&](int32_t c0, double lam, auto mode_tag) {
-        constexpr int MODE = decltype(mode_tag)::value;
-        constexpr bool EX = MODE == 0;
-        const double t = sh * lam;
-        // every species' x_g (x_{g+1}) and record in one LDS round, then, unless every guess is exact, the rare
-        // one-node corrections, then the e^a polynomials.  (The guess clamps at m - 2 only: every target of the
-        // window lies in the slice, so fma(t, inv, xs) > -1 and the integer conversion is >= 0, as seg_guess's)
-        int32_t g[NSIG];
-        double x0[NSIG], x1[NSIG];
-        double2 e[NSIG];
+    // NP points per lane at once: rows a and b (RP = 2: a row pair, the two rows' chunks k side by side -- two
+    // independent lookup chains per lane), with each row's Doppler factor, header, table and R row in scalar registers
+    struct RowS {
+      const double* h;
+      const double* tabo;
+      double* Rrow;
+      double sh;
+      int32_t w0, w1;
+    };
+    auto row_of = [&](int32_t o) {
+      RowS r;
+      r.h = hdr + (int64_t)o * kTcHdr;
+      r.tabo = ctab + (int64_t)o * ta.lg * kTcD;
+      r.Rrow = Rout + (int64_t)o * n_wav + lane;   // (this lane's column of the row)
+      r.sh = shift[o];
+      r.w0 = wa[o];
+      r.w1 = wz[o];
+      return r;
+    };
+    // MODE 0: every guess exact; 1: guesses with the one-node test; 2: as 1, kind-3 slices by bisection.  c0[p]: the
+    // chunk's first wavelength (stores only where c0[p] + lane < w1), lam[p] the lane's wavelength
+    auto chunk = [&](const RowS* rs, auto np_tag, const int32_t* c0, const double* lam, auto mode_tag) {
+      constexpr int NP = decltype(np_tag)::value;
+      constexpr int MODE = decltype(mode_tag)::value;
+      constexpr bool EX = MODE == 0;
+      double t[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) t[p] = rs[p].sh * lam[p];
+      // every species' x_g (x_{g+1}) and record in one LDS round, then, unless every guess is exact, the rare
+      // one-node corrections, then the e^a polynomials.  (The guess clamps at m - 2 only: every target of the
+      // window lies in the slice, so fma(t, inv, xs) > -1 and the integer conversion is >= 0, as seg_guess's)
+      int32_t g[NP][NSIG];
+      double x0[NP][NSIG], x1[NP][NSIG];
+      double2 e[NP][NSIG];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
 #pragma unroll
         for (int s = 0; s < NSIG; ++s) {
-          g[s] = min((int32_t)__builtin_fma(t, sg[s].inv, xsv[s]), sg[s].m - 2);
-          x0[s] = xsb[s][g[s]];
-          if constexpr (!EX) x1[s] = xsb[s][g[s] + 1];
-          e[s] = elb[s][g[s]];
+          g[p][s] = min((int32_t)__builtin_fma(t[p], sg[s].inv, xsv[s]), sg[s].m - 2);
+          x0[p][s] = xsb[s][g[p][s]];
+          if constexpr (!EX) x1[p][s] = xsb[s][g[p][s] + 1];
+          e[p][s] = elb[s][g[p][s]];
         }
-        if constexpr (!EX) {
+      if constexpr (!EX) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
           for (int s = 0; s < NSIG; ++s) {
             if (MODE == 2 && (sg[s].kind & 3) == 3) {
               // numpy's bracket, the largest k <= m - 2 with x_k <= t, by bisection over the staged slice
               int32_t k = 0;
               for (int32_t st = 1 << (31 - __builtin_clz((uint32_t)(sg[s].m - 1) | 1u)); st > 0; st >>= 1)
-                if (k + st <= sg[s].m - 2 && xsb[s][k + st] <= t) k += st;
-              x0[s] = xsb[s][k];
-              e[s] = elb[s][k];
+                if (k + st <= sg[s].m - 2 && xsb[s][k + st] <= t[p]) k += st;
+              x0[p][s] = xsb[s][k];
+              e[p][s] = elb[s][k];
               continue;
             }
-            const bool lo = t < x0[s], hi = t >= x1[s];   // (no short-circuit: that would chain the reads)
+            const bool lo = t[p] < x0[p][s], hi = t[p] >= x1[p][s];   // (no short-circuit: that would chain the reads)
             if (lo | hi) {
-              const int32_t k = lo ? g[s] - 1 : g[s] + 1;
-              x0[s] = xsb[s][k];
-              e[s] = elb[s][k];
+              const int32_t k = lo ? g[p][s] - 1 : g[p][s] + 1;
+              x0[p][s] = xsb[s][k];
+              e[p][s] = elb[s][k];
             }
           }
-        }
-        double acc = 0.0;
+      }
+      double acc[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        acc[p] = 0.0;
 #pragma unroll
         for (int s = 0; s < NSIG; ++s) {
-          const double a = e[s].y * (t - x0[s]);
-          double p = __builtin_fma(cdv, a, pc.c[D - 1]);   // (exp_taylor<D>, the leading coefficient from a VGPR)
+          const double a = e[p][s].y * (t[p] - x0[p][s]);
+          double q = __builtin_fma(cdv, a, pc.c[D - 1]);   // (exp_taylor<D>, the leading coefficient from a VGPR)
 #pragma unroll
-          for (int k = D - 2; k >= 0; --k) p = __builtin_fma(p, a, pc.c[k]);
-          if constexpr (MG) acc = __builtin_fma(e[s].x, p, acc);
-          else acc = __builtin_fma(e[s].x, p, -tabv.t[s].offset);
+          for (int k = D - 2; k >= 0; --k) q = __builtin_fma(q, a, pc.c[k]);
+          if constexpr (MG) acc[p] = __builtin_fma(e[p][s].x, q, acc[p]);
+          else acc[p] = __builtin_fma(e[p][s].x, q, -tabv.t[s].offset);
         }
-        if constexpr (MG) acc -= choff;
-        const double v = tc_eval_full(acc, h, tabo);
-        if (c0 + lane < w1) Rrow[c0] = v;
-      };
-      auto row = [&](auto mode_tag) {
-        if (nlam > 0) {
-          for (int32_t c0 = w0 + (wv % G) * 64; c0 < w1; c0 += 64 * G) chunk(c0, lamb[c0], mode_tag);
-        } else {
-          constexpr int B = 4;
-          for (int32_t c0 = w0 + (wv % G) * 64; c0 < w1; c0 += B * 64 * G) {
-            double lam[B];
+        if constexpr (MG) acc[p] -= choff;
+      }
 #pragma unroll
-            for (int j = 0; j < B; ++j) {
-              const int32_t w = c0 + j * 64 * G + lane;
-              lam[j] = wav[w < w1 ? w : w1 - 1];
+      for (int p = 0; p < NP; ++p) {
+        const double v = tc_eval_full(acc[p], rs[p].h, rs[p].tabo);
+        if (c0[p] + lane < rs[p].w1) rs[p].Rrow[c0[p]] = v;
+      }
+    };
+    // the NP rows' chunks k = k0, k0 + G, ...: the wavelengths from the LDS stage, else loaded up to four chunks at a
+    // time before any of them is computed (one vmcnt wait -- which also waits for the earlier stores -- per batch).  A
+    // row with fewer chunks than its partner computes a clamped chunk and stores nothing
+    auto rows = [&](const RowS* rs, auto np_tag, int32_t k0, int32_t G, auto mode_tag) {
+      constexpr int NP = decltype(np_tag)::value;
+      int32_t nch = 0;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) nch = max(nch, (rs[p].w1 - rs[p].w0 + 63) >> 6);
+      auto cfix = [&](int p, int32_t c) { return c < rs[p].w1 ? c : rs[p].w0; };   // (a clamped, computed chunk)
+      if (nlam > 0) {
+        for (int32_t k = k0; k < nch; k += G) {
+          int32_t c0[NP];
+          double lam[NP];
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            c0[p] = rs[p].w0 + 64 * k;
+            lam[p] = lamb[cfix(p, c0[p])];
+          }
+          chunk(rs, np_tag, c0, lam, mode_tag);
+        }
+      } else {
+        constexpr int B = 4 / NP;
+        for (int32_t k = k0; k < nch; k += B * G) {
+          double lam[B][NP];
+#pragma unroll
+          for (int j = 0; j < B; ++j)
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+              const int32_t w = cfix(p, rs[p].w0 + 64 * (k + j * G)) + lane;
+              lam[j][p] = wav[w < rs[p].w1 ? w : rs[p].w1 - 1];
             }
 #pragma unroll
-            for (int j = 0; j < B; ++j)
-              if (c0 + j * 64 * G < w1) chunk(c0 + j * 64 * G, lam[j], mode_tag);
+          for (int j = 0; j < B; ++j) {
+            if (k + j * G >= nch) break;
+            int32_t c0[NP];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) c0[p] = rs[p].w0 + 64 * (k + j * G);
+            chunk(rs, np_tag, c0, lam[j], mode_tag);
           }
         }
-      };
-      if (wexact) row(std::integral_constant<int, 0>{});
-      else if (!wsearch) row(std::integral_constant<int, 1>{});
-      else row(std::integral_constant<int, 2>{});
+      }
+    };
+    auto rows_mode = [&](const RowS* rs, auto np_tag, int32_t k0, int32_t G) {
+      if (wexact) rows(rs, np_tag, k0, G, std::integral_constant<int, 0>{});
+      else if (!wsearch) rows(rs, np_tag, k0, G, std::integral_constant<int, 1>{});
+      else rows(rs, np_tag, k0, G, std::integral_constant<int, 2>{});
+    };
+    auto rare_row = [&](int32_t o) { return ((int32_t)hdr[(int64_t)o * kTcHdr + kTcHFlags] & 6) != 0; };
+    if constexpr (RP == 1) {
+      const int32_t G = n_rows >= 4 ? 1 : (n_rows == 1 ? 4 : 2);   // waves per row
+      for (int32_t o = __builtin_amdgcn_readfirstlane(wv / G); o < n_rows; o += 4 / G) {
+        if (rare_row(o)) continue;   // (second pass)
+        const RowS r1[1] = {row_of(o)};
+        rows_mode(r1, std::integral_constant<int, 1>{}, wv % G, G);
+      }
+    } else {
+      // row pairs (2q, 2q + 1) round robin over the waves (G waves per pair when there are fewer than 4 pairs); a pair
+      // with one row in the second pass (or past n_rows) runs its other row alone
+      const int32_t P = (n_rows + 1) >> 1;
+      const int32_t G = P >= 4 ? 1 : (P == 1 ? 4 : 2);
+      for (int32_t q = __builtin_amdgcn_readfirstlane(wv / G); q < P; q += 4 / G) {
+        const int32_t oa = 2 * q, ob = 2 * q + 1;
+        const bool ra = rare_row(oa), rb = ob >= n_rows || rare_row(ob);
+        if (!ra && !rb) {
+          const RowS r2[2] = {row_of(oa), row_of(ob)};
+          rows_mode(r2, std::integral_constant<int, 2>{}, wv % G, G);
+        } else if (!ra || !rb) {
+          const RowS r1[1] = {row_of(ra ? ob : oa)};
+          rows_mode(r1, std::integral_constant<int, 1>{}, wv % G, G);
+        }
+      }
     }
   }
   // second pass: the rest (kinds 0, 2, 3, rows with header flags 2 or 4), numpy's bracket per
@@ -374,12 +448,18 @@ void launch_sigma_tw(hipStream_t s, TransitDev& tr, int32_t nsig, int32_t deg, c
   const int32_t n_rows = tr.n_orb;
   const int64_t n_wav = tr.n_wav;
   PROM_REQUIRE(deg > 0 && n_rows >= 2 && tr.n_tw > 0, "k_sigma_tw: polynomial lookups with orbital Doppler rows");
-#define PROM_TWK(NS, DG, MGV)                                                                                  \
-  hipExtLaunchKernelGGL((k_sigma_tw<NS, DG, MGV>), dim3(nbw), dim3(kBlock), 0, s, ev0, ev1, 0, tabv, tabp, pc, wav, n_wav, \
-                        n_rows, twseg, twrow, twlam, tr.n_tw, ta, ta.hdr, tabv.t[0].shift, ta.tab, ta.R)
+  // PROM_TW_RP (read once): 2 = row pairs per wave in the first pass (two lookup chains per lane), 1 = single rows
+  static const int rp = [] { const char* e = std::getenv("PROM_TW_RP"); return e && std::atoi(e) == 2 ? 2 : 1; }();
+#define PROM_TWK(NS, DG, MGV)                                                                                        \
+  if (rp == 2)                                                                                                       \
+    hipExtLaunchKernelGGL((k_sigma_tw<NS, DG, MGV, 2>), dim3(nbw), dim3(kBlock), 0, s, ev0, ev1, 0, tabv, tabp, pc, wav, \
+                          n_wav, n_rows, twseg, twrow, twlam, tr.n_tw, ta, ta.hdr, tabv.t[0].shift, ta.tab, ta.R);   \
+  else                                                                                                               \
+    hipExtLaunchKernelGGL((k_sigma_tw<NS, DG, MGV, 1>), dim3(nbw), dim3(kBlock), 0, s, ev0, ev1, 0, tabv, tabp, pc, wav, \
+                          n_wav, n_rows, twseg, twrow, twlam, tr.n_tw, ta, ta.hdr, tabv.t[0].shift, ta.tab, ta.R)
 #define PROM_TWD(NS, MGV)                 \
-  if (deg <= 8) PROM_TWK(NS, 8, MGV);     \
-  else PROM_TWK(NS, 14, MGV);
+  if (deg <= 8) { PROM_TWK(NS, 8, MGV); } \
+  else { PROM_TWK(NS, 14, MGV); }
   switch (nsig) {
     case 1: PROM_TWD(1, false) break;
     case 2: PROM_TWD(2, true) break;

@@ -87,6 +87,8 @@ bool build_target_windows(const double* wav, int64_t n_wav, const double* shift,
   // lamfit: grow windows only while their wavelengths fit the LDS beside the slices (else they are staged only where
   // they happen to fit, and read from global memory elsewhere)
   const bool lamfit = lamcap > 0 && [] { const char* e = std::getenv("PROM_TW_LAMFIT"); return e && std::atoi(e) != 0; }();
+  // PROM_TW_ALIGN: the largest overhang past a multiple of 64 wavelengths per row that a window drops (0: none)
+  static const int64_t align = [] { const char* e = std::getenv("PROM_TW_ALIGN"); return e ? (int64_t)std::atoi(e) : (int64_t)64; }();
   // LDS budget in doubles: 3 per staged node ({E, L} and x), one more x per species, one per staged wavelength
   auto fits = [&](int64_t nodes, int64_t lam) { return 3 * nodes + NS + lam <= lds && lam <= lamcap; };
   for (int64_t w = 0; w < n_wav; ++w)
@@ -176,6 +178,31 @@ bool build_target_windows(const double* wav, int64_t n_wav, const double* shift,
         for (int s = 0; s < NS; ++s) {
           const std::vector<double>& X = *T[s].X;
           while (hs[s] < (int64_t)X.size() - 2 && X[hs[s] + 1] <= thi) ++hs[s];
+        }
+      }
+      // lane alignment: a row's wavelengths are computed 64 at a time, so a window whose longest row ends a few
+      // wavelengths past a multiple of 64 (C3: ~200 = 3 full chunks + 8) spends a nearly empty fourth chunk on every
+      // row.  When the overhang is at most `align` wavelengths, end the window where the longest row holds exactly
+      // that multiple (the next window starts there); the counts of a window's rows differ by the Doppler spread only
+      if (align > 0 && e > j + 1) {
+        int64_t mxe = 0;
+        for (int32_t o = 0; o < n_rows; ++o) mxe = std::max(mxe, Pb[o] - Pa[o]);
+        const int64_t cap = mxe / 64 * 64;
+        if (cap >= 64 && mxe > cap && mxe - cap <= align) {
+          auto mx_at = [&](int64_t ee) {
+            int64_t m = 0;
+            for (int32_t o = 0; o < n_rows; ++o) m = std::max(m, (ee > K ? n_wav : count_below(o, bnd(ee))) - Pa[o]);
+            return m;
+          };
+          int64_t g = j + 1, b = e;   // the largest e' in [j + 1, e) with mx_at(e') <= cap (mx_at(e) > cap)
+          if (mx_at(g) <= cap) {
+            while (b - g > 1) {
+              const int64_t mid = (g + b) >> 1;
+              if (mx_at(mid) <= cap) g = mid; else b = mid;
+            }
+            e = g;
+            for (int32_t o = 0; o < n_rows; ++o) Pb[o] = e > K ? n_wav : count_below(o, bnd(e));
+          }
         }
       }
       // per species slice and guess; shorten the window while some in-range species' guess fails
