@@ -893,12 +893,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       seg_key_keep = seg_reuse;   // the stored key stays as it is (re-validated at the end)
       if (!seg_reuse) tr.tw_ok = false;
       // target windows (k_sigma_tw, prom_window.hip): every atomic slot on one set of Doppler factors (one scenario),
-      // n_orb >= 2; built with the sigma segments (the same inputs) and kept when they are reused.  By default for one
-      // atomic species (C4x10: k_sigma_tw 52 against k_sigma_tc's 60 us); several merged species keep k_sigma_tc's
-      // wavelength blocks (C3: 36.7 against 31.7 us isolated, equal pipelined steps).  PROM_TW (read at
-      // every set): 0 never, 1 always
+      // n_orb >= 2; built with the sigma segments (the same inputs) and kept when they are reused.  The default: C4x10
+      // k_sigma_tw 47-48 us against k_sigma_tc's 60, pipelined step 0.062 against 0.065 ms; C3 (three merged species)
+      // steps 0.0366-0.0374 against 0.0370-0.0384 ms on the same boxes, reads 46 against 79 MB per launch, though
+      // 36-37 against 32 us isolated (profiles/r06t_*, r06u_*).  PROM_TW (read at every set): 0 never
       const char* e_tw = std::getenv("PROM_TW");
-      const bool tw_off = (e_tw && std::atoi(e_tw) == 0) || (!(e_tw && std::atoi(e_tw) == 1) && n_atoms != 1);
+      const bool tw_off = e_tw && std::atoi(e_tw) == 0;
       auto build_tw = [&]() {
         tr.tw_ok = false;
         tr.n_tw = 0;

@@ -448,8 +448,11 @@ void launch_sigma_tw(hipStream_t s, TransitDev& tr, int32_t nsig, int32_t deg, c
   const int32_t n_rows = tr.n_orb;
   const int64_t n_wav = tr.n_wav;
   PROM_REQUIRE(deg > 0 && n_rows >= 2 && tr.n_tw > 0, "k_sigma_tw: polynomial lookups with orbital Doppler rows");
-  // PROM_TW_RP (read once): 2 = row pairs per wave in the first pass (two lookup chains per lane), 1 = single rows
-  static const int rp = [] { const char* e = std::getenv("PROM_TW_RP"); return e && std::atoi(e) == 2 ? 2 : 1; }();
+  // row pairs per wave in the first pass (two lookup chains per lane) for one species: 64 VGPRs either way, C4x10
+  // 47-48 against 49-52 us (profiles/r06u_*); several species: single rows (three species with pairs: 98 VGPRs, 4 waves
+  // per SIMD, C3 39.5 against 37.2 us).  PROM_TW_RP (read once): 1 or 2 forces either
+  static const int rp_env = [] { const char* e = std::getenv("PROM_TW_RP"); return e ? std::atoi(e) : 0; }();
+  const int rp = rp_env == 1 || rp_env == 2 ? rp_env : (nsig == 1 ? 2 : 1);
 #define PROM_TWK(NS, DG, MGV)                                                                                        \
   if (rp == 2)                                                                                                       \
     hipExtLaunchKernelGGL((k_sigma_tw<NS, DG, MGV, 2>), dim3(nbw), dim3(kBlock), 0, s, ev0, ev1, 0, tabv, tabp, pc, wav, \

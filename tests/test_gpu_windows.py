@@ -5,7 +5,7 @@ Every lookup evaluates fl(chi E_k) e^a of numpy's bracket k (gasProperties.py:94
 :34-51), whatever window, slice kind or pass it falls in, so R must be BITWISE the wavelength-block kernel's
 (k_sigma_tc, PROM_TW=0) -- on the golden configs, at full size (C3, C4, C4x10), for wavelength shards and with
 the host's window caps forced small (many windows, slices on the global-record and searched paths).  The windows
-are the default for one atomic species; PROM_TW=1 forces them for C3's three merged species.
+are the default (PROM_TW=0 switches them off); the tests set PROM_TW=1 explicitly.
 """
 import numpy as np
 import pytest
@@ -30,7 +30,7 @@ def _windows_line(capfd):
 @pytest.mark.parametrize("name", ["C3", "C4", "exomoon"])
 def test_windows_bitwise_reduced(name, monkeypatch, capfd):
     monkeypatch.setenv("PROM_DEBUG", "1")
-    monkeypatch.setenv("PROM_TW", "1")   # (the default for one species; forced for C3's three)
+    monkeypatch.setenv("PROM_TW", "1")   # (the default)
     tr = _transit(name, reduced=True)
     R = tr.sumOverChords(devices=[0])
     line = _windows_line(capfd)
