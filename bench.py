@@ -77,7 +77,7 @@ def parse():
                     help="strong splits (--shard, --scaling strong): contiguous wavelength ranges, orbital-phase "
                          "ranges (every wavelength, phases [o0, o1)), or auto (default): phases when every rank "
                          "gets the same number of them, else wavelengths")
-    ap.add_argument("--strong", default="C4x10,C4x10p128", metavar="CONFIGS",
+    ap.add_argument("--strong", default="C4x10,C4x10p256", metavar="CONFIGS",
                     help="N > 1: after the main leg, also time these configurations split over the N ranks in "
                          "contiguous wavelength shards (the north-star strong-scaling axis; the line's `strong` "
                          "object, with each one's full grid timed on rank 0 alone for the speedup); '' to skip")

@@ -108,10 +108,17 @@ def c4x10p64():
 
 
 def c4x10p128():
-    """C4x10 at 128 orbital phases (2.4e8 spectrum points): the >= 1 ms one-GPU strong-scaling workload of the
-    N > 1 bench line (bench.py `strong`), split over the ranks by wavelength."""
+    """C4x10 at 128 orbital phases (2.4e8 spectrum points; 0.66 ms per one-GPU step in round 6)."""
     cfg = c4x10()
     cfg["Grids"]["orbphase_steps"] = 128
+    return cfg
+
+
+def c4x10p256():
+    """C4x10 at 256 orbital phases (4.8e8 spectrum points): the >= 1 ms one-GPU strong-scaling workload of the
+    N > 1 bench line (bench.py `strong`), split over the ranks by wavelength."""
+    cfg = c4x10()
+    cfg["Grids"]["orbphase_steps"] = 256
     return cfg
 
 
@@ -195,7 +202,7 @@ def synthetic_mdot(path, n=40, seed=5):
 TIDAL = {"q": 3.34, "tau": 1.2e4, "mass": 22.99 * _AMU, "sigma_v": 10. * _KMS}
 
 
-PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C4x10p64": c4x10p64, "C4x10p128": c4x10p128,
+PRESETS = {"C1": c1, "C2": c2, "C3": c3, "C4": c4, "C4x10": c4x10, "C4x10p64": c4x10p64, "C4x10p128": c4x10p128, "C4x10p256": c4x10p256,
            "C5": c5, "C2moon": c2moon, "exomoon": exomoon}
 
 

@@ -913,9 +913,13 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
           tabs.push_back(&ctx->tables[t.table].hx);
         }
         if (!one || sc_tw < 0 || tw_off) return;
-        // (profiling knobs, read once: wavelengths per row, points per window, LDS doubles per workgroup)
+        // (profiling knobs, read once: wavelengths per row, points per window, LDS doubles per workgroup).  The point
+        // cap scales with the rows: a window's wavelengths span its rows' Doppler spread (C4x10: ~600) on top of a row's
+        // own, so many-phase windows of 64 wavelengths a row spend most of their staging there -- C4x10p128 1.07 ms per
+        // step at 8,192 points, 0.67 ms at 32,768 (128 rows x 256), C4x10p64 0.40 / 0.34 ms (profiles/r06w_*)
         static const int rowcap = [] { const char* e = std::getenv("PROM_TW_ROWCAP"); return e ? std::max(1, std::atoi(e)) : 256; }();
-        static const int64_t pmax = [] { const char* e = std::getenv("PROM_TW_PMAX"); return e ? std::max(1, std::atoi(e)) : 8192; }();
+        static const int64_t pmax_env = [] { const char* e = std::getenv("PROM_TW_PMAX"); return e ? (int64_t)std::max(1, std::atoi(e)) : (int64_t)0; }();
+        const int64_t pmax = pmax_env > 0 ? pmax_env : std::max<int64_t>(8192, (int64_t)rowcap * n_orb);
         static const int lamcap = [] {   // (wavelengths staged per window at most; 0: never)
           const char* e = std::getenv("PROM_TW_LAMCAP");
           return e ? std::max(0, std::min(prom::kTwLamCap, std::atoi(e))) : prom::kTwLamCap;

@@ -54,7 +54,10 @@ __device__ __forceinline__ double tc_clenshaw(double q, const double* __restrict
 // out of the lookup kernels' loops and their register allocation grows by ~10-20 VGPRs for paths that run only in
 // pathological cases (k_sigma_tw; k_sigma_tc keeps them inline: there the call's saved registers cost more); the
 // operations and their order are the inlined code's (tc_eval, k_sigma_tc), so the sums are bitwise the same
-__device__ __noinline__ __attribute__((optnone)) double tc_chord_sum(double Y, bool nf, bool zr, double fs,
+#ifndef PROM_TC_CS_ATTR
+#define PROM_TC_CS_ATTR __noinline__ __attribute__((optnone))
+#endif
+__device__ PROM_TC_CS_ATTR double tc_chord_sum(double Y, bool nf, bool zr, double fs,
                                                                     const int32_t* __restrict__ fl,
                                                                     const double* __restrict__ nc,
                                                                     const double* __restrict__ fout, int32_t n_pr) {

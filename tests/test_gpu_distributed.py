@@ -27,6 +27,7 @@ def _bench(tmp, world, config, axis="wavelength", scaling=("--scaling", "strong"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--steps", "3", "--warmup", "1", "--config", config, *scaling,
+           *(() if "--strong" in scaling else ("--strong", "")),   # (the default strong legs: their own test)
            "--shard-axis", axis, "--no-cpu-baseline", "--no-projection", "--dump-R", out]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
