@@ -54,7 +54,7 @@ __device__ __forceinline__ double tc_clenshaw(double q, const double* __restrict
 // out of the lookup kernels' loops and their register allocation grows by ~10-20 VGPRs for paths that run only in
 // pathological cases (k_sigma_tw; k_sigma_tc keeps them inline: there the call's saved registers cost more); the
 // operations and their order are the inlined code's (tc_eval, k_sigma_tc), so the sums are bitwise the same
-#ifndef PROM_TC_CS_ATTR
+#ifndef PROM_TC_CS_ATTR   // (inlined instead, -DPROM_TC_CS_ATTR=__forceinline__: no scratch, 77 VGPRs, no faster: r06z)
 #define PROM_TC_CS_ATTR __noinline__ __attribute__((optnone))
 #endif
 __device__ PROM_TC_CS_ATTR double tc_chord_sum(double Y, bool nf, bool zr, double fs,
