@@ -102,6 +102,36 @@ __device__ __forceinline__ double tc_eval(double Y, const double* __restrict__ h
   return tf + a;
 }
 
+// fma(a, b, c) with c wave-uniform in scalar registers: one v_fma_f64 with an SGPR operand.  (Left to itself the
+// compiler copies each scalar coefficient into VGPRs -- two v_mov_b32 -- and uses v_fmac: 15 VALU for the tail
+// polynomial instead of 7, per point)
+__device__ __forceinline__ double fma_s(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+
+// tc_eval_full with the row's header in scalar registers (h uniform): the tail polynomial by fma_s, the rest as
+// tc_eval_full (the same operations in the same order: bitwise its result)
+__device__ __forceinline__ double tc_eval_full_s(double Y, const double* __restrict__ h, const double* __restrict__ tabo) {
+  const double q = Y * h[kTcHNmax];
+  const double tf = h[kTcHTfrac];
+  if (q < kTcEps) {
+    double c5 = h[kTcHT0 + 5];
+    asm volatile("" : "+v"(c5));   // (the leading coefficient in VGPRs: one FMA may read one scalar pair)
+    double p = fma_s(c5, q, h[kTcHT0 + 4]);
+#pragma unroll
+    for (int e = 3; e >= 0; --e) p = fma_s(p, q, h[kTcHT0 + e]);
+    return tf + p;
+  }
+  const int32_t nact = (int32_t)h[kTcHNact];
+  if (!(q == q)) return nact > 0 ? q : tf;
+  const int32_t L = (int32_t)h[kTcHL];
+  const int32_t j = q <= 1.0e300 ? tc_exponent(q) - kTcExpEps : 0x7fffffff;
+  if (j >= L) return tf;
+  return tf + tc_clenshaw(q, tabo + (int64_t)j * kTcD);
+}
+
 // tc_eval for a phase whose table covers every q it can reach (curve header flag 4 clear: not truncated at the
 // host's octave cap), so the exact per-point sum beyond the table never runs
 __device__ __forceinline__ double tc_eval_full(double Y, const double* __restrict__ h, const double* __restrict__ tabo) {

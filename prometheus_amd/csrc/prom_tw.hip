@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(kBlock) k_sigma_tw(const SigTabs4 tabv, const 
       }
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
-        const double v = tc_eval_full(acc[p], rs[p].h, rs[p].tabo);
+        const double v = tc_eval_full_s(acc[p], rs[p].h, rs[p].tabo);
         if (c0[p] + lane < rs[p].w1) rs[p].Rrow[c0[p]] = v;
       }
     };
