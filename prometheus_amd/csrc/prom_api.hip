@@ -943,8 +943,16 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         if (std::getenv("PROM_DEBUG")) {
           int64_t k[4] = {0, 0, 0, 0};
           for (const auto& e : twseg) k[e.kind & 3] += 1;
+          int64_t lam_st = 0, lam_n = 0;   // windows whose wavelengths are staged; their wavelengths
+          for (int32_t b = 0; b < nw; ++b)
+            if (twlam[2 * b + 1] > twlam[2 * b]) {
+              ++lam_st;
+              lam_n += twlam[2 * b + 1] - twlam[2 * b];
+            }
           std::fprintf(stderr, "[prom] target windows: %d (slices: %lld staged, %lld global, %lld staged unguessed, "
-                       "%lld outside the table)\n", nw, (long long)k[1], (long long)k[2], (long long)k[3], (long long)k[0]);
+                       "%lld outside the table; wavelengths staged in %lld windows, %.1f per window)\n", nw,
+                       (long long)k[1], (long long)k[2], (long long)k[3], (long long)k[0], (long long)lam_st,
+                       lam_st ? (double)lam_n / (double)lam_st : 0.0);
         }
       };
       if (seg_reuse) {
