@@ -615,6 +615,12 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
       tr.species_merge_ok = !(m && std::atoi(m) == 0);   // narrowed below
       const char* tc = std::getenv("PROM_TCURVE");
       tr.tcurve = !(tc && std::atoi(tc) == 0);            // narrowed below
+      // the per-run switches of the windowed path, read here rather than in every prom_transit_run (getenv scans
+      // the environment: ~1 us a call on the GPU box's hosts, against ~8.5 us for a run's three launches)
+      const char* fk = std::getenv("PROM_SIGMA_FORK");
+      tr.env_fork = fk ? (std::atoi(fk) != 0 ? 1 : 0) : -1;
+      const char* sgs = std::getenv("PROM_SIG_STAGGER");
+      tr.env_stagger = sgs && std::atoi(sgs) != 0;
     }
     PROM_REQUIRE(pb->n_pr < (1 << 24), "transit: n_pr must be < 2^24");
     tr.terms.clear();
@@ -1424,15 +1430,13 @@ int32_t prom_transit_run(prom_ctx* ctx, prom_transit_stats* stats) {
     // one run (sigma rows beside k_columns8 / k_order) but costs pipelined throughput (C4 7.3e10 -> 3.8e10
     // pts/s, C3 unchanged: profiles/r02w_pipeline_sweep.txt), so it is the default for unpipelined
     // problems only; PROM_SIGMA_FORK=0/1 forces it off/on
-    const char* fk = std::getenv("PROM_SIGMA_FORK");
-    const bool fork_ok = tr.depth <= prom::kMaxSlots / 2 && (fk ? std::atoi(fk) != 0 : tr.depth == 1);
+    const bool fork_ok = tr.depth <= prom::kMaxSlots / 2 && (tr.env_fork >= 0 ? tr.env_fork != 0 : tr.depth == 1);
     rs.aux = fork_ok ? ctx->streams[si + tr.depth] : nullptr;
     rs.ev_fork = fork_ok ? ctx->fork_ev[si] : nullptr;
     rs.ev_join = fork_ok ? ctx->join_ev[si] : nullptr;
     // staggered kernel order on alternate slots (PROM_SIG_STAGGER=1): odd slots queue the Doppler sigma
     // rows after k_order, so their latency-bound ordering overlaps the even slots' full-chip kernels
-    const char* sg = std::getenv("PROM_SIG_STAGGER");
-    rs.sig_late = tr.depth > 1 && (si & 1) && sg && std::atoi(sg) != 0;
+    rs.sig_late = tr.depth > 1 && (si & 1) && tr.env_stagger;
     if (stats) PROM_HIP(hipMemsetAsync(rs.evals.p, 0, sizeof(unsigned long long) * 64, st));
     if (!stats && !timed && tr.graphs && tr.depth > 1) {
       // untimed fast-path run: replay the slot's graph (captured here the first time)

@@ -405,6 +405,8 @@ struct TransitDev {
   // and replayed (one host call instead of three launches; slower on ROCm 7.2, so off by default)
   hipGraphExec_t gexec[kMaxSlots] = {};
   bool graphs = false;
+  int8_t env_fork = -1;       // PROM_SIGMA_FORK at prom_transit_set (-1: unset)
+  bool env_stagger = false;   // PROM_SIG_STAGGER at prom_transit_set
   int depth = 1;                            // slots in use: fast path = pipeline depth, else 1
   int cu_count = 0;                         // the context device's compute units (launch_tau_mol; 0: not queried yet)
   int last = 0;                             // slot of the most recent run
