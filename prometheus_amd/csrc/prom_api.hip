@@ -923,7 +923,11 @@ int32_t prom_transit_set(prom_ctx* ctx, const prom_transit_problem* pb) {
         // cap scales with the rows: a window's wavelengths span its rows' Doppler spread (C4x10: ~600) on top of a row's
         // own, so many-phase windows of 64 wavelengths a row spend most of their staging there -- C4x10p128 1.07 ms per
         // step at 8,192 points, 0.67 ms at 32,768 (128 rows x 256), C4x10p64 0.40 / 0.34 ms (profiles/r06w_*)
-        static const int rowcap = [] { const char* e = std::getenv("PROM_TW_ROWCAP"); return e ? std::max(1, std::atoi(e)) : 256; }();
+        // wavelengths per row: 256, and up to 768 for few rows (a window's staging then serves more points): C4x10
+        // (8 rows) 0.0605-0.0613 ms per step at 256, 0.0563-0.0575 at 512, 0.0544 at 768; C4 0.0118 / 0.0111-0.0113;
+        // C4x10p64 (64 rows) 0.343 at 256, 0.366 at 512; C3 unchanged (its windows end at the LDS budget)
+        static const int rowcap_env = [] { const char* e = std::getenv("PROM_TW_ROWCAP"); return e ? std::max(1, std::atoi(e)) : 0; }();
+        const int rowcap = rowcap_env > 0 ? rowcap_env : std::max(256, std::min(768, (int)(4096 / std::max<int64_t>(1, n_orb)) / 64 * 64));
         static const int64_t pmax_env = [] { const char* e = std::getenv("PROM_TW_PMAX"); return e ? (int64_t)std::max(1, std::atoi(e)) : (int64_t)0; }();
         const int64_t pmax = pmax_env > 0 ? pmax_env : std::max<int64_t>(8192, (int64_t)rowcap * n_orb);
         static const int lamcap = [] {   // (wavelengths staged per window at most; 0: never)
