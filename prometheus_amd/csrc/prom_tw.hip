@@ -3,7 +3,7 @@
 
 namespace prom {
 
-// ---- sigma lookups + transmission curves over target windows (one species with orbital Doppler shift) ----
+// ---- sigma lookups + transmission curves over target windows (the default with orbital Doppler shift) ----
 // The targets t = shift_o lambda_w of all rows, not the wavelengths, are cut into windows (host: prom_window.hip):
 // window b holds, per row o, the contiguous wavelengths w in [W[b][o], W[b+1][o]) whose targets fall in the
 // window's target interval (at most a few hundred per row).  Per species the table nodes those targets reach are
