@@ -89,7 +89,13 @@ constexpr int kSigSeg = PROM_SIG_SEG;
 // wavelengths at 0.001 A under a 0.6 A Doppler spread) stay in LDS instead of the global-record front path.  Host
 // segments mark slices within the cap SigSeg kind & 64.
 constexpr int tc_slice_cap(int nsig) { return nsig <= 1 ? 1024 : (nsig == 2 ? 640 : kSigSeg); }
-constexpr int kTwLds = 2560;      // k_sigma_tw: LDS doubles per workgroup (20 KB): staged nodes (3 each) + wavelengths
+#ifndef PROM_TW_LDSD
+#define PROM_TW_LDSD 2816   // (build macro for A/B builds; 7 workgroups per CU fit up to 2,861 -- the SGPRs allow 7 waves)
+#endif
+// k_sigma_tw: LDS doubles per workgroup (22 KB): staged nodes (3 each) + wavelengths.  2,816 against 2,560: the C3
+// windows stage their wavelengths in 1,830 of 1,859 windows instead of 513 of 1,863, C3 0.0371 -> 0.0364-0.0367 ms,
+// C4x10 0.0570-0.0577 -> 0.0559-0.0570 ms per step on one box (profiles/r06_tw_ab_sessions.txt, r06q2)
+constexpr int kTwLds = PROM_TW_LDSD;
 constexpr int kTwLamCap = 1024;   // ... wavelengths staged per window at most
 constexpr int kSigBlockW = 256;   // wavelengths per resampling workgroup (== kBlock)
 #ifndef PROM_SIG_ROWS

@@ -11,7 +11,7 @@ namespace prom {
 // and no second workgroup staging the same slice for other rows.  The wavelengths the rows read, [lw0, lw1), are
 // staged with them: the item loop then issues no vector load, only its stores (on gfx9 a load's vmcnt wait also
 // waits for every earlier store: a global wavelength load per item cost each item a store round trip).  Slices and
-// wavelengths share kTwLds doubles of LDS (20 KB: 24 bytes a node, 8 a wavelength), carved per window by the host.
+// wavelengths share kTwLds doubles of LDS (22 KB: 24 bytes a node, 8 a wavelength), carved per window by the host.
 // Work items are (row, 64 wavelengths) with the row wave-uniform: its Doppler factor, curve header and coefficients
 // are scalar loads.  Per species slice (SigSeg kind & 3): 1 staged, with the host-verified linear guess (one LDS
 // round: x_g, x_{g+1} and the record; a second only for lanes one node off); 3 staged without a guess (a slice
